@@ -1,0 +1,45 @@
+/*
+ * ggml_mi355x.h — exported entry points of libggml-mi355x.so, the MI355X-native
+ * ggml backend. The reference loads it unmodified through its dynamic-backend
+ * loader; each symbol names the reference interface it stands in for.
+ */
+#pragma once
+
+#include "ggml_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Dynamic-backend entry point looked up with dlsym by load_backend()
+ * (ggml/src/ggml-backend-reg.cpp:194-238; typedef ggml_backend_init_t,
+ * ggml/src/ggml-backend-impl.h:222). Returns the registry; api_version == 2. */
+ggml_backend_reg_t ggml_backend_init(void);
+
+/* Optional score (ggml_backend_score_t, ggml-backend-impl.h:225): 0 when no
+ * HIP device is visible, so the loader skips the library (reg.cpp:207-213). */
+int ggml_backend_score(void);
+
+/* Static registration form of the above, the counterpart of
+ * ggml_backend_cuda_reg() (ggml/include/ggml-cuda.h, ggml-cuda.cu:5043). */
+ggml_backend_reg_t ggml_backend_mi355x_reg(void);
+
+/* Direct stream creation, counterpart of ggml_backend_cuda_init(int device)
+ * (ggml-cuda.cu:5100). */
+ggml_backend_t ggml_backend_mi355x_init(int device);
+
+/* ggml_backend_cuda_get_device_count() counterpart. */
+int ggml_backend_mi355x_get_device_count(void);
+
+/* ggml_backend_is_cuda() counterpart. */
+bool ggml_backend_is_mi355x(ggml_backend_t backend);
+
+/* ggml_backend_cuda_buffer_type(int device) counterpart. */
+ggml_backend_buffer_type_t ggml_backend_mi355x_buffer_type(int device);
+
+/* Executor counters: [graph_compute calls, HIP-graph replays, nodes run, nodes fused]. */
+void ggml_backend_mi355x_stats(ggml_backend_t backend, uint64_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif

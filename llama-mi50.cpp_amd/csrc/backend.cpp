@@ -1,0 +1,408 @@
+// backend.cpp — the MI355X ggml backend object model behind the reference's
+// backend C-ABI (ggml/src/ggml-backend-impl.h:17-251): registry, devices,
+// device/pinned buffer types, buffers, streams and events.
+//
+// Behavioural spec followed (the reference CUDA/HIP backend, replaced not ported):
+//   registry/device enumeration  ggml-cuda.cu:5024-5075
+//   buffer set/get/cpy           ggml-cuda.cu:600-700
+//   async copies + events        ggml-cuda.cu:2760-2860
+//   offload_op batch threshold   ggml-cuda.cu:4872-4891
+#include "backend.h"
+#include "ggml_mi355x.h"
+
+#include <cstdarg>
+#include <mutex>
+#include <memory>
+
+namespace mx {
+
+void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status);  // exec.cpp
+
+static std::vector<std::unique_ptr<Device>> g_devices;
+static ggml_backend_reg g_reg{};
+static std::once_flag g_once;
+
+static const uint8_t kGuid[16] = {0x6d, 0x69, 0x33, 0x35, 0x35, 0x78, 0x2d, 0x67,
+                                  0x66, 0x78, 0x39, 0x35, 0x30, 0x2d, 0x76, 0x31};
+
+static Device * dev_ctx(ggml_backend_dev_t d) { return (Device *) d->context; }
+
+// ---------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------
+static void buf_free(ggml_backend_buffer_t b) {
+    BufferCtx * c = (BufferCtx *) b->context;
+    if (c->base) { hipSetDevice(c->device); hipFree(c->base); }
+    delete c;
+}
+static void * buf_base(ggml_backend_buffer_t b) { return ((BufferCtx *) b->context)->base; }
+static ggml_status buf_init_tensor(ggml_backend_buffer_t, ggml_tensor *) { return GGML_STATUS_SUCCESS; }
+
+static void buf_memset(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size_t off, size_t size) {
+    BufferCtx * c = (BufferCtx *) b->context;
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipMemsetAsync((char *) t->data + off, v, size, hipStreamPerThread));
+    HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
+}
+static void buf_set(ggml_backend_buffer_t b, ggml_tensor * t, const void * data, size_t off, size_t size) {
+    BufferCtx * c = (BufferCtx *) b->context;
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipMemcpyAsync((char *) t->data + off, data, size, hipMemcpyHostToDevice, hipStreamPerThread));
+    HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
+}
+static void buf_get(ggml_backend_buffer_t b, const ggml_tensor * t, void * data, size_t off, size_t size) {
+    BufferCtx * c = (BufferCtx *) b->context;
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipMemcpyAsync(data, (const char *) t->data + off, size, hipMemcpyDeviceToHost, hipStreamPerThread));
+    HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
+}
+static bool buf_is_ours(ggml_backend_buffer_t b);
+static bool buf_cpy(ggml_backend_buffer_t b, const ggml_tensor * src, ggml_tensor * dst) {
+    if (!src->buffer || !buf_is_ours(src->buffer)) return false;
+    BufferCtx * sc = (BufferCtx *) src->buffer->context;
+    BufferCtx * dc = (BufferCtx *) b->context;
+    const size_t n = mx_nbytes(src);
+    HIP_CHECK(hipSetDevice(dc->device));
+    if (sc->device == dc->device) {
+        HIP_CHECK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, hipStreamPerThread));
+    } else {
+        HIP_CHECK(hipMemcpyPeerAsync(dst->data, dc->device, src->data, sc->device, n, hipStreamPerThread));
+    }
+    HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
+    return true;
+}
+static void buf_clear(ggml_backend_buffer_t b, uint8_t v) {
+    BufferCtx * c = (BufferCtx *) b->context;
+    HIP_CHECK(hipSetDevice(c->device));
+    HIP_CHECK(hipMemsetAsync(c->base, v, c->size, hipStreamPerThread));
+    HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
+}
+
+static const ggml_backend_buffer_i kBufIface = {
+    buf_free, buf_base, buf_init_tensor, buf_memset, buf_set, buf_get, buf_cpy, buf_clear, nullptr,
+};
+static bool buf_is_ours(ggml_backend_buffer_t b) { return b->iface.get_base == buf_base; }
+
+static const char * buft_name(ggml_backend_buffer_type_t t) { return dev_ctx(t->device)->name.c_str(); }
+static ggml_backend_buffer_t buft_alloc(ggml_backend_buffer_type_t t, size_t size) {
+    Device * d = dev_ctx(t->device);
+    HIP_CHECK(hipSetDevice(d->id));
+    void * p = nullptr;
+    size = std::max<size_t>(size, 1);
+    if (hipMalloc(&p, size) != hipSuccess) {
+        (void) hipGetLastError();
+        fprintf(stderr, "%s: failed to allocate %.2f MiB on %s\n", __func__, size / 1048576.0, d->name.c_str());
+        return nullptr;
+    }
+    BufferCtx * c = new BufferCtx{d->id, p, size, d->name};
+    // ggml_backend_buffer_free (ggml-backend.cpp) releases the struct with delete
+    return new ggml_backend_buffer{kBufIface, t, c, size, GGML_BACKEND_BUFFER_USAGE_ANY};
+}
+static size_t buft_align(ggml_backend_buffer_type_t) { return 256; }
+static size_t buft_max(ggml_backend_buffer_type_t) { return SIZE_MAX; }
+// Tail padding of quantised tensors: 16 bytes lets vector loads run past the last
+// block of the last row without faulting (the kernels mask the values).
+static size_t buft_alloc_size(ggml_backend_buffer_type_t, const ggml_tensor * t) {
+    size_t n = mx_nbytes(t);
+    if (mx_type(t->type).quant) n += 64;
+    return n;
+}
+static bool buft_is_host(ggml_backend_buffer_type_t) { return false; }
+
+static const ggml_backend_buffer_type_i kBuftIface = {
+    buft_name, buft_alloc, buft_align, buft_max, buft_alloc_size, buft_is_host,
+};
+
+// ---------------------------------------------------------------------------
+// pinned host buffers (get_host_buffer_type; ggml-cuda.cu:1120-1190 behaviour)
+// ---------------------------------------------------------------------------
+static void hbuf_free(ggml_backend_buffer_t b) { HIP_CHECK(hipHostFree(b->context)); }
+static void * hbuf_base(ggml_backend_buffer_t b) { return b->context; }
+static void hbuf_memset(ggml_backend_buffer_t, ggml_tensor * t, uint8_t v, size_t off, size_t size) { memset((char *) t->data + off, v, size); }
+static void hbuf_set(ggml_backend_buffer_t, ggml_tensor * t, const void * d, size_t off, size_t size) { memcpy((char *) t->data + off, d, size); }
+static void hbuf_get(ggml_backend_buffer_t, const ggml_tensor * t, void * d, size_t off, size_t size) { memcpy(d, (const char *) t->data + off, size); }
+static bool hbuf_cpy(ggml_backend_buffer_t, const ggml_tensor * src, ggml_tensor * dst) {
+    if (src->buffer && src->buffer->buft->iface.is_host && src->buffer->buft->iface.is_host(src->buffer->buft)) {
+        memcpy(dst->data, src->data, mx_nbytes(src));
+        return true;
+    }
+    return false;
+}
+static void hbuf_clear(ggml_backend_buffer_t b, uint8_t v) { memset(b->context, v, b->size); }
+static const ggml_backend_buffer_i kHostBufIface = {
+    hbuf_free, hbuf_base, nullptr, hbuf_memset, hbuf_set, hbuf_get, hbuf_cpy, hbuf_clear, nullptr,
+};
+static const char * hbuft_name(ggml_backend_buffer_type_t) { return "MI355X_Host"; }
+static ggml_backend_buffer_t hbuft_alloc(ggml_backend_buffer_type_t t, size_t size) {
+    void * p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(size, 1), hipHostMallocPortable) != hipSuccess) {
+        (void) hipGetLastError();
+        return nullptr;
+    }
+    return new ggml_backend_buffer{kHostBufIface, t, p, size, GGML_BACKEND_BUFFER_USAGE_ANY};
+}
+static size_t hbuft_align(ggml_backend_buffer_type_t) { return 64; }
+static bool hbuft_is_host(ggml_backend_buffer_type_t) { return true; }
+static const ggml_backend_buffer_type_i kHostBuftIface = {
+    hbuft_name, hbuft_alloc, hbuft_align, nullptr, nullptr, hbuft_is_host,
+};
+
+// ---------------------------------------------------------------------------
+// backend (stream)
+// ---------------------------------------------------------------------------
+Stream * stream_of(ggml_backend_t b) { return (Stream *) b->context; }
+
+static const char * be_name(ggml_backend_t b) { return stream_of(b)->name.c_str(); }
+static void be_free(ggml_backend_t b) {
+    Stream * s = stream_of(b);
+    hipSetDevice(s->device);
+    hipStreamSynchronize(s->stream);
+    if (s->gcache.exec) hipGraphExecDestroy(s->gcache.exec);
+    if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
+    if (s->scratch.base) hipFree(s->scratch.base);
+    hipStreamDestroy(s->stream);
+    delete s;  // the ggml_backend struct lives inside Stream
+}
+static void be_set_async(ggml_backend_t b, ggml_tensor * t, const void * data, size_t off, size_t size) {
+    Stream * s = stream_of(b);
+    HIP_CHECK(hipSetDevice(s->device));
+    HIP_CHECK(hipMemcpyAsync((char *) t->data + off, data, size, hipMemcpyHostToDevice, s->stream));
+}
+static void be_get_async(ggml_backend_t b, const ggml_tensor * t, void * data, size_t off, size_t size) {
+    Stream * s = stream_of(b);
+    HIP_CHECK(hipSetDevice(s->device));
+    HIP_CHECK(hipMemcpyAsync(data, (const char *) t->data + off, size, hipMemcpyDeviceToHost, s->stream));
+}
+static bool is_our_backend(ggml_backend_t b);
+// Layer-split hand-off (ggml-backend.cpp:1568 → reference ggml-cuda.cu:2799-2852):
+// peer copy on the source stream over xGMI, ordered for the destination by an event.
+static bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const ggml_tensor * src, ggml_tensor * dst) {
+    if (!is_our_backend(bsrc) || !is_our_backend(bdst)) return false;
+    if (!src->buffer || !dst->buffer || !buf_is_ours(src->buffer) || !buf_is_ours(dst->buffer)) return false;
+    Stream * ss = stream_of(bsrc);
+    Stream * ds = stream_of(bdst);
+    const size_t n = mx_nbytes(dst);
+    HIP_CHECK(hipSetDevice(ss->device));
+    if (ss->device == ds->device) {
+        HIP_CHECK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, ss->stream));
+    } else {
+        HIP_CHECK(hipMemcpyPeerAsync(dst->data, ds->device, src->data, ss->device, n, ss->stream));
+    }
+    if (ss != ds) {
+        hipEvent_t ev;
+        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(ev, ss->stream));
+        HIP_CHECK(hipSetDevice(ds->device));
+        HIP_CHECK(hipStreamWaitEvent(ds->stream, ev, 0));
+        HIP_CHECK(hipEventDestroy(ev));  // destruction is deferred until the event completes
+    }
+    return true;
+}
+static void be_sync(ggml_backend_t b) {
+    Stream * s = stream_of(b);
+    HIP_CHECK(hipSetDevice(s->device));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+}
+static ggml_status be_graph_compute(ggml_backend_t b, ggml_cgraph * g) {
+    Stream * s = stream_of(b);
+    ggml_status st = GGML_STATUS_SUCCESS;
+    graph_compute_impl(s, g, &st);
+    return st;
+}
+static void be_event_record(ggml_backend_t b, ggml_backend_event_t e) {
+    Stream * s = stream_of(b);
+    HIP_CHECK(hipSetDevice(s->device));
+    HIP_CHECK(hipEventRecord((hipEvent_t) e->context, s->stream));
+}
+static void be_event_wait(ggml_backend_t b, ggml_backend_event_t e) {
+    Stream * s = stream_of(b);
+    HIP_CHECK(hipSetDevice(s->device));
+    HIP_CHECK(hipStreamWaitEvent(s->stream, (hipEvent_t) e->context, 0));
+}
+
+static const ggml_backend_i kBackendIface = {
+    be_name, be_free, be_set_async, be_get_async, be_cpy_async, be_sync,
+    nullptr, nullptr, nullptr, nullptr,
+    be_graph_compute, be_event_record, be_event_wait, nullptr,
+};
+static bool is_our_backend(ggml_backend_t b) { return b && b->iface.graph_compute == be_graph_compute; }
+
+static bool env_flag(const char * name) { const char * v = getenv(name); return v && *v && strcmp(v, "0") != 0; }
+
+static ggml_backend_t make_backend(Device * d) {
+    HIP_CHECK(hipSetDevice(d->id));
+    Stream * s = new Stream();
+    s->device = d->id;
+    s->name = d->name;
+    HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    s->use_graphs = !env_flag("GGML_MI355X_DISABLE_GRAPHS");
+    s->use_fusion = !env_flag("GGML_MI355X_DISABLE_FUSION");
+    s->backend.guid = (ggml_guid_t) kGuid;
+    s->backend.iface = kBackendIface;
+    s->backend.device = &d->dev;
+    s->backend.context = s;
+    return &s->backend;
+}
+
+// ---------------------------------------------------------------------------
+// device
+// ---------------------------------------------------------------------------
+static const char * dv_name(ggml_backend_dev_t d) { return dev_ctx(d)->name.c_str(); }
+static const char * dv_desc(ggml_backend_dev_t d) { return dev_ctx(d)->description.c_str(); }
+static void dv_memory(ggml_backend_dev_t d, size_t * free, size_t * total) {
+    HIP_CHECK(hipSetDevice(dev_ctx(d)->id));
+    HIP_CHECK(hipMemGetInfo(free, total));
+}
+static ggml_backend_dev_type dv_type(ggml_backend_dev_t) { return GGML_BACKEND_DEVICE_TYPE_GPU; }
+static void dv_props(ggml_backend_dev_t d, ggml_backend_dev_props * p) {
+    p->name = dv_name(d);
+    p->description = dv_desc(d);
+    p->type = GGML_BACKEND_DEVICE_TYPE_GPU;
+    p->device_id = dev_ctx(d)->pci_bus_id.c_str();
+    dv_memory(d, &p->memory_free, &p->memory_total);
+    p->caps.async = true;
+    p->caps.host_buffer = !env_flag("GGML_MI355X_NO_PINNED");
+    p->caps.buffer_from_host_ptr = false;
+    p->caps.events = true;
+}
+static ggml_backend_t dv_init(ggml_backend_dev_t d, const char *) { return make_backend(dev_ctx(d)); }
+static ggml_backend_buffer_type_t dv_buft(ggml_backend_dev_t d) { return &dev_ctx(d)->buft; }
+static ggml_backend_buffer_type_t dv_host_buft(ggml_backend_dev_t d) { return &dev_ctx(d)->host_buft; }
+static bool dv_supports_op(ggml_backend_dev_t, const ggml_tensor * op) { return supports_op(op); }
+static bool dv_supports_buft(ggml_backend_dev_t d, ggml_backend_buffer_type_t t) {
+    return t->iface.alloc_buffer == buft_alloc && t->device == d;
+}
+static int64_t op_batch(const ggml_tensor * op) {
+    switch (op->op) {
+        case GGML_OP_GET_ROWS: return 0;
+        case GGML_OP_MUL_MAT: return op->ne[1];
+        case GGML_OP_MUL_MAT_ID: case GGML_OP_ROPE: case GGML_OP_ROPE_BACK: return op->ne[2];
+        default: return mx_nrows(op);
+    }
+}
+static bool dv_offload_op(ggml_backend_dev_t, const ggml_tensor * op) {
+    static const int64_t min_batch = [] { const char * v = getenv("GGML_OP_OFFLOAD_MIN_BATCH"); return v ? atoll(v) : 32LL; }();
+    return op_batch(op) >= min_batch;
+}
+static ggml_backend_event_t dv_event_new(ggml_backend_dev_t d) {
+    HIP_CHECK(hipSetDevice(dev_ctx(d)->id));
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return new ggml_backend_event{d, e};
+}
+static void dv_event_free(ggml_backend_dev_t, ggml_backend_event_t e) {
+    hipEventDestroy((hipEvent_t) e->context);
+    delete e;
+}
+static void dv_event_sync(ggml_backend_dev_t, ggml_backend_event_t e) { HIP_CHECK(hipEventSynchronize((hipEvent_t) e->context)); }
+
+static const ggml_backend_device_i kDevIface = {
+    dv_name, dv_desc, dv_memory, dv_type, dv_props, dv_init, dv_buft, dv_host_buft, nullptr,
+    dv_supports_op, dv_supports_buft, dv_offload_op, dv_event_new, dv_event_free, dv_event_sync,
+};
+
+// ---------------------------------------------------------------------------
+// registry
+// ---------------------------------------------------------------------------
+static const char * rg_name(ggml_backend_reg_t) { return "MI355X"; }
+static size_t rg_count(ggml_backend_reg_t) { return g_devices.size(); }
+static ggml_backend_dev_t rg_get(ggml_backend_reg_t, size_t i) { return i < g_devices.size() ? &g_devices[i]->dev : nullptr; }
+
+static ggml_backend_feature * rg_features(ggml_backend_reg_t) {
+    static ggml_backend_feature f[] = {
+        {"ARCH", "gfx950"}, {"WAVE", "64"}, {"MFMA", "f16,bf16,i8"}, {"HIP_GRAPHS", "1"}, {nullptr, nullptr},
+    };
+    return f;
+}
+static void rg_set_abort(ggml_backend_t b, ggml_abort_callback cb, void * data) {
+    if (!is_our_backend(b)) return;
+    stream_of(b)->abort_cb = cb;
+    stream_of(b)->abort_data = data;
+}
+static void * rg_proc(ggml_backend_reg_t, const char * name) {
+    if (strcmp(name, "ggml_backend_get_features") == 0) return (void *) rg_features;
+    if (strcmp(name, "ggml_backend_set_abort_callback") == 0) return (void *) rg_set_abort;
+    return nullptr;
+}
+
+static const ggml_backend_reg_i kRegIface = { rg_name, rg_count, rg_get, rg_proc };
+
+static void init_registry() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void) hipGetLastError(); n = 0; }
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
+        auto d = std::make_unique<Device>();
+        d->id = i;
+        d->name = "MI355X" + std::to_string(i);
+        d->description = std::string(p.name[0] ? p.name : "AMD Instinct MI355X") + " (" + p.gcnArchName + ")";
+        d->total_mem = p.totalGlobalMem;
+        d->n_cu = p.multiProcessorCount;
+        char pci[32] = {0};
+        if (hipDeviceGetPCIBusId(pci, sizeof(pci), i) == hipSuccess) d->pci_bus_id = pci;
+        for (auto & ch : d->pci_bus_id) ch = (char) tolower(ch);
+        d->dev = ggml_backend_device{kDevIface, &g_reg, d.get()};
+        d->buft = ggml_backend_buffer_type{kBuftIface, &d->dev, d.get()};
+        d->host_buft = ggml_backend_buffer_type{kHostBuftIface, &d->dev, d.get()};
+        g_devices.push_back(std::move(d));
+    }
+    g_reg.api_version = GGML_BACKEND_API_VERSION;
+    g_reg.iface = kRegIface;
+    g_reg.context = nullptr;
+}
+
+}  // namespace mx
+
+void mx_abort(const char * file, int line, const char * fmt, ...) {
+    fprintf(stderr, "[mi355x] %s:%d: ", file, line);
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(stderr, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "\n");
+    fflush(stderr);
+    abort();
+}
+
+extern "C" {
+
+ggml_backend_reg_t ggml_backend_mi355x_reg(void) {
+    std::call_once(mx::g_once, mx::init_registry);
+    return &mx::g_reg;
+}
+
+ggml_backend_reg_t ggml_backend_init(void) { return ggml_backend_mi355x_reg(); }
+
+int ggml_backend_score(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void) hipGetLastError(); return 0; }
+    return n > 0 ? 200 : 0;
+}
+
+ggml_backend_t ggml_backend_mi355x_init(int device) {
+    ggml_backend_reg_t r = ggml_backend_mi355x_reg();
+    if (device < 0 || (size_t) device >= mx::g_devices.size()) return nullptr;
+    return mx::make_backend(mx::g_devices[device].get());
+    (void) r;
+}
+
+int ggml_backend_mi355x_get_device_count(void) {
+    ggml_backend_mi355x_reg();
+    return (int) mx::g_devices.size();
+}
+
+bool ggml_backend_is_mi355x(ggml_backend_t b) { return mx::is_our_backend(b); }
+
+ggml_backend_buffer_type_t ggml_backend_mi355x_buffer_type(int device) {
+    ggml_backend_mi355x_reg();
+    if (device < 0 || (size_t) device >= mx::g_devices.size()) return nullptr;
+    return &mx::g_devices[device]->buft;
+}
+
+void ggml_backend_mi355x_stats(ggml_backend_t b, uint64_t out[4]) {
+    mx::Stream * s = mx::stream_of(b);
+    out[0] = s->n_graph_compute; out[1] = s->n_graph_replay; out[2] = s->n_nodes_run; out[3] = s->n_fused;
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+// common.h — shared host/device helpers for the MI355X ggml backend.
+//
+// Host side: ggml type traits and tensor-geometry helpers re-stated from the
+// semantics of ggml/src/ggml.c (ggml_nbytes, ggml_row_size, ggml_is_contiguous*,
+// type_traits table) so the backend needs nothing from libggml-base at run time.
+// Device side: wave64 reductions, fp16 helpers, HIP error handling.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "ggml_abi.h"
+
+#define MX_WAVE 64
+
+[[noreturn]] void mx_abort(const char * file, int line, const char * fmt, ...);
+#define MX_ABORT(...) mx_abort(__FILE__, __LINE__, __VA_ARGS__)
+#define MX_ASSERT(x) do { if (!(x)) MX_ABORT("assert failed: %s", #x); } while (0)
+#define HIP_CHECK(call) do { hipError_t err_ = (call); if (err_ != hipSuccess) \
+    MX_ABORT("HIP error %d (%s) in %s", (int) err_, hipGetErrorString(err_), #call); } while (0)
+
+// ---------------------------------------------------------------------------
+// ggml type traits (ggml.c type_traits[]: blck_size, type_size)
+// ---------------------------------------------------------------------------
+struct mx_type_info { int blck; int size; bool quant; const char * name; };
+
+static inline mx_type_info mx_type(int t) {
+    switch (t) {
+        case GGML_TYPE_F32:  return {1, 4, false, "f32"};
+        case GGML_TYPE_F16:  return {1, 2, false, "f16"};
+        case GGML_TYPE_BF16: return {1, 2, false, "bf16"};
+        case GGML_TYPE_F64:  return {1, 8, false, "f64"};
+        case GGML_TYPE_I8:   return {1, 1, false, "i8"};
+        case GGML_TYPE_I16:  return {1, 2, false, "i16"};
+        case GGML_TYPE_I32:  return {1, 4, false, "i32"};
+        case GGML_TYPE_I64:  return {1, 8, false, "i64"};
+        case GGML_TYPE_Q4_0: return {32, 18, true, "q4_0"};
+        case GGML_TYPE_Q4_1: return {32, 20, true, "q4_1"};
+        case GGML_TYPE_Q5_0: return {32, 22, true, "q5_0"};
+        case GGML_TYPE_Q5_1: return {32, 24, true, "q5_1"};
+        case GGML_TYPE_Q8_0: return {32, 34, true, "q8_0"};
+        case GGML_TYPE_Q8_1: return {32, 36, true, "q8_1"};
+        case GGML_TYPE_Q2_K: return {256, 84, true, "q2_K"};
+        case GGML_TYPE_Q3_K: return {256, 110, true, "q3_K"};
+        case GGML_TYPE_Q4_K: return {256, 144, true, "q4_K"};
+        case GGML_TYPE_Q5_K: return {256, 176, true, "q5_K"};
+        case GGML_TYPE_Q6_K: return {256, 210, true, "q6_K"};
+        case GGML_TYPE_Q8_K: return {256, 292, true, "q8_K"};
+        default:             return {0, 0, false, "?"};
+    }
+}
+
+static inline size_t mx_row_size(int type, int64_t ne) {
+    mx_type_info ti = mx_type(type);
+    return (size_t) (ti.size * (ne / ti.blck));
+}
+
+// ggml_nbytes (ggml.c): extent of the tensor in memory, honouring strides.
+static inline size_t mx_nbytes(const ggml_tensor * t) {
+    for (int i = 0; i < GGML_MAX_DIMS; ++i) if (t->ne[i] <= 0) return 0;
+    mx_type_info ti = mx_type(t->type);
+    size_t n;
+    if (ti.blck == 1) {
+        n = ti.size;
+        for (int i = 0; i < GGML_MAX_DIMS; ++i) n += (t->ne[i] - 1) * t->nb[i];
+    } else {
+        n = t->ne[0] * t->nb[0] / ti.blck;
+        for (int i = 1; i < GGML_MAX_DIMS; ++i) n += (t->ne[i] - 1) * t->nb[i];
+    }
+    return n;
+}
+
+static inline int64_t mx_nelements(const ggml_tensor * t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
+static inline int64_t mx_nrows(const ggml_tensor * t)     { return t->ne[1] * t->ne[2] * t->ne[3]; }
+
+// ggml_is_contiguous_n: dims >= n may be non-contiguous
+static inline bool mx_is_contiguous_n(const ggml_tensor * t, int n) {
+    size_t next = mx_type(t->type).size;
+    if (t->ne[0] != mx_type(t->type).blck && t->nb[0] != next) return false;
+    next *= t->ne[0] / mx_type(t->type).blck;
+    for (int i = 1; i < GGML_MAX_DIMS; i++) {
+        if (t->ne[i] != 1) {
+            if (i > n) {
+                if (t->nb[i] != next) return false;
+                next *= t->ne[i];
+            } else {
+                next = t->ne[i] * t->nb[i];
+            }
+        }
+    }
+    return true;
+}
+static inline bool mx_is_contiguous(const ggml_tensor * t)       { return mx_is_contiguous_n(t, 0); }
+static inline bool mx_is_contiguous_rows(const ggml_tensor * t)  { return t->ne[0] == mx_type(t->type).blck || t->nb[0] == (size_t) mx_type(t->type).size; }
+static inline bool mx_are_same_shape(const ggml_tensor * a, const ggml_tensor * b) {
+    return a->ne[0] == b->ne[0] && a->ne[1] == b->ne[1] && a->ne[2] == b->ne[2] && a->ne[3] == b->ne[3];
+}
+static inline bool mx_is_empty(const ggml_tensor * t) {
+    for (int i = 0; i < GGML_MAX_DIMS; ++i) if (t->ne[i] == 0) return true;
+    return false;
+}
+static inline bool mx_is_permuted(const ggml_tensor * t) {
+    return t->nb[0] > t->nb[1] || t->nb[1] > t->nb[2] || t->nb[2] > t->nb[3];
+}
+static inline bool mx_is_transposed(const ggml_tensor * t) { return t->nb[0] > t->nb[1]; }
+
+template <typename T> static inline T mx_op_param(const ggml_tensor * t, int i) {
+    T v; memcpy(&v, (const char *) t->op_params + 4 * i, sizeof(T)); return v;
+}
+
+static inline int64_t mx_ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+#if defined(__HIPCC__)
+
+template <int W = MX_WAVE>
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+    return v;
+}
+template <int W = MX_WAVE>
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, W));
+    return v;
+}
+template <int W = MX_WAVE>
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+    return v;
+}
+
+// block-wide sum for blockDim.x multiple of 64, <= 1024; lds >= 16 floats
+__device__ __forceinline__ float block_sum(float v, float * lds) {
+    v = wave_sum(v);
+    const int nw = blockDim.x / MX_WAVE;
+    if (nw == 1) return v;
+    const int w = threadIdx.x / MX_WAVE, l = threadIdx.x % MX_WAVE;
+    __syncthreads();
+    if (l == 0) lds[w] = v;
+    __syncthreads();
+    v = (l & 15) < nw ? lds[l & 15] : 0.0f;  // every 16-lane segment holds all partials
+    return wave_sum<16>(v);
+}
+__device__ __forceinline__ float block_max(float v, float * lds) {
+    v = wave_max(v);
+    const int nw = blockDim.x / MX_WAVE;
+    if (nw == 1) return v;
+    const int w = threadIdx.x / MX_WAVE, l = threadIdx.x % MX_WAVE;
+    __syncthreads();
+    if (l == 0) lds[w] = v;
+    __syncthreads();
+    v = (l & 15) < nw ? lds[l & 15] : -INFINITY;
+    return wave_max<16>(v);
+}
+
+__device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__float2half_rn(f)); }
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t) h) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round-to-nearest-even, NaN kept (ggml_compute_fp32_to_bf16)
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffff) > 0x7f800000) return (uint16_t) ((u >> 16) | 64);
+    return (uint16_t) ((u + (0x7fff + ((u >> 16) & 1))) >> 16);
+}
+
+__device__ __forceinline__ int dot4_i8(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
+
+#endif  // __HIPCC__

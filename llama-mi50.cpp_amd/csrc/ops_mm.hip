@@ -1,0 +1,376 @@
+// ops_mm.hip — MUL_MAT dispatcher and the prefill GEMM on CDNA4 matrix cores.
+//
+// Reference: ggml_cuda_mul_mat (ggml-cuda.cu:2183-2266) chooses mmvq for
+// src1->ne[1] <= 8 and mmq (mmq.cuh:3364-3700, int8 MMA over q8_1 tiles) above.
+// MI355X design for the GEMM ("dequant-into-LDS → MFMA"):
+//   * activations are converted once to f16 rows padded to the K tile (scratch);
+//   * per 128-deep K step a 256-thread block dequantises a 128-row weight tile
+//     straight from the ggml super-blocks (16-byte qs chunks per lane) into f16 LDS,
+//     and stages a 128-token activation tile with 16-byte loads;
+//   * 4 waves (2×2) each own a 64×64 output tile = 2×2 v_mfma_f32_32x32x16_f16,
+//     A operand = tokens, B operand = weight rows, so the epilogue's 32 lanes
+//     write 32 consecutive output rows (128-byte coalesced stores);
+//   * LDS rows are 256 B; 16-byte chunks are XOR-swizzled by (row & 15) so every
+//     ds_read_b128 lane group hits 16 distinct bank slots.
+#include "backend.h"
+#include "mm.h"
+
+namespace mx {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float float16v __attribute__((ext_vector_type(16)));
+
+constexpr int MM_BT = 128;   // tokens per block
+constexpr int MM_BW = 128;   // weight rows per block
+constexpr int MM_BK = 128;   // K per step
+
+struct MmqArgs {
+    const char * w; size_t w_row, w_c2, w_c3;
+    const _Float16 * x; int64_t kp;          // activations f16 [cols][kp]
+    float * dst; size_t d_col, d_c2, d_c3;   // in floats
+    int64_t M, N, K, ne12, r2, r3;
+};
+
+// ---- f32 → f16 activation rows, zero padded to kp --------------------------
+__global__ void k_act_f16(const char * __restrict__ x, int64_t K, int64_t ne11, int64_t ne12,
+                          size_t nb10, size_t nb11, size_t nb12, size_t nb13, int64_t kp, _Float16 * __restrict__ out) {
+    const int64_t col = blockIdx.y;
+    const int64_t i11 = col % ne11, i12 = (col / ne11) % ne12, i13 = col / (ne11 * ne12);
+    const char * px = x + i11 * nb11 + i12 * nb12 + i13 * nb13;
+    for (int64_t k = blockIdx.x * (int64_t) blockDim.x + threadIdx.x; k < kp; k += (int64_t) gridDim.x * blockDim.x) {
+        out[col * kp + k] = (_Float16) (k < K ? *(const float *) (px + k * nb10) : 0.0f);
+    }
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 16 + (chunk ^ (row & 15)); }  // in 16-byte units
+
+__device__ __forceinline__ void st_h8(uint4 * lds, int row, int chunk, const float (&v)[8]) {
+    half8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (_Float16) v[i];
+    lds[swz(row, chunk)] = *(uint4 *) &h;
+}
+
+// Dequantise the weight tile [MM_BW rows][MM_BK k] starting at k0 into LDS.
+template <int QT>
+__device__ __forceinline__ void load_w_tile(const MmqArgs & p, const char * wbase, int64_t row0, int64_t k0, uint4 * lds) {
+    const int tid = threadIdx.x;
+    if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
+        // 128 rows × 4 qs chunks (half a super-block) = 512 units, 2 per thread
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const int unit = tid + 256 * it;
+            const int r = unit >> 2, c = unit & 3;
+            const int64_t row = row0 + r;
+            float lo[16], hi[16];
+            if (row < p.M) {
+                const int64_t sb = k0 >> 8;
+                const int hf = (int) ((k0 >> 7) & 1);
+                const char * b = wbase + row * p.w_row + sb * qsize_of<QT>();
+                const int g = 2 * hf + (c >> 1), h = c & 1;
+                const int4 hd = *(const int4 *) b;
+                const int4 w = *(const int4 *) (b + (QT == GGML_TYPE_Q4_K ? 16 : 48) + 16 * (4 * hf + c));
+                const uint8_t * sc = (const uint8_t *) b + 4;
+                int s0, m0, s1, m1;
+                scale_min_k4(2 * g, sc, s0, m0);
+                scale_min_k4(2 * g + 1, sc, s1, m1);
+                const float d = h2f((uint16_t) (hd.x & 0xFFFF)), dmin = h2f((uint16_t) ((uint32_t) hd.x >> 16));
+                const float d0 = d * s0, mm0 = dmin * m0, d1 = d * s1, mm1 = dmin * m1;
+                const uint32_t wv[4] = {(uint32_t) w.x, (uint32_t) w.y, (uint32_t) w.z, (uint32_t) w.w};
+                uint32_t hv[4] = {0, 0, 0, 0};
+                if constexpr (QT == GGML_TYPE_Q5_K) {
+                    const int4 qh = *(const int4 *) (b + 16 + 16 * h);
+                    hv[0] = qh.x; hv[1] = qh.y; hv[2] = qh.z; hv[3] = qh.w;
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t byte = (wv[i >> 2] >> (8 * (i & 3))) & 0xFF;
+                    int ql = byte & 0xF, qhh = byte >> 4;
+                    if constexpr (QT == GGML_TYPE_Q5_K) {
+                        const uint32_t hb = (hv[i >> 2] >> (8 * (i & 3))) & 0xFF;
+                        ql += ((hb >> (2 * g)) & 1) << 4;
+                        qhh += ((hb >> (2 * g + 1)) & 1) << 4;
+                    }
+                    lo[i] = d0 * ql - mm0;
+                    hi[i] = d1 * qhh - mm1;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { lo[i] = 0.f; hi[i] = 0.f; }
+            }
+            // k_local of lo run = 64*(c>>1) + 16*h ; hi run = +32 ; 16-byte chunk = k_local/8
+            const int kl = 64 * (c >> 1) + 16 * (c & 1);
+            float t[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) t[i] = lo[i];
+            st_h8(lds, r, kl / 8, t);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) t[i] = lo[8 + i];
+            st_h8(lds, r, kl / 8 + 1, t);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) t[i] = hi[i];
+            st_h8(lds, r, (kl + 32) / 8, t);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) t[i] = hi[8 + i];
+            st_h8(lds, r, (kl + 32) / 8 + 1, t);
+        }
+    } else if constexpr (QT == GGML_TYPE_Q6_K) {
+        // 128 rows × 4 l-runs (t) of half n = k0/128 % 2 : 512 units, 2 per thread
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const int unit = tid + 256 * it;
+            const int r = unit >> 2, t = unit & 3;
+            const int64_t row = row0 + r;
+            float v[4][8];
+            if (row < p.M) {
+                const int64_t sb = k0 >> 8;
+                const int n = (int) ((k0 >> 7) & 1);
+                const char * b = wbase + row * p.w_row + sb * 210;
+                const float d = h2f(ld_u16(b + 208));
+                const char * qlp = b + 64 * n + 8 * t;
+                const char * qhp = b + 128 + 32 * n + 8 * t;
+                const int8_t * scp = (const int8_t *) (b + 192 + 8 * n + (t >> 1));
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint8_t la = (uint8_t) qlp[i], lb = (uint8_t) qlp[32 + i], hb = (uint8_t) qhp[i];
+                    v[0][i] = (float) (((la & 0xF) | (((hb >> 0) & 3) << 4)) - 32);
+                    v[1][i] = (float) (((lb & 0xF) | (((hb >> 2) & 3) << 4)) - 32);
+                    v[2][i] = (float) (((la >> 4) | (((hb >> 4) & 3) << 4)) - 32);
+                    v[3][i] = (float) (((lb >> 4) | (((hb >> 6) & 3) << 4)) - 32);
+                }
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq) {
+                    const float s = d * (float) scp[2 * qq];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[qq][i] *= s;
+                }
+            } else {
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[qq][i] = 0.f;
+            }
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) st_h8(lds, r, (32 * qq + 8 * t) / 8, v[qq]);
+        }
+    } else if constexpr (QT == GGML_TYPE_F16) {
+        // 128 rows × 16 chunks of 8 halves
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int unit = tid + 256 * it;
+            const int r = unit >> 4, ch = unit & 15;
+            const int64_t row = row0 + r;
+            const int64_t k = k0 + 8 * ch;
+            uint4 val = make_uint4(0, 0, 0, 0);
+            if (row < p.M) {
+                const uint16_t * src = (const uint16_t *) (wbase + row * p.w_row) + k;
+                if (k + 8 <= p.K && ((uintptr_t) src % 16) == 0) val = *(const uint4 *) src;
+                else {
+                    uint16_t tmp[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) tmp[i] = k + i < p.K ? src[i] : 0;
+                    val = *(uint4 *) tmp;
+                }
+            }
+            lds[swz(r, ch)] = val;
+        }
+    } else {
+        // generic: 8 consecutive k per unit via exact per-element dequant
+#pragma unroll 2
+        for (int it = 0; it < 8; ++it) {
+            const int unit = tid + 256 * it;
+            const int r = unit >> 4, ch = unit & 15;
+            const int64_t row = row0 + r;
+            const int64_t k = k0 + 8 * ch;
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int64_t kk = k + i;
+                if (row < p.M && kk < p.K) {
+                    const char * rb = wbase + row * p.w_row;
+                    if constexpr (QT == GGML_TYPE_F32) v[i] = ((const float *) rb)[kk];
+                    else if constexpr (QT == GGML_TYPE_BF16) v[i] = bf2f(((const uint16_t *) rb)[kk]);
+                    else v[i] = dequant_one<QT>(rb + (kk / qk_of<QT>()) * qsize_of<QT>(), (int) (kk % qk_of<QT>()));
+                } else {
+                    v[i] = 0.f;
+                }
+            }
+            st_h8(lds, r, ch, v);
+        }
+    }
+}
+
+template <int QT>
+__global__ __launch_bounds__(256, 2) void k_mmq(MmqArgs p) {
+    __shared__ uint4 lds_a[MM_BT * MM_BK / 8];   // tokens × K (f16)
+    __shared__ uint4 lds_b[MM_BW * MM_BK / 8];   // weight rows × K (f16)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;     // wave's 64-token × 64-row quadrant
+    const int64_t tok0 = (int64_t) blockIdx.x * MM_BT;
+    const int64_t row0 = (int64_t) blockIdx.y * MM_BW;
+    const int64_t ch = blockIdx.z;
+    const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
+    const char * wbase = p.w + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
+    const _Float16 * xbase = p.x + ch * p.N * p.kp;
+
+    float16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int r = lane & 31, hsel = lane >> 5;
+    for (int64_t k0 = 0; k0 < p.K; k0 += MM_BK) {
+        // activation tile: 128 tokens × 16 chunks, 8 per thread
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int unit = tid + 256 * it;
+            const int t = unit >> 4, chn = unit & 15;
+            const int64_t tok = tok0 + t;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (tok < p.N) v = *(const uint4 *) (xbase + tok * p.kp + k0 + 8 * chn);
+            lds_a[swz(t, chn)] = v;
+        }
+        load_w_tile<QT>(p, wbase, row0, k0, lds_b);
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < MM_BK; kk += 16) {
+            const int chn = kk / 8 + hsel;
+            half8 a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint4 va = lds_a[swz(wm * 64 + i * 32 + r, chn)];
+                a[i] = *(const half8 *) &va;
+                const uint4 vb = lds_b[swz(wn * 64 + i * 32 + r, chn)];
+                b[i] = *(const half8 *) &vb;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // epilogue: C[token][row]; col = lane&31 → weight row, row formula → token
+    float * dbase = p.dst + i12 * p.d_c2 + i13 * p.d_c3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t wrow = row0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t tok = tok0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+                if (tok < p.N && wrow < p.M) dbase[tok * p.d_col + wrow] = acc[i][j][e];
+            }
+        }
+    }
+}
+
+bool mmq_type_ok(int t) {
+    switch (t) {
+        case GGML_TYPE_Q4_0: case GGML_TYPE_Q4_1: case GGML_TYPE_Q5_0: case GGML_TYPE_Q5_1: case GGML_TYPE_Q8_0:
+        case GGML_TYPE_Q4_K: case GGML_TYPE_Q5_K: case GGML_TYPE_Q6_K:
+        case GGML_TYPE_F16: case GGML_TYPE_F32: case GGML_TYPE_BF16:
+            return true;
+        default: return false;
+    }
+}
+
+static int64_t mmq_kp(const ggml_tensor * dst) { return mx_ceil_div(dst->src[0]->ne[0], MM_BK) * MM_BK; }
+
+size_t mmq_scratch(const ggml_tensor * dst) {
+    const ggml_tensor * x = dst->src[1];
+    const int64_t ncols = x->ne[1] * x->ne[2] * x->ne[3];
+    return ncols * mmq_kp(dst) * 2 + 256;
+}
+
+void mmq_run(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    const int64_t kp = mmq_kp(dst);
+    const int64_t ncols = x->ne[1] * x->ne[2] * x->ne[3];
+    _Float16 * xa = (_Float16 *) c.scratch->take(ncols * kp * 2);
+    {
+        dim3 grid((unsigned) std::min<int64_t>(mx_ceil_div(kp, 256), 16), (unsigned) ncols);
+        k_act_f16<<<grid, 256, 0, c.st>>>((const char *) x->data, x->ne[0], x->ne[1], x->ne[2],
+                                          x->nb[0], x->nb[1], x->nb[2], x->nb[3], kp, xa);
+    }
+    MmqArgs p{};
+    p.w = (const char *) w->data; p.w_row = w->nb[1]; p.w_c2 = w->nb[2]; p.w_c3 = w->nb[3];
+    p.x = xa; p.kp = kp;
+    p.dst = (float *) dst->data; p.d_col = dst->nb[1] / 4; p.d_c2 = dst->nb[2] / 4; p.d_c3 = dst->nb[3] / 4;
+    p.M = w->ne[1]; p.N = x->ne[1]; p.K = w->ne[0]; p.ne12 = x->ne[2];
+    p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
+    dim3 grid((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, MM_BW), (unsigned) (x->ne[2] * x->ne[3]));
+    switch (w->type) {
+#define MQ(T) case T: k_mmq<T><<<grid, 256, 0, c.st>>>(p); break;
+        MQ(GGML_TYPE_Q4_0) MQ(GGML_TYPE_Q4_1) MQ(GGML_TYPE_Q5_0) MQ(GGML_TYPE_Q5_1) MQ(GGML_TYPE_Q8_0)
+        MQ(GGML_TYPE_Q4_K) MQ(GGML_TYPE_Q5_K) MQ(GGML_TYPE_Q6_K)
+        MQ(GGML_TYPE_F16) MQ(GGML_TYPE_F32) MQ(GGML_TYPE_BF16)
+#undef MQ
+        default: MX_ABORT("mmq type %d", (int) w->type);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MUL_MAT dispatch
+// ---------------------------------------------------------------------------
+static bool quant_fast_path_ok(const ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    if (!mmvq_type_ok(w->type)) return false;
+    if (x->type != GGML_TYPE_F32 || dst->nb[0] != 4) return false;
+    if (w->nb[0] != (size_t) mx_type(w->type).size) return false;    // rows of whole blocks
+    if (w->ne[0] % qk_of_type(w->type) != 0) return false;
+    if (x->nb[0] != 4) return false;
+    return true;
+}
+
+static bool mmq_ok(const ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    if (!mmq_type_ok(w->type) || x->type != GGML_TYPE_F32 || dst->nb[0] != 4) return false;
+    if (w->nb[0] != (size_t) mx_type(w->type).size) return false;
+    if (mx_type(w->type).quant && w->ne[0] % qk_of_type(w->type) != 0) return false;
+    // K-quant tile loaders step through whole 128-wide halves of super-blocks
+    if ((w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K) && w->ne[0] % 256 != 0) return false;
+    if ((w->type == GGML_TYPE_F16) && (w->nb[1] % 16 != 0)) return false;
+    return true;
+}
+
+bool mul_mat_supported(const ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    if (dst->type != GGML_TYPE_F32 || x->type != GGML_TYPE_F32) return false;
+    if (x->ne[2] % w->ne[2] != 0 || x->ne[3] % w->ne[3] != 0) return false;
+    switch (w->type) {
+        case GGML_TYPE_F32: case GGML_TYPE_F16: case GGML_TYPE_BF16:
+        case GGML_TYPE_Q4_0: case GGML_TYPE_Q4_1: case GGML_TYPE_Q5_0: case GGML_TYPE_Q5_1: case GGML_TYPE_Q8_0:
+        case GGML_TYPE_Q4_K: case GGML_TYPE_Q5_K: case GGML_TYPE_Q6_K:
+            break;
+        default: return false;
+    }
+    if (mx_type(w->type).quant && w->nb[0] != (size_t) mx_type(w->type).size) return false;
+    return true;
+}
+
+size_t mul_mat_scratch(const ggml_tensor * dst) {
+    const ggml_tensor * x = dst->src[1];
+    size_t s = 0;
+    if (x->ne[1] <= 8 && quant_fast_path_ok(dst)) s = quantize_scratch(x);
+    else if (mmq_ok(dst)) s = mmq_scratch(dst);
+    return s;
+}
+
+void op_mul_mat(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * x = dst->src[1];
+    if (x->ne[1] <= 8 && quant_fast_path_ok(dst)) { mmvq_run(c, dst); return; }
+    if (x->ne[1] > 8 && mmq_ok(dst)) { mmq_run(c, dst); return; }
+    mmv_generic_run(c, dst);
+}
+
+}  // namespace mx
