@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""bench.py — llama-bench tg128 (+ pp512) tokens/s for Llama-3-8B Q4_K_M on MI355X.
+
+Workload (BASELINE.json configs[1]): Llama-3-8B shapes (n_embd 4096, 32 layers, 32/8
+heads, n_ff 14336, vocab 128256) with Q4_K_M weights (Q4_K + Q6_K attn_v/ffn_down on
+the 16 use_more_bits layers + Q6_K output), synthetic random weights generated on the
+device (no checkpoints offline). A *step* is one tg128 run exactly as llama-bench's
+test_gen does it (tools/llama-bench/llama-bench.cpp:1991): reset the KV cache, then 128
+single-token decodes of random tokens, each followed by a device synchronise and the
+logits copy-back. value = generated tokens / wall time. pp512 (one 512-token prefill,
+test_prompt :1962) is reported beside it.
+
+Multi-GPU (torchrun, one process per GPU): layer split — rank r owns a
+contiguous block of layers of its own replica-sized slice; see DESIGN.md. With
+--gpus N > 1 every rank runs its own tg128 stream and value is the job aggregate
+("replicas" — decode of one sequence does not speed up with layer split).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "llama-bench tg128 + pp512 tok/s, Llama-3-8B Q4_K_M, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        tdist.init_process_group(backend=backend)
+        dist = tdist
+    return world, rank, local, dist
+
+
+def barrier(dist, local):
+    if dist is None:
+        return
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize(local)
+    dist.barrier()
+
+
+def max_over_ranks(dist, v):
+    if dist is None:
+        return v
+    import torch
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, v):
+    if dist is None:
+        return v
+    import torch
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def tg_step(sess, rng, n_vocab, n_gen):
+    sess.reset()
+    toks = rng.integers(0, n_vocab, size=n_gen, dtype=np.int32)
+    for t in toks:
+        sess.decode(np.array([t], dtype=np.int32), want_logits=True)
+
+
+def roofline_glu(pkg, be, iters=200):
+    """Dominant decode kernel: the fused gate/up SWIGLU GEMV over two Q4_K
+    [4096 -> 14336] weights (2.1 GB of the 4.6 GB read per token). Algorithmic bytes
+    per launch = both weight matrices + the int8 activation with its per-32 scales."""
+    lib = pkg._lib.load()
+    ctx = pkg.Context()
+    K, M = 4096, 14336
+    wg = ctx.new_tensor("q4_K", K, M)
+    wu = ctx.new_tensor("q4_K", K, M)
+    x = ctx.new_tensor("f32", K, 1)
+    out = ctx.new_tensor("f32", M, 1)
+    ctx.alloc(be)
+    rng = np.random.default_rng(7)
+    for w in (wg, wu):
+        raw = rng.integers(0, 256, size=w.nbytes(), dtype=np.uint8)
+        blk = raw.reshape(-1, 144)
+        blk[:, 0:2] = np.frombuffer(np.float16(1e-4).tobytes(), np.uint8)
+        blk[:, 2:4] = np.frombuffer(np.float16(7.5e-4).tobytes(), np.uint8)
+        w.set(raw)
+    x.set(rng.standard_normal(K).astype(np.float32))
+    us = lib.ggml_backend_mi355x_time_mmvq(be.ptr, wg.ptr, wu.ptr, x.ptr, out.ptr, iters)
+    bytes_per_launch = wg.nbytes() + wu.nbytes() + K + (K // 32) * 8
+    ctx.free()
+    achieved = bytes_per_launch / (us * 1e-6) / 1e9
+    return {"bound": "hbm", "kernel": "k_mmvq<Q4_K,1,32,GLU> (ffn gate+up, 4096->14336 x2)",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(us, 2)}
+
+
+def cpu_baseline(args):
+    """Reference CPU backend (oracle/_ref, built from /root/reference sources) on the same
+    workload shape, bounded sample. Returns None when the reference build is absent."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref-llama-bench")
+    if not os.path.exists(exe) or args.no_cpu_baseline:
+        return None
+    threads = int(os.environ.get("MX_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    gguf = os.path.join(os.environ.get("TMPDIR", "/tmp"), "mx_bench_llama3_8b_q4km.gguf")
+    try:
+        if not os.path.exists(gguf):
+            subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gguf_synth.py"), "--shape", "llama3_8b",
+                            "--recipe", "q4_k_m", "--out", gguf], check=True, timeout=900)
+        r = subprocess.run([exe, "-m", gguf, "-t", str(threads), "-p", str(args.cpu_pp), "-n", str(args.cpu_tg)],
+                           capture_output=True, text=True, timeout=900)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        res = json.loads(line)
+        return {"value": res["tg_tok_s"], "unit": "tok/s", "cores": threads, "kind": "reference",
+                "pp_tok_s": res.get("pp_tok_s"),
+                "sample": f"reference CPU backend (libllama+ggml-cpu from /root/reference), same GGUF shape/recipe, "
+                          f"tg{args.cpu_tg} after pp{args.cpu_pp}, {threads} threads"}
+    except Exception as e:  # noqa: BLE001 — the GPU number stays valid without the baseline
+        return {"value": None, "unit": "tok/s", "cores": threads, "kind": "reference", "sample": f"failed: {e}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tg", type=int, default=128)
+    ap.add_argument("--pp", type=int, default=512)
+    ap.add_argument("--recipe", default="q4_k_m")
+    ap.add_argument("--no-fa", action="store_true", help="llama-bench -fa 0 graph (KQ mul_mat + softmax)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-pp", type=int, default=32)
+    ap.add_argument("--cpu-tg", type=int, default=16)
+    ap.add_argument("--skip-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local, dist = dist_setup(args.gpus)
+    from mi355x_pkg import load_package
+    pkg = load_package()
+    be = pkg.Backend(local if world > 1 else 0)
+    model = pkg.Model.random(be, pkg.LLAMA3_8B, args.recipe, seed=1234 + rank)
+    n_vocab = model.hp.n_vocab
+    sess = pkg.Session(model, n_ctx=max(args.pp, args.tg) + 256, n_ubatch=512, flash_attn=not args.no_fa)
+    rng = np.random.default_rng(42 + rank)
+
+    for _ in range(args.warmup):
+        tg_step(sess, rng, n_vocab, args.tg)
+    barrier(dist, local)
+    be.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tg_step(sess, rng, n_vocab, args.tg)
+    be.synchronize()
+    barrier(dist, local)
+    dt = max_over_ranks(dist, time.perf_counter() - t0)
+    tokens = sum_over_ranks(dist, args.steps * args.tg)
+    tg_value = tokens / dt
+
+    # pp512 beside it (not the headline value)
+    pp_tok_s = None
+    if args.pp > 0:
+        toks = rng.integers(0, n_vocab, size=args.pp, dtype=np.int32)
+        sess.reset(); sess.decode(toks)  # warm the prefill graph
+        reps = 3
+        be.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            sess.reset()
+            sess.decode(toks)
+        be.synchronize()
+        pp_tok_s = reps * args.pp / (time.perf_counter() - t1)
+
+    stats = be.stats()
+    decode_bytes = model.decode_bytes()
+    roof = None if args.skip_roofline else roofline_glu(pkg, be)
+    cpu = cpu_baseline(args) if (rank == 0 and world == 1) else None
+
+    if rank == 0:
+        per_gpu_tg = tg_value / world
+        out = {
+            "metric": METRIC,
+            "value": round(tg_value, 2),
+            "unit": "tok/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "q4_K/q6_K weights, int8 x int8 dot (sdot4) + f32 accumulate",
+            "data": "synthetic (random Q4_K_M weights generated on device, random tokens)",
+            "config": {"workload": "Llama-3-8B Q4_K_M tg128 decode (llama-bench test_gen), 1 sequence per GPU",
+                       "model_shape": "llama3-8b", "recipe": args.recipe, "tg": args.tg, "pp": args.pp,
+                       "flash_attn": not args.no_fa, "parallelism": f"replicas x{world}" if world > 1 else "single"},
+            "pp512_tok_s": round(pp_tok_s, 1) if pp_tok_s else None,
+            "decode_bytes_per_token": decode_bytes,
+            "decode_roofline": {"achieved_GBs": round(decode_bytes * per_gpu_tg / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
+                                "frac": round(decode_bytes * per_gpu_tg / 1e9 / HBM_PEAK_GBS, 4)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "executor": stats,
+        }
+        print(json.dumps(out), flush=True)
+    sess.free()
+    model.free()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -43,3 +43,15 @@ void ggml_backend_mi355x_stats(ggml_backend_t backend, uint64_t out[4]);
 #ifdef __cplusplus
 }
 #endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Profiling hook (bench roofline): average µs of one launch of the decode GEMV that
+ * MUL_MAT(w, x) (w2 == NULL) or the fused gate/up SWIGLU (w2 = up weight) runs,
+ * timed with HIP events on `backend`'s stream over `iters` back-to-back launches. */
+double ggml_backend_mi355x_time_mmvq(ggml_backend_t backend, const struct ggml_tensor * w, const struct ggml_tensor * w2,
+                                     const struct ggml_tensor * x, struct ggml_tensor * dst, int iters);
+#ifdef __cplusplus
+}
+#endif

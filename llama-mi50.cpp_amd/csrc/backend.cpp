@@ -406,3 +406,12 @@ void ggml_backend_mi355x_stats(ggml_backend_t b, uint64_t out[4]) {
 }
 
 }  // extern "C"
+
+namespace mx { double time_mmvq(Stream * s, const ggml_tensor * w, const ggml_tensor * w2, const ggml_tensor * x, ggml_tensor * dst, int iters); }
+
+extern "C" double ggml_backend_mi355x_time_mmvq(ggml_backend_t b, const ggml_tensor * w, const ggml_tensor * w2,
+                                                const ggml_tensor * x, ggml_tensor * dst, int iters) {
+    mx::Stream * s = mx::stream_of(b);
+    HIP_CHECK(hipSetDevice(s->device));
+    return mx::time_mmvq(s, w, w2, x, dst, iters);
+}

@@ -240,7 +240,7 @@ bool flash_attn_supported(const ggml_tensor * dst) {
     if (!((k->type == GGML_TYPE_F16 && v->type == GGML_TYPE_F16) || (k->type == GGML_TYPE_F32 && v->type == GGML_TYPE_F32))) return false;
     if (k->ne[0] != v->ne[0]) return false;
     const int64_t D = k->ne[0];
-    if (D != 64 && D != 128 && D != 256 && D != 80 && D != 96 && D != 112) return false;
+    if (D != 32 && D != 40 && D != 48 && D != 64 && D != 80 && D != 96 && D != 112 && D != 128 && D != 256) return false;
     if (q->ne[2] % k->ne[2] != 0 || q->ne[2] / k->ne[2] > FA_MAXG) return false;
     if (k->ne[2] != v->ne[2]) return false;
     if (m && m->type != GGML_TYPE_F16) return false;
@@ -253,6 +253,9 @@ bool flash_attn_supported(const ggml_tensor * dst) {
 template <typename TK, typename TV>
 static void fa_launch(OpCtx & c, int D, dim3 grid, const FaArgs & a) {
     switch (D) {
+        case 32:  k_fattn<TK, TV, 32><<<grid, 256, 0, c.st>>>(a); break;
+        case 40:  k_fattn<TK, TV, 40><<<grid, 256, 0, c.st>>>(a); break;
+        case 48:  k_fattn<TK, TV, 48><<<grid, 256, 0, c.st>>>(a); break;
         case 64:  k_fattn<TK, TV, 64><<<grid, 256, 0, c.st>>>(a); break;
         case 80:  k_fattn<TK, TV, 80><<<grid, 256, 0, c.st>>>(a); break;
         case 96:  k_fattn<TK, TV, 96><<<grid, 256, 0, c.st>>>(a); break;
@@ -306,7 +309,7 @@ void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
     switch (D) {
 #define CMB(DD) case DD: k_fattn_combine<DD><<<(unsigned) rows, 64, 0, c.st>>>(a.opart, a.mpart, a.lpart, psk, (char *) dst->data, \
                                                        dst->nb[1], dst->nb[2], dst->nb[3], rows, nsplit, q->ne[2], q->ne[1]); break;
-        CMB(64) CMB(80) CMB(96) CMB(112) CMB(128) CMB(256)
+        CMB(32) CMB(40) CMB(48) CMB(64) CMB(80) CMB(96) CMB(112) CMB(128) CMB(256)
 #undef CMB
     }
 }

@@ -219,6 +219,45 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up,
 }
 
 // ---------------------------------------------------------------------------
+// kernel timing hook for the bench's roofline: quantise x once, then time `iters`
+// back-to-back launches of exactly the GEMV kernel the executor would launch for
+// MUL_MAT(w, x) (or the fused gate/up GLU when w2 != NULL) with HIP events on the
+// backend's own stream. Returns the average µs per launch.
+// ---------------------------------------------------------------------------
+double time_mmvq(Stream * s, const ggml_tensor * w, const ggml_tensor * w2, const ggml_tensor * x, ggml_tensor * dst, int iters) {
+    OpCtx c{s, s->stream, &s->scratch};
+    const size_t need = quantize_scratch(x);
+    if (need > s->scratch.cap) {
+        HIP_CHECK(hipStreamSynchronize(s->stream));
+        if (s->scratch.base) HIP_CHECK(hipFree(s->scratch.base));
+        HIP_CHECK(hipMalloc((void **) &s->scratch.base, need));
+        s->scratch.cap = need;
+        s->gcache.key.clear();
+    }
+    s->scratch.reset();
+    ActQ a = quantize_activations(c, x);
+    MmvArgs p = mmv_args(w, x, dst);
+    if (w2) p.w2 = (const char *) w2->data;
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) {
+        if (w2) mmvq_dispatch<true>(c, w->type, p, a, 1); else mmvq_dispatch<false>(c, w->type, p, a, 1);
+    }
+    HIP_CHECK(hipEventRecord(e0, s->stream));
+    for (int i = 0; i < iters; ++i) {
+        if (w2) mmvq_dispatch<true>(c, w->type, p, a, 1); else mmvq_dispatch<false>(c, w->type, p, a, 1);
+    }
+    HIP_CHECK(hipEventRecord(e1, s->stream));
+    HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    return 1000.0 * ms / iters;
+}
+
+// ---------------------------------------------------------------------------
 // generic GEMV: any dequantisable / float weight type, f32 activations, exact
 // dequant (used for types without an sdot4 unit, and as the oracle-shaped path)
 // ---------------------------------------------------------------------------
