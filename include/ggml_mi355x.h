@@ -48,10 +48,15 @@ void ggml_backend_mi355x_stats(ggml_backend_t backend, uint64_t out[4]);
 extern "C" {
 #endif
 /* Profiling hook (bench roofline): average µs of one launch of the decode GEMV that
- * MUL_MAT(w, x) (w2 == NULL) or the fused gate/up SWIGLU (w2 = up weight) runs,
- * timed with HIP events on `backend`'s stream over `iters` back-to-back launches. */
-double ggml_backend_mi355x_time_mmvq(ggml_backend_t backend, const struct ggml_tensor * w, const struct ggml_tensor * w2,
+ * MUL_MAT(w[i], x) (w2 == NULL) or the fused gate/up SWIGLU (w2[i] = up weight) runs,
+ * timed with HIP events on `backend`'s stream over `iters` back-to-back launches that
+ * cycle over the n_w weight sets (pass every layer's weights to stream from HBM). */
+double ggml_backend_mi355x_time_mmvq(ggml_backend_t backend, const struct ggml_tensor * const * w,
+                                     const struct ggml_tensor * const * w2, int n_w,
                                      const struct ggml_tensor * x, struct ggml_tensor * dst, int iters);
+/* Launch-geometry overrides for tuning sweeps (0 = built-in choice):
+ * idx 0/1 = GEMV lanes-per-row / units-per-lane, 2/3 = the same for the fused SwiGLU GEMV. */
+void ggml_backend_mi355x_set_tune(int idx, int value);
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,9 @@ void        mxr_model_free(mxr_model * m);
 void        mxr_model_hparams(const mxr_model * m, mxr_hparams * out);
 /* bytes of all weights a decode step reads (every tensor except token_embd) */
 int64_t     mxr_model_decode_bytes(const mxr_model * m);
+/* weight of layer il by GGUF role ("attn_q", "attn_k", "attn_v", "attn_output",
+ * "ffn_gate", "ffn_up", "ffn_down", "attn_norm", "ffn_norm"); NULL if absent */
+struct ggml_tensor * mxr_model_layer_tensor(const mxr_model * m, int32_t il, const char * which);
 /* bytes per weight type id (index = ggml_type), for reporting */
 void        mxr_model_type_bytes(const mxr_model * m, int64_t out[GGML_TYPE_COUNT]);
 

@@ -70,7 +70,8 @@ def load():
     _sig(lib, "ggml_backend_is_mi355x", ctypes.c_bool, P)
     _sig(lib, "ggml_backend_mi355x_buffer_type", P, I)
     _sig(lib, "ggml_backend_mi355x_stats", None, P, ctypes.POINTER(ctypes.c_uint64))
-    _sig(lib, "ggml_backend_mi355x_time_mmvq", ctypes.c_double, P, P, P, P, P, I)
+    _sig(lib, "ggml_backend_mi355x_time_mmvq", ctypes.c_double, P, P, P, I, P, P, I)
+    _sig(lib, "ggml_backend_mi355x_set_tune", None, I, I)
     # graph builder
     _sig(lib, "mxg_init", P)
     _sig(lib, "mxg_free", None, P)
@@ -115,6 +116,7 @@ def load():
     _sig(lib, "mxr_model_load_gguf", P, P, ctypes.c_char_p)
     _sig(lib, "mxr_model_free", None, P)
     _sig(lib, "mxr_model_hparams", None, P, ctypes.POINTER(MxrHparams))
+    _sig(lib, "mxr_model_layer_tensor", P, P, I, ctypes.c_char_p)
     _sig(lib, "mxr_model_decode_bytes", I64, P)
     _sig(lib, "mxr_model_type_bytes", None, P, ctypes.POINTER(I64))
     _sig(lib, "mxr_context_new", P, P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32)

@@ -160,6 +160,7 @@ static void be_free(ggml_backend_t b) {
     if (s->gcache.exec) hipGraphExecDestroy(s->gcache.exec);
     if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
     if (s->scratch.base) hipFree(s->scratch.base);
+    if (s->act.base) hipFree(s->act.base);
     hipStreamDestroy(s->stream);
     delete s;  // the ggml_backend struct lives inside Stream
 }
@@ -407,11 +408,19 @@ void ggml_backend_mi355x_stats(ggml_backend_t b, uint64_t out[4]) {
 
 }  // extern "C"
 
-namespace mx { double time_mmvq(Stream * s, const ggml_tensor * w, const ggml_tensor * w2, const ggml_tensor * x, ggml_tensor * dst, int iters); }
+namespace mx {
+double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * const * w2, int nw,
+                 const ggml_tensor * x, ggml_tensor * dst, int iters);
+extern int g_tune[16];
+}
 
-extern "C" double ggml_backend_mi355x_time_mmvq(ggml_backend_t b, const ggml_tensor * w, const ggml_tensor * w2,
-                                                const ggml_tensor * x, ggml_tensor * dst, int iters) {
+extern "C" double ggml_backend_mi355x_time_mmvq(ggml_backend_t b, const ggml_tensor * const * w, const ggml_tensor * const * w2,
+                                                int n_w, const ggml_tensor * x, ggml_tensor * dst, int iters) {
     mx::Stream * s = mx::stream_of(b);
     HIP_CHECK(hipSetDevice(s->device));
-    return mx::time_mmvq(s, w, w2, x, dst, iters);
+    return mx::time_mmvq(s, w, w2, n_w, x, dst, iters);
+}
+
+extern "C" void ggml_backend_mi355x_set_tune(int idx, int value) {
+    if (idx >= 0 && idx < 16) mx::g_tune[idx] = value;
 }

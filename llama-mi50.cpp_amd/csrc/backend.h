@@ -41,6 +41,26 @@ struct Scratch {
     void reset() { off = 0; }
 };
 
+// quantised activation columns: int8 values + per-32 f32 scale d and d·Σq
+struct ActQ {
+    const int8_t * q;    // [ncols][kp]
+    const float * d;     // [ncols][kp/32]
+    const float * s;     // [ncols][kp/32]
+    int64_t kp;          // padded K (multiple of 32)
+};
+
+// A MUL_MAT src1 quantised once per graph pass and shared by every GEMV that reads
+// it (Q/K/V share the attn-norm output, gate/up share the ffn-norm output).
+// Keyed by the memory it was quantised from (data, row length, column count), so a
+// reshape/view of the producer's output (e.g. the flash-attn result reshaped to
+// [n_embd, n_tokens]) finds it too.
+struct ActCacheEntry {
+    const void * data = nullptr;
+    int64_t ne0 = 0, ncols = 0;
+    size_t bytes = 0;
+    ActQ a{};
+};
+
 struct GraphCache {
     std::vector<uint64_t> key;    // signature of the captured cgraph
     hipGraph_t graph = nullptr;
@@ -48,10 +68,23 @@ struct GraphCache {
     int hits = 0;
 };
 
+// RMS_NORM → MUL(w) whose only consumers are single-token GEMVs: not materialised,
+// the GEMV prologues recompute it from x (exec.cpp run_nodes)
+struct DeferredNorm {
+    ggml_tensor * norm;
+    const ggml_tensor * w;
+    ggml_tensor * mul;
+};
+
 struct Stream {
     int device = 0;
+    std::vector<DeferredNorm> deferred;
     hipStream_t stream = nullptr;
     Scratch scratch;
+    Scratch act;                       // ring of quantised activations (act_cache)
+    ActCacheEntry act_cache[4];
+    int act_next = 0;
+    size_t act_slot = 0;               // bytes per ring slot
     GraphCache gcache;
     bool use_graphs = true;
     bool use_fusion = true;
@@ -104,9 +137,25 @@ bool mul_mat_supported(const ggml_tensor * dst);
 bool mul_mat_id_supported(const ggml_tensor * dst);
 bool flash_attn_supported(const ggml_tensor * dst);
 
-// fused decode helpers (fusion.cpp decides, kernels live in ops_mmvq.hip)
+// fused decode helpers (exec.cpp decides, kernels live in ops_mmvq.hip / ops_misc.hip)
 // y_gate/up = W·x ; out = act(gate) * up   (ggml-cuda.cu:2145-2181 semantics)
 bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * up_mm, ggml_tensor * glu);
+// out = W·x + residual (MUL_MAT followed by ADD)
+bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * residual, ggml_tensor * add);
+// RMS_NORM → MUL(w) that also emits the quantised activation of its output
+bool rms_norm_mul_q8(OpCtx & c, ggml_tensor * norm, const ggml_tensor * w, ggml_tensor * out);
+// activation-cache management (ops_mmvq.hip)
+size_t act_slot_bytes(const ggml_tensor * src1);
+void act_cache_reset(Stream * s);
+void act_cache_invalidate(Stream * s, const ggml_tensor * written);
+ActQ * act_cache_alloc(Stream * s, const ggml_tensor * t);   // reserve a slot for t (caller fills it)
+ActQ * act_cache_alloc_raw(Stream * s, const void * data, int64_t ne0, int64_t ncols, size_t bytes);
+const ActQ * act_cache_find(Stream * s, const ggml_tensor * t);   // q8 form of t, if cached
+bool mmvq_small_batch_ok(const ggml_tensor * mm);             // MUL_MAT runs on the GEMV path
+// consumer count of every tensor in the graph being executed
+using UseCount = std::unordered_map<const ggml_tensor *, int>;
+// decode Q/K/V projections + RoPE + KV-cache stores in one launch; returns nodes consumed
+int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 
 Stream * stream_of(ggml_backend_t b);
 

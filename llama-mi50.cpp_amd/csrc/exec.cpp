@@ -10,6 +10,7 @@
 // strides, data pointers, op params) decides replay; capture happens only on the
 // second sighting of a signature so one-shot prefill graphs run eagerly.
 #include "backend.h"
+#include "gemv.h"
 
 #include <algorithm>
 #include <unordered_map>
@@ -55,7 +56,113 @@ static void graph_signature(const ggml_cgraph * g, std::vector<uint64_t> & k) {
 // ---- fusion ---------------------------------------------------------------
 // RMS_NORM → MUL(norm, w): the build_norm pair (src/llama-graph.cpp build_norm;
 // reference fusion gate ggml-cuda.cu:3844-3854).
-using UseMap = std::unordered_map<const ggml_tensor *, int>;
+using UseMap = UseCount;
+static bool g_no_qkv = getenv("GGML_MI355X_NO_QKV_FUSION") != nullptr;
+
+// ---- deferred RMS norm --------------------------------------------------------
+// An attn_norm / ffn_norm pair whose every consumer is a single-token GEMV is not
+// run: each GEMV workgroup recomputes rms_norm(x)·w in its prologue (gemv.cuh).
+// The pair is materialised after all if anything else reads its output or writes
+// the memory it depends on before the consumers ran.
+static bool overlaps(const void * a, size_t na, const void * b, size_t nb) {
+    const char * pa = (const char *) a, * pb = (const char *) b;
+    return pa < pb + nb && pb < pa + na;
+}
+static bool t_overlaps(const ggml_tensor * a, const ggml_tensor * b) {
+    return a && b && a->data && b->data && overlaps(a->data, mx_nbytes(a), b->data, mx_nbytes(b));
+}
+
+XStage xstage_of(Stream * s, const ggml_tensor * x) {
+    for (const DeferredNorm & d : s->deferred)
+        if (x->data == d.mul->data && mx_nelements(x) == mx_nelements(d.mul) && mx_is_contiguous(x))
+            return XStage{(const float *) d.norm->src[0]->data, (const float *) d.w->data, mx_op_param<float>(d.norm, 0), 1};
+    XStage xs{(const float *) x->data, nullptr, 0.0f, 0};
+    if (const ActQ * a = act_cache_find(s, x)) {
+        if (a->kp == x->ne[0]) { xs.q8 = a->q; xs.q8d = a->d; xs.q8s = a->s; }
+    }
+    return xs;
+}
+
+static void materialize(OpCtx & c, size_t k) {
+    const DeferredNorm d = c.s->deferred[k];
+    c.s->deferred.erase(c.s->deferred.begin() + k);
+    act_cache_invalidate(c.s, d.mul);
+    op_rms_norm(c, d.norm, d.w, d.mul);
+}
+
+void deferred_guard_write(OpCtx & c, const ggml_tensor * t) {
+    for (size_t k = 0; k < c.s->deferred.size();) {
+        const DeferredNorm & d = c.s->deferred[k];
+        if (t_overlaps(t, d.norm->src[0]) || t_overlaps(t, d.w) || t_overlaps(t, d.mul)) materialize(c, k);
+        else ++k;
+    }
+}
+
+void deferred_guard_read(OpCtx & c, const ggml_tensor * t) {
+    for (size_t k = 0; k < c.s->deferred.size();) {
+        if (t_overlaps(t, c.s->deferred[k].mul)) materialize(c, k);
+        else ++k;
+    }
+}
+
+bool gemv2_stage(OpCtx & c, const ggml_tensor * x, std::initializer_list<const ggml_tensor *> outs,
+                 std::initializer_list<const ggml_tensor *> reads, XStage * xs) {
+    for (const ggml_tensor * t : reads) deferred_guard_read(c, t);
+    for (const ggml_tensor * t : outs) deferred_guard_write(c, t);
+    *xs = xstage_of(c.s, x);
+    const size_t xb = (size_t) x->ne[0] * sizeof(float);
+    for (const ggml_tensor * t : outs) {
+        if (overlaps(t->data, mx_nbytes(t), xs->x, xb)) return false;
+        if (xs->norm && overlaps(t->data, mx_nbytes(t), xs->nw, xb)) return false;
+    }
+    return true;
+}
+
+// before an ordinary node: it reads nothing deferred (except a GEMV's src1, which the
+// GEMV absorbs) and overwrites nothing a deferred norm still needs
+static void deferred_guard_node(OpCtx & c, const ggml_tensor * n) {
+    if (c.s->deferred.empty()) return;
+    const bool absorbs = n->op == GGML_OP_MUL_MAT && g_gemv2 && gemv2_ok(n->src[0], n->src[1], n);
+    for (size_t k = 0; k < c.s->deferred.size();) {
+        bool hit = false;
+        for (int j = 0; j < GGML_MAX_SRC && !hit; ++j) {
+            if (!n->src[j] || (absorbs && j == 1)) continue;
+            hit = t_overlaps(n->src[j], c.s->deferred[k].mul);
+        }
+        if (hit) materialize(c, k);
+        else ++k;
+    }
+    deferred_guard_write(c, n);
+}
+
+static bool try_defer_norm(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
+    if (!g_gemv2 || i + 1 >= g->n_nodes) return false;
+    ggml_tensor * norm = g->nodes[i];
+    ggml_tensor * mul = g->nodes[i + 1];
+    if (mul->op != GGML_OP_MUL || norm->type != GGML_TYPE_F32 || mul->type != GGML_TYPE_F32) return false;
+    const ggml_tensor * w = mul->src[0] == norm ? mul->src[1] : (mul->src[1] == norm ? mul->src[0] : nullptr);
+    const ggml_tensor * x = norm->src[0];
+    if (!w || !mx_are_same_shape(mul, norm) || uses[norm] != 1) return false;
+    if ((norm->flags | mul->flags) & GGML_TENSOR_FLAG_OUTPUT) return false;
+    const int64_t K = x->ne[0];
+    if (x->type != GGML_TYPE_F32 || mx_nelements(x) != K || !mx_is_contiguous(x) || K % 32 || K > GEMV2_MAX_NORM_K) return false;
+    if (w->type != GGML_TYPE_F32 || mx_nelements(w) != K || !mx_is_contiguous(w)) return false;
+    if (((uintptr_t) x->data | (uintptr_t) w->data) & 15) return false;
+    const int need = uses[mul];
+    if (need < 1) return false;   // a graph result, not an intermediate
+    int found = 0;
+    for (int j = i + 2; j < g->n_nodes && j < i + 66 && found < need; ++j) {
+        const ggml_tensor * m = g->nodes[j];
+        for (int k = 0; k < GGML_MAX_SRC; ++k) {
+            if (m->src[k] != mul) continue;
+            if (m->op != GGML_OP_MUL_MAT || k != 1 || !gemv2_ok(m->src[0], mul, m)) return false;
+            ++found;
+        }
+    }
+    if (found != need) return false;
+    c.s->deferred.push_back(DeferredNorm{norm, w, mul});
+    return true;
+}
 
 static bool try_fuse_rms_mul(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     if (i + 1 >= g->n_nodes) return false;
@@ -67,8 +174,24 @@ static bool try_fuse_rms_mul(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     if (!mx_are_same_shape(mul, norm)) return false;
     // the norm output must be consumed only by the MUL (it is a graph-internal temporary)
     if (uses[norm] != 1 || (norm->flags & GGML_TENSOR_FLAG_OUTPUT)) return false;
-    op_rms_norm(c, norm, w, mul);
+    act_cache_invalidate(c.s, mul);
+    // decode rows: also emit the q8 activation the following GEMVs read
+    if (!rms_norm_mul_q8(c, norm, w, mul)) op_rms_norm(c, norm, w, mul);
     return true;
+}
+
+// MUL_MAT → ADD(mm, residual): the GEMV epilogue adds the residual
+// (attention output projection and FFN down projection of every layer).
+static bool try_fuse_mm_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
+    if (i + 1 >= g->n_nodes) return false;
+    ggml_tensor * mm = g->nodes[i];
+    ggml_tensor * add = g->nodes[i + 1];
+    if (add->op != GGML_OP_ADD) return false;
+    const ggml_tensor * res = add->src[0] == mm ? add->src[1] : (add->src[1] == mm ? add->src[0] : nullptr);
+    if (!res || res == mm || uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return false;
+    if (!mmvq_small_batch_ok(mm)) return false;
+    act_cache_invalidate(c.s, add);
+    return mmvq_fused_add(c, mm, res, add);
 }
 
 // MUL_MAT(gate) , MUL_MAT(up) , GLU(gate, up) with one activation column:
@@ -87,6 +210,7 @@ static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     else if (glu->src[0] == b && glu->src[1] == a) { gate = b; up = a; }
     else return false;
     if (uses[a] != 1 || uses[b] != 1 || ((a->flags | b->flags) & GGML_TENSOR_FLAG_OUTPUT)) return false;
+    act_cache_invalidate(c.s, glu);
     return mmvq_fused_glu(c, gate, up, glu);
 }
 
@@ -129,14 +253,24 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             for (int k = 0; k < GGML_MAX_SRC; ++k)
                 if (g->nodes[i]->src[k]) uses[g->nodes[i]->src[k]]++;
     }
+    act_cache_reset(s);
+    s->deferred.clear();
     for (int i = 0; i < g->n_nodes; ++i) {
         ggml_tensor * n = g->nodes[i];
         if (is_view_op(n->op) || mx_is_empty(n)) continue;
         s->scratch.reset();
         if (s->use_fusion) {
+            if (n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }
             if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
+            if (n->op == GGML_OP_MUL_MAT && !g_no_qkv) {
+                const int k = fuse_qkv_rope_store(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; continue; }
+            }
             if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
+            if (n->op == GGML_OP_MUL_MAT && try_fuse_mm_add(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
         }
+        deferred_guard_node(c, n);
+        act_cache_invalidate(s, n);
         run_node(c, n);
         s->n_nodes_run++;
         if (g_sync_debug) {
@@ -144,6 +278,8 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             if (e != hipSuccess) MX_ABORT("node %d (%s, op %d) failed: %s", i, n->name, (int) n->op, hipGetErrorString(e));
         }
     }
+    // every consumer of a deferred norm has run by now; nothing is left pending
+    s->deferred.clear();
     HIP_CHECK(hipGetLastError());
 }
 
@@ -152,8 +288,20 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     s->n_graph_compute++;
     if (s->abort_cb && s->abort_cb(s->abort_data)) { *status = GGML_STATUS_ABORTED; return; }
 
-    size_t need = 0;
-    for (int i = 0; i < g->n_nodes; ++i) need = std::max(need, scratch_bytes(g->nodes[i]));
+    size_t need = 0, slot = 0;
+    for (int i = 0; i < g->n_nodes; ++i) {
+        need = std::max(need, scratch_bytes(g->nodes[i]));
+        if (g->nodes[i]->op == GGML_OP_MUL_MAT && mmvq_small_batch_ok(g->nodes[i])) slot = std::max(slot, act_slot_bytes(g->nodes[i]->src[1]));
+        if (g->nodes[i]->op == GGML_OP_MUL && mx_nrows(g->nodes[i]) <= 8) slot = std::max(slot, act_slot_bytes(g->nodes[i]));
+    }
+    if (slot > s->act_slot) {
+        HIP_CHECK(hipStreamSynchronize(s->stream));
+        if (s->act.base) HIP_CHECK(hipFree(s->act.base));
+        s->act_slot = (slot + 4095) & ~(size_t) 4095;
+        HIP_CHECK(hipMalloc((void **) &s->act.base, 4 * s->act_slot));
+        s->act.cap = 4 * s->act_slot;
+        s->gcache.key.clear();
+    }
     if (need > s->scratch.cap) {
         HIP_CHECK(hipStreamSynchronize(s->stream));
         if (s->scratch.base) HIP_CHECK(hipFree(s->scratch.base));

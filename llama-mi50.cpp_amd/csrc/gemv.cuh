@@ -1,0 +1,340 @@
+// gemv.cuh — building blocks of the single-column decode GEMV (y = W·x, one token),
+// the hot loop of llama-bench tg (reference: mul_mat_vec_q, ggml-cuda/mmvq.cu:142-356,
+// vec_dot_q*_K_q8_1 vecdotq.cuh:461-867).
+//
+// MI355X design (v2)
+//  * prologue: every workgroup reads the f32 activation x (L2-resident, written by the
+//    previous kernel), optionally applies the RMS norm · weight that precedes it in the
+//    graph (build_norm, src/llama-graph.cpp), and quantises it into LDS: int8 q[K],
+//    f32 d[K/32] and d·Σq [K/32] (quantize_q8_1 semantics, ggml-cuda/quantize.cu:5-48,
+//    with the CPU's s = d·Σq, ggml-quants.c:270-300). No separate quantise or norm
+//    launch, no global round trip of the quantised activation;
+//  * the weight loads of all a lane's units are issued before the prologue runs, so the
+//    HBM latency overlaps the x read and the LDS fill;
+//  * a "unit" is 64 weights of a K-quant super-block (Q4_K/Q5_K: one 6-bit scale pair,
+//    Q6_K: four 16-wide runs) or one 32-weight block (Q4_0/Q8_0); loads are 16-byte
+//    (dwordx4) even where the block is only 2-byte aligned (gfx950 global loads need no
+//    natural alignment: the compiler itself emits dwordx4 for 2-aligned memcpy);
+//  * int8 dot products with v_dot4_i32_i8, scales in f32, wave64 shuffle reductions.
+#pragma once
+
+#include "common.h"
+#include "quants.cuh"
+#include "gemv.h"
+
+namespace mx {
+
+// ---------------------------------------------------------------------------
+// activation staging
+// ---------------------------------------------------------------------------
+struct LdsAct {
+    int8_t * q;
+    float * d;
+    float * s;
+};
+
+__host__ __device__ inline size_t gemv_lds_bytes(int64_t K) { return (size_t) K + (size_t) (K / 32) * 8 + 64; }
+
+__device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
+    LdsAct a;
+    a.q = (int8_t *) smem;
+    a.d = (float *) (smem + K);
+    a.s = a.d + K / 32;
+    return a;
+}
+
+// quantise 16 values held by this thread; the partner thread (tid ^ 1) holds the other
+// half of the 32-block. Bit-identical to k_quantize_act (amax/127, roundf(x/d)).
+__device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) {
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    const float dd = amax / 127.0f;
+    const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
+    int sum = 0, pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int w = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int qi = (int) roundf(v[4 * j + k] * id);
+            sum += qi;
+            w |= (qi & 0xFF) << (8 * k);
+        }
+        pk[j] = w;
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    *(int4 *) (a.q + 16 * hg) = make_int4(pk[0], pk[1], pk[2], pk[3]);
+    if ((hg & 1) == 0) {
+        a.d[hg >> 1] = dd;
+        a.s[hg >> 1] = dd * (float) sum;
+    }
+}
+
+// Fill LDS with the quantised activation. Block = NT threads, K % 32 == 0.
+// Three sources: a q8 activation already in memory (copied), f32 x (quantised), or
+// f32 x through RMS norm · nw (K <= 2*16*NT: two 16-value halves per thread held
+// across the block reduction).
+template <int NT>
+__device__ __forceinline__ void stage_x(const XStage & xs, int64_t K, LdsAct a, float * red) {
+    const int t = threadIdx.x;
+    const int nhg = (int) (K / 16);
+    if (xs.q8) {
+        const int nq = (int) (K / 16), nb = (int) (K / 32);
+        for (int i = t; i < nq; i += NT) ((int4 *) a.q)[i] = ((const int4 *) xs.q8)[i];
+        for (int i = t; i < nb; i += NT) { a.d[i] = xs.q8d[i]; a.s[i] = xs.q8s[i]; }
+    } else if (xs.norm) {
+        float v[2][16];
+        float ss = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int hg = t + NT * h;
+            if (hg < nhg) {
+#pragma unroll
+                for (int j = 0; j < 16; j += 4) {
+                    const float4 f = *(const float4 *) (xs.x + 16 * hg + j);
+                    v[h][j] = f.x; v[h][j + 1] = f.y; v[h][j + 2] = f.z; v[h][j + 3] = f.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[h][j] = 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) ss += v[h][j] * v[h][j];
+        }
+        ss = wave_sum(ss);
+        if ((t & 63) == 0) red[t >> 6] = ss;
+        __syncthreads();
+        ss = 0.f;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) ss += red[w];
+        const float scale = 1.0f / sqrtf(ss / (float) K + xs.eps);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int hg = t + NT * h;
+            if (hg < nhg) {
+#pragma unroll
+                for (int j = 0; j < 16; j += 4) {
+                    const float4 w = *(const float4 *) (xs.nw + 16 * hg + j);
+                    v[h][j] = (v[h][j] * scale) * w.x; v[h][j + 1] = (v[h][j + 1] * scale) * w.y;
+                    v[h][j + 2] = (v[h][j + 2] * scale) * w.z; v[h][j + 3] = (v[h][j + 3] * scale) * w.w;
+                }
+                q8_half(v[h], hg, a);
+            }
+        }
+    } else {
+        for (int hg0 = 0; hg0 < nhg; hg0 += 2 * NT) {
+            float v[2][16];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int hg = hg0 + t + NT * h;
+                if (hg < nhg) {
+#pragma unroll
+                    for (int j = 0; j < 16; j += 4) {
+                        const float4 f = *(const float4 *) (xs.x + 16 * hg + j);
+                        v[h][j] = f.x; v[h][j + 1] = f.y; v[h][j + 2] = f.z; v[h][j + 3] = f.w;
+                    }
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int hg = hg0 + t + NT * h;
+                if (hg < nhg) q8_half(v[h], hg, a);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// weight units (v2)
+// ---------------------------------------------------------------------------
+template <int QT> struct W2;
+template <> struct W2<GGML_TYPE_Q4_K> { int4 hd, w0, w1; };
+template <> struct W2<GGML_TYPE_Q5_K> { int4 hd, w0, w1, h0, h1; };
+template <> struct W2<GGML_TYPE_Q6_K> { int4 la, lb, qh, sc; uint16_t d; };
+template <> struct W2<GGML_TYPE_Q4_0> { int4 w; uint16_t d; };
+template <> struct W2<GGML_TYPE_Q8_0> { int4 w0, w1; uint16_t d; };
+
+template <int QT> __host__ __device__ constexpr int unit_w() {   // weights per unit
+    return (QT == GGML_TYPE_Q4_0 || QT == GGML_TYPE_Q8_0) ? 32 : 64;
+}
+
+__device__ __forceinline__ int4 ld_a4(const void * p) { return *(const int4 *) p; }
+__device__ __forceinline__ int4 ldu4(const char * p) {   // 16-byte load, any 2-byte alignment
+    int4 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 2), 16);
+    return v;
+}
+
+template <int QT>
+__device__ __forceinline__ void w2_load(const char * __restrict__ row, int u, W2<QT> & r) {
+    if constexpr (QT == GGML_TYPE_Q4_K) {
+        const char * b = row + (int64_t) (u >> 2) * 144;
+        const int g = u & 3;
+        r.hd = ld_a4(b);
+        r.w0 = ld_a4(b + 16 + 32 * g);
+        r.w1 = ld_a4(b + 32 + 32 * g);
+    } else if constexpr (QT == GGML_TYPE_Q5_K) {
+        const char * b = row + (int64_t) (u >> 2) * 176;
+        const int g = u & 3;
+        r.hd = ld_a4(b);
+        r.h0 = ld_a4(b + 16);
+        r.h1 = ld_a4(b + 32);
+        r.w0 = ld_a4(b + 48 + 32 * g);
+        r.w1 = ld_a4(b + 64 + 32 * g);
+    } else if constexpr (QT == GGML_TYPE_Q6_K) {
+        const char * b = row + (int64_t) (u >> 2) * 210;
+        const int n = (u >> 1) & 1, hl = u & 1;
+        r.la = ldu4(b + 64 * n + 16 * hl);
+        r.lb = ldu4(b + 64 * n + 32 + 16 * hl);
+        r.qh = ldu4(b + 128 + 32 * n + 16 * hl);
+        r.sc = ldu4(b + 192);
+        r.d = ld_u16(b + 208);
+    } else if constexpr (QT == GGML_TYPE_Q4_0) {
+        const char * b = row + (int64_t) u * 18;
+        r.d = ld_u16(b);
+        r.w = ldu4(b + 2);
+    } else if constexpr (QT == GGML_TYPE_Q8_0) {
+        const char * b = row + (int64_t) u * 34;
+        r.d = ld_u16(b);
+        r.w0 = ldu4(b + 2);
+        r.w1 = ldu4(b + 18);
+    }
+}
+
+__device__ __forceinline__ int dot16(const int (&w)[4], int4 a, int acc) {
+    acc = dot4_i8(w[0], a.x, acc); acc = dot4_i8(w[1], a.y, acc);
+    acc = dot4_i8(w[2], a.z, acc); acc = dot4_i8(w[3], a.w, acc);
+    return acc;
+}
+
+template <int QT>
+__device__ __forceinline__ float w2_dot(const W2<QT> & r, int u, const LdsAct & a) {
+    if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
+        const int sb = u >> 2, g = u & 3;
+        const uint32_t s0 = (uint32_t) r.hd.y, s1 = (uint32_t) r.hd.z, s2 = (uint32_t) r.hd.w;
+        auto byte = [&](int j) -> int {
+            const uint32_t v = j < 4 ? s0 : (j < 8 ? s1 : s2);
+            return (v >> (8 * (j & 3))) & 0xFF;
+        };
+        int sc[2], mn[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {   // get_scale_min_k4 (ggml-quants.c:703)
+            const int j = 2 * g + t;
+            if (j < 4) { sc[t] = byte(j) & 63; mn[t] = byte(j + 4) & 63; }
+            else { sc[t] = (byte(j + 4) & 0xF) | ((byte(j - 4) >> 6) << 4); mn[t] = (byte(j + 4) >> 4) | ((byte(j) >> 6) << 4); }
+        }
+        const float d = h2f((uint16_t) (r.hd.x & 0xFFFF)), dmin = h2f((uint16_t) ((uint32_t) r.hd.x >> 16));
+        const int wv[8] = {r.w0.x, r.w0.y, r.w0.z, r.w0.w, r.w1.x, r.w1.y, r.w1.z, r.w1.w};
+        int lo[2][4], hi[2][4];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            lo[k >> 2][k & 3] = wv[k] & 0x0F0F0F0F;
+            hi[k >> 2][k & 3] = (wv[k] >> 4) & 0x0F0F0F0F;
+        }
+        if constexpr (QT == GGML_TYPE_Q5_K) {
+            const int hv[8] = {r.h0.x, r.h0.y, r.h0.z, r.h0.w, r.h1.x, r.h1.y, r.h1.z, r.h1.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                lo[k >> 2][k & 3] |= ((hv[k] >> (2 * g)) & 0x01010101) << 4;
+                hi[k >> 2][k & 3] |= ((hv[k] >> (2 * g + 1)) & 0x01010101) << 4;
+            }
+        }
+        const int e0 = sb * 256 + 64 * g;
+        const int4 * aq = (const int4 *) (a.q + e0);
+        int d0 = 0, d1 = 0;
+        d0 = dot16(lo[0], aq[0], d0); d0 = dot16(lo[1], aq[1], d0);
+        d1 = dot16(hi[0], aq[2], d1); d1 = dot16(hi[1], aq[3], d1);
+        const int b0 = e0 >> 5;
+        const float2 ad = *(const float2 *) (a.d + b0);
+        const float2 as = *(const float2 *) (a.s + b0);
+        return d * ((float) sc[0] * ad.x * (float) d0 + (float) sc[1] * ad.y * (float) d1)
+             - dmin * ((float) mn[0] * as.x + (float) mn[1] * as.y);
+    } else if constexpr (QT == GGML_TYPE_Q6_K) {
+        const int sb = u >> 2, n = (u >> 1) & 1, hl = u & 1;
+        const int la[4] = {r.la.x, r.la.y, r.la.z, r.la.w};
+        const int lb[4] = {r.lb.x, r.lb.y, r.lb.z, r.lb.w};
+        const int qh[4] = {r.qh.x, r.qh.y, r.qh.z, r.qh.w};
+        int q[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            q[0][k] = (la[k] & 0x0F0F0F0F) | (((qh[k] >> 0) & 0x03030303) << 4);
+            q[1][k] = (lb[k] & 0x0F0F0F0F) | (((qh[k] >> 2) & 0x03030303) << 4);
+            q[2][k] = ((la[k] >> 4) & 0x0F0F0F0F) | (((qh[k] >> 4) & 0x03030303) << 4);
+            q[3][k] = ((lb[k] >> 4) & 0x0F0F0F0F) | (((qh[k] >> 6) & 0x03030303) << 4);
+        }
+        // scales sc[8n + hl + 2qq]: byte (8n + hl + 2qq) of the 16 scale bytes
+        const int scw[4] = {r.sc.x, r.sc.y, r.sc.z, r.sc.w};
+        const int e0 = sb * 256 + 128 * n + 16 * hl;
+        float v = 0.f;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const int si = 8 * n + hl + 2 * qq;
+            const int scv = (int) (int8_t) ((scw[si >> 2] >> (8 * (si & 3))) & 0xFF);
+            const int4 av = *(const int4 *) (a.q + e0 + 32 * qq);
+            int dt = dot16(q[qq], av, 0);
+            int sm = 0;
+            sm = dot4_i8(0x20202020, av.x, sm); sm = dot4_i8(0x20202020, av.y, sm);
+            sm = dot4_i8(0x20202020, av.z, sm); sm = dot4_i8(0x20202020, av.w, sm);
+            v += (float) scv * a.d[(e0 >> 5) + qq] * (float) (dt - sm);
+        }
+        return h2f(r.d) * v;
+    } else if constexpr (QT == GGML_TYPE_Q4_0) {
+        const int w[4] = {r.w.x, r.w.y, r.w.z, r.w.w};
+        int lo[4], hi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { lo[k] = w[k] & 0x0F0F0F0F; hi[k] = (w[k] >> 4) & 0x0F0F0F0F; }
+        const int4 * aq = (const int4 *) (a.q + 32 * u);
+        int dt = dot16(lo, aq[0], 0);
+        dt = dot16(hi, aq[1], dt);
+        return h2f(r.d) * (a.d[u] * (float) dt - 8.0f * a.s[u]);
+    } else if constexpr (QT == GGML_TYPE_Q8_0) {
+        const int w0[4] = {r.w0.x, r.w0.y, r.w0.z, r.w0.w};
+        const int w1[4] = {r.w1.x, r.w1.y, r.w1.z, r.w1.w};
+        const int4 * aq = (const int4 *) (a.q + 32 * u);
+        int dt = dot16(w0, aq[0], 0);
+        dt = dot16(w1, aq[1], dt);
+        return h2f(r.d) * a.d[u] * (float) dt;
+    }
+    return 0.f;
+}
+
+template <int QT> __host__ __device__ constexpr bool gemv2_type_ok() {
+    return QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K || QT == GGML_TYPE_Q6_K || QT == GGML_TYPE_Q4_0 || QT == GGML_TYPE_Q8_0;
+}
+
+// One row's partial dot over its units, LPR lanes per row, UPL units per lane in
+// flight; weight loads for the first batch are issued before `stage` runs.
+template <int QT, int LPR, int UPL, int NM, typename Stage>
+__device__ __forceinline__ void gemv_rows(const char * const (&rows)[NM], int units, int sub, const LdsAct & a,
+                                          Stage && stage, float (&acc)[NM]) {
+    W2<QT> r[NM][UPL];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) acc[m] = 0.f;
+    // block-uniform trip count: stage() holds a barrier
+    const int n_iter = (units + LPR * UPL - 1) / (LPR * UPL);
+    for (int it = 0; it < n_iter; ++it) {
+        const int u0 = it * LPR * UPL + sub;
+#pragma unroll
+        for (int j = 0; j < UPL; ++j)
+#pragma unroll
+            for (int m = 0; m < NM; ++m) w2_load<QT>(rows[m], min(u0 + j * LPR, units - 1), r[m][j]);
+        if (it == 0) stage();
+#pragma unroll
+        for (int j = 0; j < UPL; ++j) {
+            if (u0 + j * LPR < units) {
+#pragma unroll
+                for (int m = 0; m < NM; ++m) acc[m] += w2_dot<QT>(r[m][j], u0 + j * LPR, a);
+            }
+        }
+    }
+    if (n_iter == 0) stage();
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) acc[m] += __shfl_xor(acc[m], o, 64);
+}
+
+}  // namespace mx

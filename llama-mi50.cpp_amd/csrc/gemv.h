@@ -1,0 +1,46 @@
+// gemv.h — host interface of the single-token decode GEMV v2 (ops_gemv.hip) and of
+// the executor's deferred RMS norm that the GEMV prologue absorbs.
+#pragma once
+#include "backend.h"
+#include <initializer_list>
+
+namespace mx {
+
+constexpr int64_t GEMV2_MAX_K = 32768;      // LDS: K + K/4 bytes per workgroup
+constexpr int64_t GEMV2_MAX_NORM_K = 8192;  // fused RMS norm keeps 32 values per thread (256 threads)
+
+// f32 activation source of a GEMV; norm != 0: x -> (x * rsqrt(mean(x^2) + eps)) * nw
+struct XStage {
+    const float * x;
+    const float * nw;
+    float eps;
+    int norm;
+    const int8_t * q8 = nullptr;    // q8 activation already in memory (act cache):
+    const float * q8d = nullptr;    //   copied, not recomputed
+    const float * q8s = nullptr;
+};
+
+extern int g_tune[16];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)
+extern bool g_gemv2;        // v2 GEMV enabled (GGML_MI355X_GEMV_V1 turns it off)
+
+bool gemv2_type_ok(int t);
+bool gemv2_ok(const ggml_tensor * w, const ggml_tensor * x, const ggml_tensor * dst);
+// dst[r] = epi(W[r]·x): w2 != null → silu(W·x)*(W2·x); res != null → + res[r].
+// q8out (SwiGLU only, rows % 32 == 0): also write the q8 form of dst there.
+void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, const XStage & xs, float * dst,
+                  const float * res, ActQ * q8out = nullptr);
+
+// The activation a GEMV should stage for src1: the deferred RMS_NORM→MUL pair that
+// produces src1 when there is one (exec.cpp), else src1 itself.
+XStage xstage_of(Stream * s, const ggml_tensor * src1);
+// materialise every deferred norm whose input/weight/output memory `t` overlaps
+void deferred_guard_write(OpCtx & c, const ggml_tensor * t);
+// materialise every deferred norm whose output `t` reads
+void deferred_guard_read(OpCtx & c, const ggml_tensor * t);
+// Activation staging for a fused GEMV that writes `outs` (and reads `reads`): guards the
+// deferred norms, then fails when an output overlaps what the prologue reads (the
+// workgroups would race) — the caller then takes the quantise-first path.
+bool gemv2_stage(OpCtx & c, const ggml_tensor * x, std::initializer_list<const ggml_tensor *> outs,
+                 std::initializer_list<const ggml_tensor *> reads, XStage * xs);
+
+}  // namespace mx

@@ -104,7 +104,7 @@ bool gguf_read(const char * path, Gguf & g) {
         ok = rd_str(f, tt.name) && rd(f, &nd, 4) && nd <= 4;
         for (int d = 0; d < 4; ++d) tt.ne[d] = 1;
         for (uint32_t d = 0; ok && d < nd; ++d) { uint64_t v; ok = rd(f, &v, 8); tt.ne[d] = (int64_t) v; }
-        uint32_t ty;
+        uint32_t ty = 0;
         ok = ok && rd(f, &ty, 4) && rd(f, &tt.offset, 8);
         tt.type = (int) ty;
         g.tensors.push_back(tt);
@@ -311,6 +311,22 @@ static void add_bytes(const ggml_tensor * t, int64_t * acc, int64_t * by_type) {
     const int64_t b = (int64_t) mx_nbytes(t);
     *acc += b;
     if (by_type) by_type[t->type] += b;
+}
+
+ggml_tensor * mxr_model_layer_tensor(const mxr_model * m, int32_t il, const char * which) {
+    if (!m || il < 0 || il >= (int32_t) m->layers.size() || !which) return nullptr;
+    const Layer & L = m->layers[il];
+    const std::string w = which;
+    if (w == "attn_norm") return L.attn_norm;
+    if (w == "attn_q") return L.wq;
+    if (w == "attn_k") return L.wk;
+    if (w == "attn_v") return L.wv;
+    if (w == "attn_output") return L.wo;
+    if (w == "ffn_norm") return L.ffn_norm;
+    if (w == "ffn_gate") return L.gate;
+    if (w == "ffn_up") return L.up;
+    if (w == "ffn_down") return L.down;
+    return nullptr;
 }
 
 int64_t mxr_model_decode_bytes(const mxr_model * m) {

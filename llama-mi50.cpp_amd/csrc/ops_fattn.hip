@@ -13,6 +13,7 @@
 // reads), block softmax update, then threads over (head, dim) accumulate P·V with
 // coalesced V row reads. Splits are merged by a combine kernel.
 #include "backend.h"
+#include <type_traits>
 
 namespace mx {
 
@@ -180,39 +181,279 @@ __global__ __launch_bounds__(256) void k_fattn(FaArgs p) {
     }
 }
 
-template <int D>
-__global__ void k_fattn_combine(const float * __restrict__ op, const float * __restrict__ mp, const float * __restrict__ lp,
-                                const float * __restrict__ sinks, char * __restrict__ dst, size_t nb1, size_t nb2, size_t nb3,
-                                int64_t nrows, int64_t nsplit, int64_t H, int64_t n_q) {
-    const int64_t r = blockIdx.x;          // (iq3, iq1, h)
-    const int64_t h = r % H, iq1 = (r / H) % n_q, iq3 = r / (H * n_q);
-    float m = -INFINITY;
-    for (int64_t s = 0; s < nsplit; ++s) m = fmaxf(m, mp[s * nrows + r]);
-    float sk = 0.f;
-    const bool has_sink = sinks != nullptr;
-    if (has_sink) { sk = sinks[h]; m = fmaxf(m, sk); }
-    float l = 0.f;
-    for (int64_t s = 0; s < nsplit; ++s) {
-        const float ms = mp[s * nrows + r];
-        if (ms != -INFINITY) l += lp[s * nrows + r] * expf(ms - m);
+// ---------------------------------------------------------------------------
+// Decode kernel (n_q <= 4, f16 K/V): one block = (query row, KV head, 256-key split),
+// the G query heads of the KV head together (G compile-time). Wave w owns keys
+// [64w, 64w+64) of the split, one key per lane: the lane's K row and (D <= 128) its
+// wave's V rows are all loaded before any arithmetic. Per wave: scores for the G heads
+// (q broadcast from LDS), wave softmax, P·V with lanes over head dims; the four waves
+// merge in LDS (flash-decoding inside the block). A single split (n_kv <= 256, every
+// tg128 step) writes the output directly: no combine launch. Longer caches write
+// partials (unnormalised O, m, l) for k_fattn_combine.
+// ---------------------------------------------------------------------------
+constexpr int FW_CH = 256;
+
+struct FaOut {
+    const float * sinks;
+    char * dst; size_t nb1, nb2, nb3;
+    int direct;
+};
+
+__device__ __forceinline__ void h8(const uint4 v, float (&f)[8]) {
+    f[0] = h2f((uint16_t) (v.x & 0xFFFF)); f[1] = h2f((uint16_t) (v.x >> 16));
+    f[2] = h2f((uint16_t) (v.y & 0xFFFF)); f[3] = h2f((uint16_t) (v.y >> 16));
+    f[4] = h2f((uint16_t) (v.z & 0xFFFF)); f[5] = h2f((uint16_t) (v.z >> 16));
+    f[6] = h2f((uint16_t) (v.w & 0xFFFF)); f[7] = h2f((uint16_t) (v.w >> 16));
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
+    static_assert(D % 64 == 0 && D <= 256, "decode FA head size");
+    constexpr int NKL = D / 8;                 // 16-byte K loads per lane (its key's row)
+    constexpr int D8 = D / 8;                  // 16-byte chunks of a V row
+    constexpr int KQ = 64 / D8;                // key subsets of a wave in P·V
+    constexpr int KPL = 64 / KQ;               // V rows per lane
+    constexpr bool V_EARLY = D <= 128;         // V loads issued with K (register budget)
+    __shared__ float qs[G][D];
+    __shared__ float pw[4][G][64];
+    __shared__ float wm[4][G], wl[4][G];
+    __shared__ float wo[4][G][D];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Hkv = (int) p.Hkv, n_q = (int) p.n_q, n_kv = (int) p.n_kv;
+    const int bx = blockIdx.x;
+    const int hk = bx % Hkv;
+    const int iq1 = (bx / Hkv) % n_q;
+    const int iq3 = bx / (Hkv * n_q);
+    const int split = blockIdx.y;
+    const int kw0 = split * FW_CH + wave * 64;          // first key of this wave
+    const int key = kw0 + lane;
+    const char * kb = p.k + hk * p.k2 + (iq3 % (int) p.ns) * p.k3;
+    const char * vb = p.v + hk * p.v2 + (iq3 % (int) p.ns) * p.v3;
+    const int vc = lane % D8, vq = lane / D8;           // P·V: 16-byte chunk, key subset
+
+    uint4 kr[NKL];
+    {
+        const uint4 * src = (const uint4 *) (kb + (size_t) min(key, n_kv - 1) * p.k1);
+#pragma unroll
+        for (int j = 0; j < NKL; ++j) kr[j] = src[j];
     }
-    if (has_sink) l += expf(sk - m);
-    const float inv = l == 0.f ? 0.f : 1.0f / l;
-    float * out = (float *) (dst + h * nb1 + iq1 * nb2 + iq3 * nb3);
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-        float o = 0.f;
-        for (int64_t s = 0; s < nsplit; ++s) {
-            const float ms = mp[s * nrows + r];
-            if (ms != -INFINITY) o += op[(s * nrows + r) * D + d] * expf(ms - m);
+    uint4 vr[KPL];
+    auto load_v = [&] {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j)
+            vr[j] = *(const uint4 *) (vb + (size_t) min(kw0 + vq * KPL + j, n_kv - 1) * p.v1 + vc * 16);
+    };
+    if constexpr (V_EARLY) load_v();
+    const bool live = key < n_kv;
+    float mv = 0.f;
+    if (p.mask && live) mv = h2f(((const uint16_t *) (p.mask + iq1 * p.m1 + (iq3 % (int) p.mne3) * p.m3))[key]);
+    for (int i = tid; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        const float x = *(const float *) (p.q + iq1 * p.q1 + (hk * G + g) * p.q2 + iq3 * p.q3 + d * 4);
+        qs[g][d] = (float) (_Float16) x;   // the CPU vec-dot rounds q to the K type
+    }
+    __syncthreads();
+    if constexpr (!V_EARLY) load_v();
+    // ---- scores (lane = key) and wave softmax, one head at a time (bounded live ranges)
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < NKL; ++j) {
+            float kv[8];
+            h8(kr[j], kv);
+            const float4 q0 = *(const float4 *) &qs[g][8 * j];
+            const float4 q1 = *(const float4 *) &qs[g][8 * j + 4];
+            acc += q0.x * kv[0] + q0.y * kv[1] + q0.z * kv[2] + q0.w * kv[3]
+                 + q1.x * kv[4] + q1.y * kv[5] + q1.z * kv[6] + q1.w * kv[7];
         }
-        out[d] = o * inv;
+        float s = -INFINITY;
+        const int h = hk * G + g;
+        float m = mv;
+        if (p.mask && p.mne2 > 1)
+            m = live ? h2f(((const uint16_t *) (p.mask + iq1 * p.m1 + (h % (int) p.mne2) * p.m2 + (iq3 % (int) p.mne3) * p.m3))[key]) : 0.f;
+        if (p.max_bias > 0.0f)
+            m *= (uint32_t) h < p.n_head_log2 ? powf(p.m0, h + 1) : powf(p.m1f, 2 * (h - (int) p.n_head_log2) + 1);
+        if (live && m != -INFINITY) {
+            float x = acc * p.scale;
+            if (p.softcap != 0.0f) x = p.softcap * tanhf(x);
+            s = x + m;
+        }
+        const float mx = wave_max(s);
+        const float e = mx == -INFINITY ? 0.f : expf(s - mx);
+        const float l = wave_sum(e);
+        pw[wave][g][lane] = e;
+        if (lane == 0) { wm[wave][g] = mx; wl[wave][g] = l; }
     }
+    __syncthreads();
+    // ---- P·V: lane = (16-byte chunk vc, key subset vq), one head at a time
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            float v[8];
+            h8(vr[j], v);
+            const float w = pw[wave][g][vq * KPL + j];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] += w * v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int off = D8; off < 64; off <<= 1) o[i] += __shfl_xor(o[i], off, 64);
+        if (vq == 0) {
+            *(float4 *) &wo[wave][g][vc * 8] = make_float4(o[0], o[1], o[2], o[3]);
+            *(float4 *) &wo[wave][g][vc * 8 + 4] = make_float4(o[4], o[5], o[6], o[7]);
+        }
+    }
+    __syncthreads();
+    // ---- merge the four waves
+    const int rows = (int) (p.ns * p.n_q * p.H);
+    const int row0 = (iq3 * n_q + iq1) * (int) p.H + hk * G;
+    for (int i = tid; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        float M = fmaxf(fmaxf(wm[0][g], wm[1][g]), fmaxf(wm[2][g], wm[3][g]));
+        const int h = hk * G + g;
+        const float sk = (fo.direct && fo.sinks) ? fo.sinks[h] : -INFINITY;
+        M = fmaxf(M, sk);
+        float L = 0.f, O = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const float f = wm[w][g] == -INFINITY ? 0.f : expf(wm[w][g] - M);
+            L += wl[w][g] * f;
+            O += wo[w][g][d] * f;
+        }
+        if (sk != -INFINITY) L += expf(sk - M);
+        if (fo.direct) {
+            float * out = (float *) (fo.dst + h * fo.nb1 + iq1 * fo.nb2 + iq3 * fo.nb3);
+            out[d] = L == 0.f ? 0.f : O / L;
+        } else {
+            p.opart[((size_t) split * rows + row0 + g) * D + d] = O;
+            if (d == 0) {
+                p.mpart[split * rows + row0 + g] = M;
+                p.lpart[split * rows + row0 + g] = L;
+            }
+        }
+    }
+}
+
+// Merge the split partials of one output row (block = row, 64 threads). All loads of
+// the first 8 splits are issued before any arithmetic: one memory round trip.
+template <int D>
+__global__ __launch_bounds__(64) void k_fattn_combine(const float * __restrict__ op, const float * __restrict__ mp, const float * __restrict__ lp,
+                                const float * __restrict__ sinks, char * __restrict__ dst, size_t nb1, size_t nb2, size_t nb3,
+                                int64_t nrows_, int64_t nsplit_, int64_t H, int64_t n_q,
+                                int8_t * __restrict__ q8, float * __restrict__ q8d, float * __restrict__ q8s, int64_t q8kp) {
+    constexpr int DPT = (D + 63) / 64;
+    constexpr int PRE = 8;
+    const int nrows = (int) nrows_, nsplit = (int) nsplit_;
+    const int r = blockIdx.x;          // (iq3, iq1, h)
+    const int lane = threadIdx.x;
+    const int h = r % (int) H, iq1 = (r / (int) H) % (int) n_q, iq3 = r / (int) (H * n_q);
+    float ov[PRE][DPT];
+#pragma unroll
+    for (int s = 0; s < PRE; ++s)
+#pragma unroll
+        for (int i = 0; i < DPT; ++i) {
+            const int d = lane + 64 * i;
+            ov[s][i] = (s < nsplit && d < D) ? op[((size_t) s * nrows + r) * D + d] : 0.f;
+        }
+    // per-split maxima and sums: lane s holds split s (splits >= 64 fold into lane s % 64)
+    float m_l = -INFINITY;
+    for (int s = lane; s < nsplit; s += 64) m_l = fmaxf(m_l, mp[(size_t) s * nrows + r]);
+    float M = wave_max(m_l);
+    const bool has_sink = sinks != nullptr;
+    const float sk = has_sink ? sinks[h] : 0.f;
+    if (has_sink) M = fmaxf(M, sk);
+    float l_l = 0.f;
+    for (int s = lane; s < nsplit; s += 64) {
+        const float ms = mp[(size_t) s * nrows + r];
+        if (ms != -INFINITY) l_l += lp[(size_t) s * nrows + r] * expf(ms - M);
+    }
+    float L = wave_sum(l_l);
+    if (has_sink) L += expf(sk - M);
+    const float inv = L == 0.f ? 0.f : 1.0f / L;
+    float o[DPT];
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) o[i] = 0.f;
+    for (int s0 = 0; s0 < nsplit; s0 += PRE) {
+        if (s0 > 0) {
+#pragma unroll
+            for (int s = 0; s < PRE; ++s)
+#pragma unroll
+                for (int i = 0; i < DPT; ++i) {
+                    const int d = lane + 64 * i;
+                    ov[s][i] = (s0 + s < nsplit && d < D) ? op[((size_t) (s0 + s) * nrows + r) * D + d] : 0.f;
+                }
+        }
+#pragma unroll
+        for (int s = 0; s < PRE; ++s) {
+            if (s0 + s >= nsplit) break;
+            const float ms = mp[(size_t) (s0 + s) * nrows + r];
+            const float w = ms == -INFINITY ? 0.f : expf(ms - M);
+#pragma unroll
+            for (int i = 0; i < DPT; ++i) o[i] += w * ov[s][i];
+        }
+    }
+    float * out = (float *) (dst + h * nb1 + iq1 * nb2 + iq3 * nb3);
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+        const int d = lane + 64 * i;
+        const float v = o[i] * inv;
+        if (d < D) out[d] = v;
+        if (q8 && (D % 32) == 0) {
+            // q8 form of the attention output row (the multi-column GEMV input):
+            // column = query row, element = h*D + d, one 32-block per half-wave
+            float amax = d < D ? fabsf(v) : 0.f;
+#pragma unroll
+            for (int off = 16; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 32));
+            const float dd = amax / 127.0f;
+            const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
+            const int qi = (int) roundf(v * id);
+            int sum = qi;
+#pragma unroll
+            for (int off = 16; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 32);
+            if (d < D) {
+                const int64_t col = (int64_t) iq3 * n_q + iq1;
+                const int64_t e = (int64_t) h * D + d;
+                q8[col * q8kp + e] = (int8_t) qi;
+                if ((lane & 31) == 0) {
+                    q8d[col * (q8kp / 32) + e / 32] = dd;
+                    q8s[col * (q8kp / 32) + e / 32] = dd * (float) sum;
+                }
+            }
+        }
+    }
+}
+
+// decode kernel eligibility: few query rows, f16 K/V with 16-byte aligned rows
+static bool fa_use_dec(const ggml_tensor * dst) {
+    const ggml_tensor * q = dst->src[0];
+    const ggml_tensor * k = dst->src[1];
+    const ggml_tensor * v = dst->src[2];
+    const int64_t D = k->ne[0];
+    if (q->ne[1] > 4 || k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16) return false;
+    if (D != 64 && D != 128 && D != 256) return false;
+    if (k->ne[1] > INT32_MAX / 2) return false;
+    const int64_t G = q->ne[2] / k->ne[2];
+    if (G != 1 && G != 2 && G != 4 && G != 8) return false;
+    if (k->nb[1] % 16 || k->nb[2] % 16 || k->nb[3] % 16 || v->nb[1] % 16 || v->nb[2] % 16 || v->nb[3] % 16) return false;
+    if (k->data && ((uintptr_t) k->data % 16 || (uintptr_t) v->data % 16)) return false;
+    return true;
 }
 
 static int64_t fa_chunk(const ggml_tensor * dst, int64_t * nsplit_out) {
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * k = dst->src[1];
     const int64_t n_kv = k->ne[1];
+    if (fa_use_dec(dst)) {
+        *nsplit_out = mx_ceil_div(n_kv, FW_CH);
+        return FW_CH;
+    }
     const int64_t blocks = q->ne[1] * k->ne[2] * q->ne[3];
     // enough blocks to cover the chip: split KV when there are few query rows
     int64_t nsplit = std::max<int64_t>(1, std::min<int64_t>(mx_ceil_div(n_kv, FA_TILE), mx_ceil_div(512, blocks)));
@@ -303,12 +544,27 @@ void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
     // kernel indexes K/V by (iq3 % ns): pass kv stream count through k3 stride when ns==1
     if (k->ne[3] == 1) { b.k3 = 0; b.v3 = 0; }
     b.k_aligned = ((uintptr_t) k->data % 16 == 0) && k->nb[1] % 16 == 0 && k->nb[2] % 16 == 0 && k->nb[3] % 16 == 0;
-    if (k->type == GGML_TYPE_F16) fa_launch<uint16_t, uint16_t>(c, D, grid, b);
-    else fa_launch<float, float>(c, D, grid, b);
     const float * psk = sk ? (const float *) sk->data : nullptr;
+    if (fa_use_dec(dst)) {
+        const int G = (int) (q->ne[2] / k->ne[2]);
+        const FaOut fo{psk, (char *) dst->data, dst->nb[1], dst->nb[2], dst->nb[3], nsplit == 1};
+#define DEC(DD, GG) if (D == DD && G == GG) k_fattn_dec<DD, GG><<<grid, 256, 0, c.st>>>(b, fo); else
+#define DECG(DD) DEC(DD, 1) DEC(DD, 2) DEC(DD, 4) DEC(DD, 8)
+        DECG(64) DECG(128) DECG(256) MX_ABORT("fattn dec D=%d G=%d", D, G);
+#undef DECG
+#undef DEC
+        if (nsplit == 1) return;
+    } else if (k->type == GGML_TYPE_F16) fa_launch<uint16_t, uint16_t>(c, D, grid, b);
+    else fa_launch<float, float>(c, D, grid, b);
+    // decode: also emit the q8 activation of the output for the O-projection GEMV
+    ActQ * q8 = nullptr;
+    if (D % 32 == 0 && q->ne[1] * q->ne[3] > 1 && q->ne[1] * q->ne[3] <= 8 && mx_is_contiguous(dst))
+        q8 = act_cache_alloc_raw(c.s, dst->data, D * q->ne[2], q->ne[1] * q->ne[3], mx_nbytes(dst));
     switch (D) {
 #define CMB(DD) case DD: k_fattn_combine<DD><<<(unsigned) rows, 64, 0, c.st>>>(a.opart, a.mpart, a.lpart, psk, (char *) dst->data, \
-                                                       dst->nb[1], dst->nb[2], dst->nb[3], rows, nsplit, q->ne[2], q->ne[1]); break;
+                                                       dst->nb[1], dst->nb[2], dst->nb[3], rows, nsplit, q->ne[2], q->ne[1], \
+                                                       q8 ? (int8_t *) q8->q : nullptr, q8 ? (float *) q8->d : nullptr, \
+                                                       q8 ? (float *) q8->s : nullptr, q8 ? q8->kp : 0); break;
         CMB(32) CMB(40) CMB(48) CMB(64) CMB(80) CMB(96) CMB(112) CMB(128) CMB(256)
 #undef CMB
     }

@@ -1,0 +1,159 @@
+// ops_gemv.hip — single-token decode GEMV v2 (gemv.cuh): activation quantised (and
+// optionally RMS-normalised) in each workgroup's prologue, weights streamed with all
+// of a lane's loads in flight. Epilogues: plain store, SwiGLU of two weight streams
+// (ggml-cuda.cu:2145-2181 fusion), residual add (the MUL_MAT→ADD pair of every layer).
+#include "backend.h"
+#include "gemv.cuh"
+
+namespace mx {
+
+int g_tune[16] = {0};
+bool g_gemv2 = getenv("GGML_MI355X_GEMV_V1") == nullptr;
+
+struct G2Args {
+    const char * w; const char * w2;
+    size_t w_row;
+    float * dst; const float * res;
+    int nrows, units, K;
+    XStage xs;
+    int8_t * q8o; float * q8od; float * q8os;   // EPI 1 with 8 waves: q8 form of the output
+};
+
+// EPI 0 store, 1 SwiGLU(w, w2), 2 + residual. W waves per block; with W = 8 and
+// LPR = 16 a block owns 32 consecutive rows and (q8o != null) also emits the q8
+// activation of its 32 outputs for the next GEMV (the FFN down projection).
+template <int QT, int LPR, int UPL, int EPI, int W>
+__global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
+    extern __shared__ __align__(16) char smem[];
+    __shared__ float o32[32];
+    constexpr int NM = EPI == 1 ? 2 : 1;
+    constexpr int RPW = 64 / LPR;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane % LPR;
+    const int row = (blockIdx.x * W + wave) * RPW + lane / LPR;
+    const bool valid = row < p.nrows;
+    const int64_t rr = valid ? row : p.nrows - 1;
+    const char * rows[NM];
+    rows[0] = p.w + rr * p.w_row;
+    if constexpr (NM == 2) rows[1] = p.w2 + rr * p.w_row;
+    const LdsAct a = lds_act(smem, p.K);
+    float * red = (float *) (smem + gemv_lds_bytes(p.K) - 64);
+    float acc[NM];
+    gemv_rows<QT, LPR, UPL, NM>(rows, p.units, sub, a, [&] { stage_x<64 * W>(p.xs, p.K, a, red); }, acc);
+    float v = acc[0];
+    if constexpr (EPI == 1) v = (v / (1.0f + expf(-v))) * acc[1];
+    if constexpr (EPI == 2) v += valid ? p.res[row] : 0.f;
+    if (sub == 0 && valid) p.dst[row] = v;
+    if constexpr (W * RPW == 32) {
+        if (p.q8o) {     // block-uniform
+            if (sub == 0) o32[row & 31] = v;
+            __syncthreads();
+            if (wave == 0 && lane < 32) {
+                const float x = o32[lane];
+                float amax = fabsf(x);
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 32));
+                const float dd = amax / 127.0f;
+                const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
+                const int qi = (int) roundf(x * id);
+                int sum = qi;
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
+                p.q8o[blockIdx.x * 32 + lane] = (int8_t) qi;
+                if (lane == 0) { p.q8od[blockIdx.x] = dd; p.q8os[blockIdx.x] = dd * (float) sum; }
+            }
+        }
+    }
+}
+
+template <int QT, int LPR, int UPL, int EPI, int W = 4>
+static void launch_cfg(hipStream_t st, const G2Args & p) {
+    constexpr int RPB = W * (64 / LPR);
+    const unsigned grid = (unsigned) ((p.nrows + RPB - 1) / RPB);
+    k_gemv2<QT, LPR, UPL, EPI, W><<<grid, 64 * W, gemv_lds_bytes(p.K), st>>>(p);
+}
+
+template <int QT, int EPI>
+static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
+    if constexpr (EPI == 1) {
+        if (p.q8o) return launch_cfg<QT, 16, 2, 1, 8>(st, p);   // 32 rows per block
+    }
+    constexpr bool FULL = QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q6_K;   // full tuning grid
+    if constexpr (FULL) {
+#define CFG(L, U) if (lpr == L && upl == U) return launch_cfg<QT, L, U, EPI>(st, p);
+        CFG(16, 2) CFG(16, 4) CFG(32, 2) CFG(32, 4) CFG(64, 2) CFG(64, 4)
+        if constexpr (EPI != 1) { CFG(16, 8) CFG(32, 8) CFG(64, 8) }
+#undef CFG
+    }
+    constexpr int U = EPI == 1 ? 2 : 4;
+    (void) upl;
+    if (lpr == 16) return launch_cfg<QT, 16, U, EPI>(st, p);
+    if (lpr == 32) return launch_cfg<QT, 32, U, EPI>(st, p);
+    return launch_cfg<QT, 64, U, EPI>(st, p);
+}
+
+static int units_of(int type, int64_t K) {
+    return (int) (K / ((type == GGML_TYPE_Q4_0 || type == GGML_TYPE_Q8_0) ? 32 : 64));
+}
+
+// launch geometry: defaults from the tools/opbench.py sweep on MI355X (profiles/r01/
+// opbench_sweep.txt); g_tune overrides for sweeps
+static void pick_cfg(int type, int units, int nrows, bool glu, int & lpr, int & upl) {
+    if (glu) { lpr = 32; upl = 2; }
+    else if (units >= 128) { lpr = 32; upl = type == GGML_TYPE_Q6_K ? 2 : 4; }
+    else if (nrows <= 2048) { lpr = 64; upl = 2; }
+    else { lpr = 16; upl = 4; }
+    const int base = glu ? 2 : 0;
+    if (g_tune[base]) lpr = g_tune[base];
+    if (g_tune[base + 1]) upl = g_tune[base + 1];
+}
+
+bool gemv2_type_ok(int t) {
+    return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K || t == GGML_TYPE_Q4_0 || t == GGML_TYPE_Q8_0;
+}
+
+bool gemv2_ok(const ggml_tensor * w, const ggml_tensor * x, const ggml_tensor * dst) {
+    if (!gemv2_type_ok(w->type) || x->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
+    const int64_t K = w->ne[0];
+    const int64_t qk = (w->type == GGML_TYPE_Q4_0 || w->type == GGML_TYPE_Q8_0) ? 32 : 256;
+    if (K % qk || K > GEMV2_MAX_K || x->ne[0] != K) return false;
+    if (x->ne[1] * x->ne[2] * x->ne[3] != 1 || w->ne[2] != 1 || w->ne[3] != 1) return false;
+    if (w->nb[0] != (size_t) mx_type(w->type).size || w->ne[1] > INT32_MAX) return false;
+    if (x->nb[0] != 4 || ((uintptr_t) x->data & 15) || dst->nb[0] != 4 || dst->ne[0] != w->ne[1]) return false;
+    return true;
+}
+
+void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, const XStage & xs, float * dst,
+                  const float * res, ActQ * q8out) {
+    G2Args p{};
+    p.w = (const char *) w->data;
+    p.w2 = w2 ? (const char *) w2->data : nullptr;
+    p.w_row = w->nb[1];
+    p.dst = dst;
+    p.res = res;
+    p.nrows = (int) w->ne[1];
+    p.K = (int) w->ne[0];
+    p.units = units_of(w->type, w->ne[0]);
+    p.xs = xs;
+    const bool glu = w2 != nullptr;
+    if (q8out) {
+        MX_ASSERT(glu && p.nrows % 32 == 0);
+        p.q8o = (int8_t *) q8out->q; p.q8od = (float *) q8out->d; p.q8os = (float *) q8out->s;
+    }
+    int lpr, upl;
+    pick_cfg(w->type, p.units, p.nrows, glu, lpr, upl);
+    MX_ASSERT(!(glu && res));
+    const int epi = glu ? 1 : (res ? 2 : 0);
+#define TY(T) case T: \
+        if (epi == 0) launch_type<T, 0>(c.st, p, lpr, upl); \
+        else if (epi == 1) launch_type<T, 1>(c.st, p, lpr, upl); \
+        else launch_type<T, 2>(c.st, p, lpr, upl); \
+        break;
+    switch (w->type) {
+        TY(GGML_TYPE_Q4_K) TY(GGML_TYPE_Q5_K) TY(GGML_TYPE_Q6_K) TY(GGML_TYPE_Q4_0) TY(GGML_TYPE_Q8_0)
+        default: MX_ABORT("gemv2 type %d", w->type);
+    }
+#undef TY
+}
+
+}  // namespace mx

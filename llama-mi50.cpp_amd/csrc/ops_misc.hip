@@ -499,6 +499,90 @@ void op_rms_norm(OpCtx & c, ggml_tensor * norm, const ggml_tensor * mul, ggml_te
     }
 }
 
+// RMS_NORM → MUL(w) for decode rows (≤ 8 rows, ne0 % 32 == 0), writing the f32
+// output AND its q8 form (int8 + per-32 d, d·Σq) that the following GEMVs consume,
+// so no separate activation-quantisation launch is needed (quantize.cu:5-48 semantics).
+__global__ void k_rms_norm_q8(const char * __restrict__ x, const char * __restrict__ w, char * __restrict__ y,
+                              T4 gx, T4 gw, T4 gy, float eps, int8_t * __restrict__ q, float * __restrict__ qd,
+                              float * __restrict__ qs, int64_t kp) {
+    __shared__ float lds[16];
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % gx.ne[1], i2 = (r / gx.ne[1]) % gx.ne[2], i3 = r / (gx.ne[1] * gx.ne[2]);
+    const float * px = (const float *) (x + i1 * gx.nb[1] + i2 * gx.nb[2] + i3 * gx.nb[3]);
+    const float * pw = (const float *) (w + (i1 % gw.ne[1]) * gw.nb[1] + (i2 % gw.ne[2]) * gw.nb[2] + (i3 % gw.ne[3]) * gw.nb[3]);
+    float * py = (float *) (y + i1 * gy.nb[1] + i2 * gy.nb[2] + i3 * gy.nb[3]);
+    const int64_t n = gx.ne[0];
+    const int64_t nchunk = n / 32;
+    // one memory round trip: each thread holds its 32-element chunk of x and w in
+    // registers across the reduction (n <= 32*blockDim; larger rows loop below)
+    const int64_t b0 = threadIdx.x;
+    float xr[32], wr[32];
+    float s = 0.f;
+    if (b0 < nchunk) {
+#pragma unroll
+        for (int j = 0; j < 32; j += 4) {
+            const float4 xv = *(const float4 *) (px + 32 * b0 + j);
+            const float4 wv = *(const float4 *) (pw + 32 * b0 + j);
+            xr[j] = xv.x; xr[j + 1] = xv.y; xr[j + 2] = xv.z; xr[j + 3] = xv.w;
+            wr[j] = wv.x; wr[j + 1] = wv.y; wr[j + 2] = wv.z; wr[j + 3] = wv.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) s += xr[j] * xr[j];
+    }
+    for (int64_t i = 32 * (b0 + blockDim.x); i < n; i += 32 * blockDim.x)
+        for (int j = 0; j < 32; ++j) s += px[i + j] * px[i + j];
+    s = block_sum(s, lds);
+    const float scale = 1.0f / sqrtf(s / (float) n + eps);
+    for (int64_t b = b0; b < nchunk; b += blockDim.x) {
+        float v[32];
+        if (b != b0) {
+            for (int j = 0; j < 32; ++j) { xr[j] = px[32 * b + j]; wr[j] = pw[32 * b + j]; }
+        }
+#pragma unroll
+        for (int j = 0; j < 32; j += 4) {
+            v[j] = (xr[j] * scale) * wr[j]; v[j + 1] = (xr[j + 1] * scale) * wr[j + 1];
+            v[j + 2] = (xr[j + 2] * scale) * wr[j + 2]; v[j + 3] = (xr[j + 3] * scale) * wr[j + 3];
+            *(float4 *) (py + 32 * b + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+        const float dd = amax / 127.0f;
+        const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
+        int sum = 0, packed[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            int wq = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int qi = (int) roundf(v[4 * j + k] * id);
+                sum += qi;
+                wq |= (qi & 0xFF) << (8 * k);
+            }
+            packed[j] = wq;
+        }
+        int4 * out = (int4 *) (q + r * kp + 32 * b);
+        out[0] = make_int4(packed[0], packed[1], packed[2], packed[3]);
+        out[1] = make_int4(packed[4], packed[5], packed[6], packed[7]);
+        qd[r * (kp / 32) + b] = dd;
+        qs[r * (kp / 32) + b] = dd * (float) sum;
+    }
+}
+
+bool rms_norm_mul_q8(OpCtx & c, ggml_tensor * norm, const ggml_tensor * w, ggml_tensor * out) {
+    const ggml_tensor * x = norm->src[0];
+    const int64_t nr = mx_nrows(x);
+    if (nr > 8 || x->ne[0] % 32 != 0 || x->nb[0] != 4 || w->nb[0] != 4 || out->nb[0] != 4) return false;
+    if ((uintptr_t) x->data % 16 || (uintptr_t) w->data % 16 || (uintptr_t) out->data % 16) return false;
+    for (int i = 1; i < 4; ++i) if (x->nb[i] % 16 || w->nb[i] % 16 || out->nb[i] % 16) return false;
+    ActQ * a = act_cache_alloc(c.s, out);
+    if (!a) return false;
+    k_rms_norm_q8<<<(unsigned) nr, 256, 0, c.st>>>((const char *) x->data, (const char *) w->data, (char *) out->data,
+                                                  geo(x), geo(w), geo(out), mx_op_param<float>(norm, 0),
+                                                  (int8_t *) a->q, (float *) a->d, (float *) a->s, a->kp);
+    return true;
+}
+
 __global__ void k_norm(const char * __restrict__ x, char * __restrict__ y, T4 gx, T4 gy, float eps) {
     __shared__ float lds[16];
     const int64_t r = blockIdx.x;

@@ -14,6 +14,7 @@
 //     ds_read_b128 lane group hits 16 distinct bank slots.
 #include "backend.h"
 #include "mm.h"
+#include "gemv.h"
 
 namespace mx {
 
@@ -368,6 +369,10 @@ size_t mul_mat_scratch(const ggml_tensor * dst) {
 
 void op_mul_mat(OpCtx & c, ggml_tensor * dst) {
     const ggml_tensor * x = dst->src[1];
+    if (g_gemv2 && gemv2_ok(dst->src[0], x, dst)) {
+        gemv2_launch(c, dst->src[0], nullptr, xstage_of(c.s, x), (float *) dst->data, nullptr);
+        return;
+    }
     if (x->ne[1] <= 8 && quant_fast_path_ok(dst)) { mmvq_run(c, dst); return; }
     if (x->ne[1] > 8 && mmq_ok(dst)) { mmq_run(c, dst); return; }
     mmv_generic_run(c, dst);

@@ -6,6 +6,7 @@
 #include "backend.h"
 #include "mmvq.cuh"
 #include "mm.h"
+#include "gemv.h"
 
 namespace mx {
 
@@ -58,42 +59,115 @@ __global__ void k_quantize_act(const char * __restrict__ x, int64_t K, int64_t n
     s[col * (kp / 32) + blk] = dd * (float) sum;
 }
 
-ActQ quantize_activations(OpCtx & c, const ggml_tensor * src1) {
+static ActQ quantize_into(OpCtx & c, const ggml_tensor * src1, int8_t * q, float * d, float * s) {
     const int64_t K = src1->ne[0];
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
     const int64_t kp = (K + 31) / 32 * 32;
-    // +8 columns: the GEMV reads NC-padded column groups (NC in {1,2,4,8})
-    int8_t * q = (int8_t *) c.scratch->take((ncols + 8) * kp);
-    float * d = (float *) c.scratch->take((ncols + 8) * (kp / 32) * sizeof(float));
-    float * s = (float *) c.scratch->take((ncols + 8) * (kp / 32) * sizeof(float));
     const int64_t nblk = kp / 32;
-    dim3 grid((unsigned) mx_ceil_div(nblk, 128), (unsigned) ncols);
-    k_quantize_act<<<grid, 128, 0, c.st>>>((const char *) src1->data, K, src1->ne[1], src1->ne[2],
-                                            src1->nb[1], src1->nb[2], src1->nb[3], kp, q, d, s);
+    dim3 grid((unsigned) mx_ceil_div(nblk, 64), (unsigned) ncols);
+    k_quantize_act<<<grid, 64, 0, c.st>>>((const char *) src1->data, K, src1->ne[1], src1->ne[2],
+                                           src1->nb[1], src1->nb[2], src1->nb[3], kp, q, d, s);
     return ActQ{q, d, s, kp};
 }
 
-size_t quantize_scratch(const ggml_tensor * src1) {
+// bytes of one quantised activation set (+8 padding columns: the GEMV reads
+// NC-padded column groups, NC in {1,2,4,8})
+size_t act_slot_bytes(const ggml_tensor * src1) {
     const int64_t ncols = src1->ne[1] * src1->ne[2] * src1->ne[3];
     const int64_t kp = (src1->ne[0] + 31) / 32 * 32;
     return (ncols + 8) * kp + 2 * (ncols + 8) * (kp / 32) * sizeof(float) + 3 * 256;
 }
 
+size_t quantize_scratch(const ggml_tensor * src1) { return act_slot_bytes(src1); }
+
+static ActQ carve_raw(char * base, int64_t ne0, int64_t ncols) {
+    const int64_t kp = (ne0 + 31) / 32 * 32;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t) 255; };
+    char * p = base;
+    int8_t * q = (int8_t *) p; p += al((ncols + 8) * kp);
+    float * d = (float *) p; p += al((ncols + 8) * (kp / 32) * sizeof(float));
+    float * s = (float *) p;
+    return ActQ{q, d, s, kp};
+}
+static ActQ carve(char * base, const ggml_tensor * src1) {
+    return carve_raw(base, src1->ne[0], src1->ne[1] * src1->ne[2] * src1->ne[3]);
+}
+static size_t slot_bytes_raw(int64_t ne0, int64_t ncols) {
+    const int64_t kp = (ne0 + 31) / 32 * 32;
+    return (ncols + 8) * kp + 2 * (ncols + 8) * (kp / 32) * sizeof(float) + 3 * 256;
+}
+
+void act_cache_reset(Stream * s) {
+    for (auto & e : s->act_cache) e = ActCacheEntry{};
+    s->act_next = 0;
+}
+
+void act_cache_invalidate(Stream * s, const ggml_tensor * w) {
+    const char * lo = (const char *) w->data;
+    const char * hi = lo + mx_nbytes(w);
+    for (auto & e : s->act_cache) {
+        if (!e.data) continue;
+        const char * a = (const char *) e.data, * b = a + e.bytes;
+        if (a < hi && lo < b) e = ActCacheEntry{};
+    }
+}
+
+static ActCacheEntry * act_lookup(Stream * s, const ggml_tensor * t) {
+    if (!mx_is_contiguous(t)) return nullptr;
+    const int64_t ncols = t->ne[1] * t->ne[2] * t->ne[3];
+    for (auto & e : s->act_cache)
+        if (e.data && e.data == t->data && e.ne0 == t->ne[0] && e.ncols == ncols) return &e;
+    return nullptr;
+}
+
+const ActQ * act_cache_find(Stream * s, const ggml_tensor * t) {
+    ActCacheEntry * e = act_lookup(s, t);
+    return e ? &e->a : nullptr;
+}
+
+ActQ * act_cache_alloc_raw(Stream * s, const void * data, int64_t ne0, int64_t ncols, size_t bytes) {
+    if (!s->act.base || slot_bytes_raw(ne0, ncols) > s->act_slot) return nullptr;
+    const int slot = s->act_next;
+    s->act_next = (s->act_next + 1) % 4;
+    ActCacheEntry & e = s->act_cache[slot];
+    e.data = data; e.ne0 = ne0; e.ncols = ncols; e.bytes = bytes;
+    e.a = carve_raw(s->act.base + slot * s->act_slot, ne0, ncols);
+    return &e.a;
+}
+
+ActQ * act_cache_alloc(Stream * s, const ggml_tensor * t) {
+    if (!mx_is_contiguous(t)) return nullptr;
+    return act_cache_alloc_raw(s, t->data, t->ne[0], t->ne[1] * t->ne[2] * t->ne[3], mx_nbytes(t));
+}
+
+// quantised activations of src1, shared across the GEMVs of one graph pass
+ActQ quantize_activations(OpCtx & c, const ggml_tensor * src1) {
+    if (ActCacheEntry * e = act_lookup(c.s, src1)) return e->a;
+    if (ActQ * a = act_cache_alloc(c.s, src1)) {
+        return *a = quantize_into(c, src1, (int8_t *) a->q, (float *) a->d, (float *) a->s);
+    }
+    ActQ a = carve((char *) c.scratch->take(act_slot_bytes(src1)), src1);
+    return quantize_into(c, src1, (int8_t *) a.q, (float *) a.d, (float *) a.s);
+}
+
 // ---------------------------------------------------------------------------
-// quantised GEMV. LPR lanes cooperate on one weight row; 4 waves per block.
+// quantised GEMV. LPR lanes cooperate on one weight row (64/LPR rows per wave,
+// 4 waves per block); each lane loads UNR units before computing any.
 // Channel c = blockIdx.y spans (i12, i13); src0 broadcast by r2 = ne12/ne02.
 // ---------------------------------------------------------------------------
 struct MmvArgs {
     const char * w;   size_t w_row, w_c2, w_c3;     // weight base and strides (rows, dim2, dim3)
     const char * w2;                                // second weight (fused GLU up), same geometry
     float * dst;      size_t d_col, d_c2, d_c3;     // dst strides in floats
+    const float * res; size_t r_col;                // fused residual (ADD), same shape as dst
     int64_t nrows, units;
     int64_t ncols;                                  // activation columns per channel (ne11)
     int64_t ne12, r2, r3;
 };
 
-template <int QT, int NC, int LPR, bool GLU>
+template <int QT, int NC, int LPR, int UNR, int EPI>   // EPI: 0 plain, 1 GLU (silu(W·x)*(W2·x)), 2 +residual
 __global__ __launch_bounds__(256) void k_mmvq(MmvArgs p, ActQ a) {
+    constexpr bool GLU = EPI == 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int RPW = 64 / LPR;
     const int64_t row = ((int64_t) blockIdx.x * 4 + wave) * RPW + lane / LPR;
@@ -110,9 +184,25 @@ __global__ __launch_bounds__(256) void k_mmvq(MmvArgs p, ActQ a) {
         const size_t off = (size_t) row * p.w_row + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
         const char * r = p.w + off;
         const char * r2 = GLU ? p.w2 + off : nullptr;
-        for (int u = sub; u < p.units; u += LPR) {
-            unit_dot<QT, NC>(r, u, ac, acc);
-            if constexpr (GLU) unit_dot<QT, NC>(r2, u, ac, acc2);
+        for (int u0 = sub; u0 < p.units; u0 += LPR * UNR) {
+            URegs<QT> rg[UNR];
+            URegs<QT> rg2[GLU ? UNR : 1];
+            // branch-free issue of every weight load (out-of-range units re-read the
+            // last unit and are skipped in the compute loop)
+#pragma unroll
+            for (int j = 0; j < UNR; ++j) {
+                const int u = min(u0 + j * LPR, (int) p.units - 1);
+                unit_load<QT>(r, u, rg[j]);
+                if constexpr (GLU) unit_load<QT>(r2, u, rg2[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < UNR; ++j) {
+                const int u = u0 + j * LPR;
+                if (u < p.units) {
+                    unit_compute<QT, NC>(rg[j], u, ac, acc);
+                    if constexpr (GLU) unit_compute<QT, NC>(rg2[j], u, ac, acc2);
+                }
+            }
         }
     }
 #pragma unroll
@@ -130,35 +220,45 @@ __global__ __launch_bounds__(256) void k_mmvq(MmvArgs p, ActQ a) {
             if (c < p.ncols) {
                 float v = acc[c];
                 if constexpr (GLU) v = (v / (1.0f + expf(-v))) * acc2[c];
+                if constexpr (EPI == 2) v += p.res[row + c * p.r_col];
                 out[c * p.d_col] = v;
             }
         }
     }
 }
 
-template <int QT, int NC, bool GLU>
-static void launch_mmvq_nc(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
-    const int64_t K = p.units * 32;
-    // short rows: several rows per wave so every lane has work
-    if (K <= 2048) {
-        dim3 grid((unsigned) mx_ceil_div(p.nrows, 4 * 4), (unsigned) nch);
-        k_mmvq<QT, NC, 16, GLU><<<grid, 256, 0, c.st>>>(p, a);
-    } else if (K <= 8192) {
-        dim3 grid((unsigned) mx_ceil_div(p.nrows, 4 * 2), (unsigned) nch);
-        k_mmvq<QT, NC, 32, GLU><<<grid, 256, 0, c.st>>>(p, a);
+// launch geometry: enough blocks to cover 256 CUs, every lane's units in flight at once
+template <int QT, int NC, int EPI, int LPR>
+static void launch_lpr(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
+    constexpr int RPB = 4 * (64 / LPR);
+    dim3 grid((unsigned) mx_ceil_div(p.nrows, RPB), (unsigned) nch);
+    const int64_t per_lane = mx_ceil_div(p.units, LPR);
+    if constexpr (NC == 1) {
+        if (per_lane >= 5) k_mmvq<QT, NC, LPR, 8, EPI><<<grid, 256, 0, c.st>>>(p, a);
+        else if (per_lane >= 3) k_mmvq<QT, NC, LPR, 4, EPI><<<grid, 256, 0, c.st>>>(p, a);
+        else k_mmvq<QT, NC, LPR, 2, EPI><<<grid, 256, 0, c.st>>>(p, a);
     } else {
-        dim3 grid((unsigned) mx_ceil_div(p.nrows, 4), (unsigned) nch);
-        k_mmvq<QT, NC, 64, GLU><<<grid, 256, 0, c.st>>>(p, a);
+        k_mmvq<QT, NC, LPR, 2, EPI><<<grid, 256, 0, c.st>>>(p, a);
     }
 }
 
-template <int QT, bool GLU>
+template <int QT, int NC, int EPI>
+static void launch_mmvq_nc(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
+    // GLU streams two matrices: one LPR step wider keeps its register tile (and
+    // occupancy) equal to the single-matrix kernels
+    const int64_t small_units = EPI == 1 ? 64 : 128;
+    if (p.nrows <= 2048 || p.units > 256) launch_lpr<QT, NC, EPI, 64>(c, p, a, nch);
+    else if (p.units <= small_units) launch_lpr<QT, NC, EPI, 16>(c, p, a, nch);
+    else launch_lpr<QT, NC, EPI, 32>(c, p, a, nch);
+}
+
+template <int QT, int EPI>
 static void launch_mmvq(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
     switch (p.ncols) {
-        case 1: launch_mmvq_nc<QT, 1, GLU>(c, p, a, nch); break;
-        case 2: launch_mmvq_nc<QT, 2, GLU>(c, p, a, nch); break;
-        case 3: case 4: launch_mmvq_nc<QT, 4, GLU>(c, p, a, nch); break;
-        default: launch_mmvq_nc<QT, 8, GLU>(c, p, a, nch); break;
+        case 1: launch_mmvq_nc<QT, 1, EPI>(c, p, a, nch); break;
+        case 2: launch_mmvq_nc<QT, 2, EPI>(c, p, a, nch); break;
+        case 3: case 4: launch_mmvq_nc<QT, 4, EPI>(c, p, a, nch); break;
+        default: launch_mmvq_nc<QT, 8, EPI>(c, p, a, nch); break;
     }
 }
 
@@ -181,14 +281,14 @@ static MmvArgs mmv_args(const ggml_tensor * w, const ggml_tensor * src1, ggml_te
     return p;
 }
 
-template <bool GLU>
+template <int EPI>
 static void mmvq_dispatch(OpCtx & c, int type, const MmvArgs & p, const ActQ & a, int64_t nch) {
     switch (type) {
-        case GGML_TYPE_Q4_K: launch_mmvq<GGML_TYPE_Q4_K, GLU>(c, p, a, nch); break;
-        case GGML_TYPE_Q5_K: launch_mmvq<GGML_TYPE_Q5_K, GLU>(c, p, a, nch); break;
-        case GGML_TYPE_Q6_K: launch_mmvq<GGML_TYPE_Q6_K, GLU>(c, p, a, nch); break;
-        case GGML_TYPE_Q4_0: launch_mmvq<GGML_TYPE_Q4_0, GLU>(c, p, a, nch); break;
-        case GGML_TYPE_Q8_0: launch_mmvq<GGML_TYPE_Q8_0, GLU>(c, p, a, nch); break;
+        case GGML_TYPE_Q4_K: launch_mmvq<GGML_TYPE_Q4_K, EPI>(c, p, a, nch); break;
+        case GGML_TYPE_Q5_K: launch_mmvq<GGML_TYPE_Q5_K, EPI>(c, p, a, nch); break;
+        case GGML_TYPE_Q6_K: launch_mmvq<GGML_TYPE_Q6_K, EPI>(c, p, a, nch); break;
+        case GGML_TYPE_Q4_0: launch_mmvq<GGML_TYPE_Q4_0, EPI>(c, p, a, nch); break;
+        case GGML_TYPE_Q8_0: launch_mmvq<GGML_TYPE_Q8_0, EPI>(c, p, a, nch); break;
         default: MX_ABORT("mmvq type %d", type);
     }
 }
@@ -199,22 +299,56 @@ void mmvq_run(OpCtx & c, ggml_tensor * dst) {
     const ggml_tensor * x = dst->src[1];
     ActQ a = quantize_activations(c, x);
     MmvArgs p = mmv_args(w, x, dst);
-    mmvq_dispatch<false>(c, w->type, p, a, x->ne[2] * x->ne[3]);
+    mmvq_dispatch<0>(c, w->type, p, a, x->ne[2] * x->ne[3]);
+}
+
+bool mmvq_small_batch_ok(const ggml_tensor * mm) {
+    const ggml_tensor * w = mm->src[0];
+    const ggml_tensor * x = mm->src[1];
+    return mm->op == GGML_OP_MUL_MAT && mmvq_type_ok(w->type) && x->type == GGML_TYPE_F32 && x->ne[1] <= 8 &&
+           x->nb[0] == 4 && mm->nb[0] == 4 && w->nb[0] == (size_t) mx_type(w->type).size && w->ne[0] % qk_of_type(w->type) == 0;
 }
 
 bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu) {
     const ggml_tensor * wg = gate->src[0], * wu = up->src[0];
     const ggml_tensor * x = gate->src[1];
-    if (up->src[1] != x || wg->type != wu->type || !mmvq_type_ok(wg->type)) return false;
+    if (up->src[1] != x || wg->type != wu->type || !mmvq_small_batch_ok(gate) || !mmvq_small_batch_ok(up)) return false;
     if (mx_op_param<int32_t>(glu, 0) != GGML_GLU_OP_SWIGLU) return false;
-    if (x->type != GGML_TYPE_F32 || x->ne[1] > 8 || x->ne[2] != 1 || x->ne[3] != 1) return false;
+    if (x->ne[2] != 1 || x->ne[3] != 1) return false;
     for (int i = 0; i < 4; ++i) if (wg->ne[i] != wu->ne[i] || wg->nb[i] != wu->nb[i]) return false;
-    if (wg->ne[2] != 1 || wg->ne[3] != 1 || wg->ne[0] % qk_of_type(wg->type) != 0) return false;
+    if (wg->ne[2] != 1 || wg->ne[3] != 1) return false;
     if (glu->type != GGML_TYPE_F32 || glu->nb[0] != 4 || !mx_are_same_shape(glu, gate)) return false;
+    XStage xs;
+    if (g_gemv2 && gemv2_ok(wg, x, glu) && gemv2_stage(c, x, {glu}, {}, &xs)) {
+        // the q8 form of the output feeds the down projection's prologue (act cache)
+        ActQ * q8 = (wg->ne[1] % 32 == 0 && mx_is_contiguous(glu)) ? act_cache_alloc(c.s, glu) : nullptr;
+        if (q8 && xs.q8 == q8->q) q8 = nullptr;
+        gemv2_launch(c, wg, wu, xs, (float *) glu->data, nullptr, q8);
+        return true;
+    }
     ActQ a = quantize_activations(c, x);
     MmvArgs p = mmv_args(wg, x, glu);
     p.w2 = (const char *) wu->data;
-    mmvq_dispatch<true>(c, wg->type, p, a, 1);
+    mmvq_dispatch<1>(c, wg->type, p, a, 1);
+    return true;
+}
+
+bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, ggml_tensor * add) {
+    const ggml_tensor * w = mm->src[0];
+    const ggml_tensor * x = mm->src[1];
+    if (!mmvq_small_batch_ok(mm) || x->ne[2] != 1 || x->ne[3] != 1) return false;
+    if (res->type != GGML_TYPE_F32 || add->type != GGML_TYPE_F32 || !mx_are_same_shape(res, mm) || !mx_are_same_shape(add, mm)) return false;
+    if (res->nb[0] != 4 || add->nb[0] != 4 || w->ne[2] != 1 || w->ne[3] != 1) return false;
+    XStage xs;
+    if (g_gemv2 && gemv2_ok(w, x, add) && mx_is_contiguous(res) && gemv2_stage(c, x, {add}, {res}, &xs)) {
+        gemv2_launch(c, w, nullptr, xs, (float *) add->data, (const float *) res->data);
+        return true;
+    }
+    ActQ a = quantize_activations(c, x);
+    MmvArgs p = mmv_args(w, x, add);
+    p.res = (const float *) res->data;
+    p.r_col = res->nb[1] / 4;
+    mmvq_dispatch<2>(c, w->type, p, a, 1);
     return true;
 }
 
@@ -224,31 +358,44 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up,
 // MUL_MAT(w, x) (or the fused gate/up GLU when w2 != NULL) with HIP events on the
 // backend's own stream. Returns the average µs per launch.
 // ---------------------------------------------------------------------------
-double time_mmvq(Stream * s, const ggml_tensor * w, const ggml_tensor * w2, const ggml_tensor * x, ggml_tensor * dst, int iters) {
+double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * const * w2, int nw,
+                 const ggml_tensor * x, ggml_tensor * dst, int iters) {
     OpCtx c{s, s->stream, &s->scratch};
-    const size_t need = quantize_scratch(x);
-    if (need > s->scratch.cap) {
-        HIP_CHECK(hipStreamSynchronize(s->stream));
-        if (s->scratch.base) HIP_CHECK(hipFree(s->scratch.base));
-        HIP_CHECK(hipMalloc((void **) &s->scratch.base, need));
-        s->scratch.cap = need;
-        s->gcache.key.clear();
-    }
-    s->scratch.reset();
-    ActQ a = quantize_activations(c, x);
-    MmvArgs p = mmv_args(w, x, dst);
-    if (w2) p.w2 = (const char *) w2->data;
+    MX_ASSERT(nw >= 1);
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
-    for (int i = 0; i < 3; ++i) {
-        if (w2) mmvq_dispatch<true>(c, w->type, p, a, 1); else mmvq_dispatch<false>(c, w->type, p, a, 1);
+    if (g_gemv2 && gemv2_ok(w[0], x, dst)) {
+        // exactly the launch the executor makes; cycling over nw weight sets (e.g. all
+        // layers of a model) so the stream comes from HBM, not the 256 MiB MALL
+        const XStage xs{(const float *) x->data, nullptr, 0.0f, 0};
+        auto launch = [&](int i) { gemv2_launch(c, w[i % nw], w2 ? w2[i % nw] : nullptr, xs, (float *) dst->data, nullptr); };
+        for (int i = 0; i < 3; ++i) launch(i);
+        HIP_CHECK(hipEventRecord(e0, s->stream));
+        for (int i = 0; i < iters; ++i) launch(i);
+        HIP_CHECK(hipEventRecord(e1, s->stream));
+    } else {
+        const size_t need = quantize_scratch(x);
+        if (need > s->scratch.cap) {
+            HIP_CHECK(hipStreamSynchronize(s->stream));
+            if (s->scratch.base) HIP_CHECK(hipFree(s->scratch.base));
+            HIP_CHECK(hipMalloc((void **) &s->scratch.base, need));
+            s->scratch.cap = need;
+            s->gcache.key.clear();
+        }
+        s->scratch.reset();
+        ActQ a = carve((char *) s->scratch.take(act_slot_bytes(x)), x);
+        a = quantize_into(c, x, (int8_t *) a.q, (float *) a.d, (float *) a.s);
+        auto launch = [&](int i) {
+            MmvArgs p = mmv_args(w[i % nw], x, dst);
+            if (w2) { p.w2 = (const char *) w2[i % nw]->data; mmvq_dispatch<1>(c, w[0]->type, p, a, 1); }
+            else mmvq_dispatch<0>(c, w[0]->type, p, a, 1);
+        };
+        for (int i = 0; i < 3; ++i) launch(i);
+        HIP_CHECK(hipEventRecord(e0, s->stream));
+        for (int i = 0; i < iters; ++i) launch(i);
+        HIP_CHECK(hipEventRecord(e1, s->stream));
     }
-    HIP_CHECK(hipEventRecord(e0, s->stream));
-    for (int i = 0; i < iters; ++i) {
-        if (w2) mmvq_dispatch<true>(c, w->type, p, a, 1); else mmvq_dispatch<false>(c, w->type, p, a, 1);
-    }
-    HIP_CHECK(hipEventRecord(e1, s->stream));
     HIP_CHECK(hipEventSynchronize(e1));
     float ms = 0.f;
     HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));

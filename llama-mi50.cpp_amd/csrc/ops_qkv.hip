@@ -1,0 +1,197 @@
+// ops_qkv.hip — fused decode attention-input block: the Q, K and V projections of
+// one token in ONE launch, with RoPE (NORMAL mode) on Q and K in the epilogue and
+// the K/V rows written straight into the f16 KV cache.
+//
+// Replaces, for n_tokens == 1, the node chain libllama emits per layer
+// (src/models/llama.cpp:44-79 + build_attn src/llama-graph.cpp:1918-1945 +
+// llama_kv_cache::cpy_k/cpy_v src/llama-kv-cache.cpp:1072-1161):
+//   MUL_MAT(wq,x) MUL_MAT(wk,x) MUL_MAT(wv,x) ROPE(q) ROPE(k) SET_ROWS(k) SET_ROWS(v)
+// = 7 launches → 1. The reference CUDA backend fuses ROPE→SET_ROWS only
+// (ggml-cuda.cu:3088-3122). Semantics per node are unchanged: GEMV as mmvq,
+// RoPE as ops.cpp:5523-5800 (theta by repeated multiplication), f32→f16 RNE stores.
+#include "backend.h"
+#include "gemv.cuh"
+
+namespace mx {
+
+struct QkvArgs {
+    const char * w[3];
+    size_t w_row[3];
+    int rows[3];
+    int nblk_q, nblk_k;            // block ranges: [0,nq) q, [nq,nq+nk) k, rest v
+    int units_a, units_v, K;
+    XStage xs;
+    float * q_out;                 // roped q, f32 [n_embd]
+    char * kc; size_t kc_nb1; const char * kidx; int kidx64;
+    char * vc; size_t vc_nb1; const char * vidx; int vidx64; int v_trans;
+    const int32_t * pos; const float * ff;
+    int n_dims;
+    float theta_scale, freq_scale, ext_factor, attn_factor, corr0, corr1;
+};
+
+__device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i) {
+    return is64 ? ((const int64_t *) p)[i] : (int64_t) ((const int32_t *) p)[i];
+}
+
+// LPR = 16: the RoPE pair (rows 2i, 2i+1) sits 16 lanes apart in one wave
+template <int QTA, int QTV>
+__global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
+    extern __shared__ __align__(16) char smem[];
+    constexpr int LPR = 16, UPL = 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane & 15;
+    const int b = blockIdx.x;
+    const int m = b < p.nblk_q ? 0 : (b < p.nblk_q + p.nblk_k ? 1 : 2);
+    const int bl = m == 0 ? b : (m == 1 ? b - p.nblk_q : b - p.nblk_q - p.nblk_k);
+    const int row = bl * 16 + wave * 4 + (lane >> 4);
+    const bool valid = row < p.rows[m];
+    const char * rows[1] = {p.w[m] + (int64_t) (valid ? row : p.rows[m] - 1) * p.w_row[m]};
+    const LdsAct a = lds_act(smem, p.K);
+    float * red = (float *) (smem + gemv_lds_bytes(p.K) - 64);
+    float acc[1];
+    auto stage = [&] { stage_x<256>(p.xs, p.K, a, red); };
+    if (m == 2) gemv_rows<QTV, LPR, UPL, 1>(rows, p.units_v, sub, a, stage, acc);   // block-uniform branch
+    else gemv_rows<QTA, LPR, UPL, 1>(rows, p.units_a, sub, a, stage, acc);
+    const float v = acc[0];
+    const float pv = __shfl_xor(v, 16, 64);
+    if (sub != 0 || !valid) return;
+    if (m == 2) {
+        const uint16_t h = f2h(v);
+        if (p.v_trans) *(uint16_t *) (p.vc + read_idx(p.vidx, p.vidx64, row) * p.vc_nb1) = h;
+        else *(uint16_t *) (p.vc + read_idx(p.vidx, p.vidx64, 0) * p.vc_nb1 + row * 2) = h;
+        return;
+    }
+    const int d = row % p.n_dims;
+    const bool odd = d & 1;
+    const int i0 = d & ~1;
+    float theta = (float) p.pos[0];
+    for (int k = 0; k < i0 / 2; ++k) theta *= p.theta_scale;
+    if (p.ff) theta /= p.ff[i0 / 2];
+    // rope_yarn (ops.cpp:5529-5546)
+    const float ti = p.freq_scale * theta;
+    float th = ti, ms = p.attn_factor;
+    if (p.ext_factor != 0.0f) {
+        const float y = (i0 / 2 - p.corr0) / fmaxf(0.001f, p.corr1 - p.corr0);
+        const float mix = (1.0f - fminf(1.0f, fmaxf(0.0f, y))) * p.ext_factor;
+        th = ti * (1 - mix) + theta * mix;
+        ms *= 1.0f + 0.1f * logf(1.0f / p.freq_scale);
+    }
+    const float cs = cosf(th) * ms, sn = sinf(th) * ms;
+    const float x0 = odd ? pv : v, x1 = odd ? v : pv;
+    const float r = odd ? x0 * sn + x1 * cs : x0 * cs - x1 * sn;
+    if (m == 0) p.q_out[row] = r;
+    else *(uint16_t *) (p.kc + read_idx(p.kidx, p.kidx64, 0) * p.kc_nb1 + row * 2) = f2h(r);
+}
+
+static const ggml_tensor * base_of(const ggml_tensor * t) {
+    while (t && (t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW)) t = t->src[0];
+    return t;
+}
+
+static float yarn_corr(int n_dims, int n_ctx_orig, float n_rot, float base) {
+    return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float) M_PI)) / (2 * logf(base));
+}
+
+// Returns the number of graph nodes consumed starting at i (0 = not fused).
+int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map) {
+    auto uses = [&](const ggml_tensor * t) { auto it = use_map.find(t); return it == use_map.end() ? 0 : it->second; };
+    // Collect the 7 member nodes from i on, skipping views. Any other node in the
+    // window aborts the match, so running the fused kernel at position i cannot
+    // reorder anything but the members. Order-independent: matches both this
+    // runner's order and libllama's (q, v, k expansion, build_attn).
+    ggml_tensor * mm[3] = {}, * rope[2] = {}, * sr[2] = {};
+    int n_mm = 0, n_rope = 0, n_sr = 0, last = -1;
+    const ggml_tensor * x = g->nodes[i]->src[1];
+    if (g->nodes[i]->op != GGML_OP_MUL_MAT || !x) return 0;
+    auto is_mm = [&](const ggml_tensor * t) { for (int k = 0; k < n_mm; ++k) if (mm[k] == t) return true; return false; };
+    auto is_rope = [&](const ggml_tensor * t) { for (int k = 0; k < n_rope; ++k) if (rope[k] == t) return true; return false; };
+    for (int j = i; j < g->n_nodes && j < i + 32; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (n->op == GGML_OP_RESHAPE || n->op == GGML_OP_VIEW) continue;
+        if (n->op == GGML_OP_MUL_MAT && n->src[1] == x && n_mm < 3) mm[n_mm++] = n;
+        else if (n->op == GGML_OP_ROPE && n_rope < 2 && is_mm(base_of(n->src[0]))) rope[n_rope++] = n;
+        else if (n->op == GGML_OP_SET_ROWS && n_sr < 2 && (is_rope(base_of(n->src[0])) || is_mm(base_of(n->src[0])))) sr[n_sr++] = n;
+        else return 0;
+        last = j;
+        if (n_mm == 3 && n_rope == 2 && n_sr == 2) break;
+    }
+    if (n_mm != 3 || n_rope != 2 || n_sr != 2) return 0;
+    // classify: K is the roped projection that is stored, Q the roped one that is not,
+    // V the projection stored without rope
+    ggml_tensor * rq = nullptr, * rk = nullptr, * sk = nullptr, * sv = nullptr;
+    for (ggml_tensor * r : sr) {
+        const ggml_tensor * src = base_of(r->src[0]);
+        if (src == rope[0] || src == rope[1]) { if (sk) return 0; sk = r; rk = (ggml_tensor *) src; }
+        else { if (sv) return 0; sv = r; }
+    }
+    if (!sk || !sv) return 0;
+    rq = rope[0] == rk ? rope[1] : rope[0];
+    ggml_tensor * mq = (ggml_tensor *) base_of(rq->src[0]), * mk = (ggml_tensor *) base_of(rk->src[0]);
+    ggml_tensor * mv = (ggml_tensor *) base_of(sv->src[0]);
+    if (mq == mk || mq == mv || mk == mv) return 0;
+    if (x->ne[1] != 1 || x->ne[2] != 1 || x->ne[3] != 1) return 0;
+    if (!g_gemv2 || !gemv2_ok(mq->src[0], x, mq) || !gemv2_ok(mk->src[0], x, mk) || !gemv2_ok(mv->src[0], x, mv)) return 0;
+    const ggml_tensor * wq = mq->src[0], * wk = mk->src[0], * wv = mv->src[0];
+    if (wq->type != wk->type || wq->ne[0] != wk->ne[0] || wq->ne[0] != wv->ne[0]) return 0;
+    for (const ggml_tensor * r : {rq, rk}) {
+        if (mx_op_param<int32_t>(r, 2) != GGML_ROPE_TYPE_NORMAL || r->type != GGML_TYPE_F32 || !mx_is_contiguous(r)) return 0;
+        if (r->src[1]->type != GGML_TYPE_I32 || r->src[1]->ne[0] != 1) return 0;
+    }
+    if (memcmp(rq->op_params, rk->op_params, 11 * sizeof(int32_t)) != 0 || rq->src[1] != rk->src[1] || rq->src[2] != rk->src[2]) return 0;
+    const int n_dims = mx_op_param<int32_t>(rq, 1);
+    if (n_dims != rq->ne[0] || n_dims % 2 || (rq->src[2] && rq->src[2]->type != GGML_TYPE_F32)) return 0;
+    // only the fused consumers may read the intermediate results
+    if ((mq->flags | mk->flags | mv->flags | rk->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
+    if (uses(mq) != 1 || uses(mk) != 1 || uses(mv) != 1 || uses(rk) != 1) return 0;
+    // KV stores: f16 caches, one token
+    const ggml_tensor * kcache = sk, * vcache = sv;
+    if (kcache->type != GGML_TYPE_F16 || vcache->type != GGML_TYPE_F16) return 0;
+    const ggml_tensor * kix = sk->src[1], * vix = sv->src[1];
+    if (sk->src[0]->ne[0] != wk->ne[1] || sk->src[0]->ne[1] != 1 || kix->ne[0] != 1 || sk->nb[0] != 2) return 0;
+    int v_trans;
+    if (sv->src[0]->ne[0] == wv->ne[1] && sv->src[0]->ne[1] == 1 && vix->ne[0] == 1 && sv->nb[0] == 2) v_trans = 0;
+    else if (sv->src[0]->ne[0] == 1 && sv->src[0]->ne[1] == wv->ne[1] && vix->ne[0] == wv->ne[1] && sv->ne[0] == 1) v_trans = 1;
+    else return 0;
+    for (const ggml_tensor * ix : {kix, vix}) if (ix->type != GGML_TYPE_I64 && ix->type != GGML_TYPE_I32) return 0;
+
+    QkvArgs p{};
+    const ggml_tensor * ws[3] = {wq, wk, wv};
+    for (int t = 0; t < 3; ++t) { p.w[t] = (const char *) ws[t]->data; p.w_row[t] = ws[t]->nb[1]; p.rows[t] = ws[t]->ne[1]; }
+    p.nblk_q = (int) mx_ceil_div(wq->ne[1], 16);
+    p.K = (int) wq->ne[0];
+    p.units_a = (int) (wq->ne[0] / ((wq->type == GGML_TYPE_Q4_0 || wq->type == GGML_TYPE_Q8_0) ? 32 : 64));
+    p.units_v = (int) (wv->ne[0] / ((wv->type == GGML_TYPE_Q4_0 || wv->type == GGML_TYPE_Q8_0) ? 32 : 64));
+    p.nblk_k = (int) mx_ceil_div(wk->ne[1], 16);
+    const int nblk_v = (int) mx_ceil_div(wv->ne[1], 16);
+    p.q_out = (float *) rq->data;
+    p.kc = (char *) sk->data; p.kc_nb1 = sk->nb[1]; p.kidx = (const char *) kix->data; p.kidx64 = kix->type == GGML_TYPE_I64;
+    p.vc = (char *) sv->data; p.vc_nb1 = sv->nb[1]; p.vidx = (const char *) vix->data; p.vidx64 = vix->type == GGML_TYPE_I64;
+    p.v_trans = v_trans;
+    p.pos = (const int32_t *) rq->src[1]->data;
+    p.ff = rq->src[2] ? (const float *) rq->src[2]->data : nullptr;
+    p.n_dims = n_dims;
+    const int n_ctx_orig = mx_op_param<int32_t>(rq, 4);
+    const float base = mx_op_param<float>(rq, 5);
+    p.freq_scale = mx_op_param<float>(rq, 6);
+    p.ext_factor = mx_op_param<float>(rq, 7);
+    p.attn_factor = mx_op_param<float>(rq, 8);
+    p.theta_scale = powf(base, -2.0f / n_dims);
+    p.corr0 = std::max(0.0f, floorf(yarn_corr(n_dims, n_ctx_orig, mx_op_param<float>(rq, 9), base)));
+    p.corr1 = std::min((float) (n_dims - 1), ceilf(yarn_corr(n_dims, n_ctx_orig, mx_op_param<float>(rq, 10), base)));
+
+    const int ta = wq->type, tv = wv->type;
+    void (*kern)(QkvArgs) = nullptr;
+#define QKV(TA, TV) if (ta == TA && tv == TV) kern = k_qkv_rope_store<TA, TV>;
+    QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
+    QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
+    QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
+#undef QKV
+    if (!kern) return 0;
+    if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs)) return 0;
+    for (int j = i; j <= last; ++j) act_cache_invalidate(c.s, g->nodes[j]);
+    const dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
+    hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K), c.st, p);
+    return last - i + 1;
+}
+
+}  // namespace mx

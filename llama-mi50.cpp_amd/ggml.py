@@ -72,7 +72,7 @@ class Tensor:
         return list(self.raw.op_params)[:n]
 
     def nbytes(self):
-        return self.ctx.lib.mxg_nbytes(self.ptr)
+        return _lib.load().mxg_nbytes(self.ptr)
 
     def set(self, arr):
         a = np.ascontiguousarray(arr)

@@ -50,6 +50,10 @@ class Model:
         lib = _lib.load()
         return cls(backend, lib.mxr_model_load_gguf(backend.ptr, str(path).encode()))
 
+    def layer_tensor(self, il, which):
+        """Raw ggml_tensor* of layer il's weight by GGUF role (e.g. "ffn_gate")."""
+        return self.lib.mxr_model_layer_tensor(self.ptr, il, which.encode())
+
     def decode_bytes(self):
         """Algorithmic weight bytes read per decoded token (all weights but token_embd)."""
         return int(self.lib.mxr_model_decode_bytes(self.ptr))

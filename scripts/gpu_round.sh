@@ -19,6 +19,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} ;;
     refops) OUT=$OUT/refops step refops 1200 bash scripts/gpu_ref_ops.sh ;;
+    opbench) step opbench 900 bash scripts/opbench.sh ${OPBENCH_ARGS:-} ;;
     bench) step bench 900 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
           step prof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;

@@ -100,3 +100,15 @@ def test_moe_decode_matches_prefill(pkg, backend):
     assert np.all(np.isfinite(full))
     assert nmse(inc, full) < 5e-4
     a.free(); b.free(); m.free()
+
+
+@pytest.mark.parametrize("fa", [True, False])
+def test_decode_fusions_fire(pkg, backend, tiny, fa):
+    """Every decode layer runs the fused chains: rms_norm·w (1), Q/K/V+RoPE+KV-store (6),
+    wo+residual (1), rms_norm·w (1), gate/up/GLU (2), down+residual (1)."""
+    s = pkg.Session(tiny, n_ctx=256, flash_attn=fa)
+    before = backend.stats()["nodes_fused"]
+    s.decode(np.array([5], dtype=np.int32))
+    fused = backend.stats()["nodes_fused"] - before
+    s.free()
+    assert fused >= 12 * TINY["n_layer"], f"only {fused} nodes fused"

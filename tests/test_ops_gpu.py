@@ -217,3 +217,38 @@ def test_mul_mat_id(pkg, backend, orc):
             ex = ids[t, e]
             ref = orc.mul_mat(tid, w[ex * M * rb:(ex + 1) * M * rb], rb, x[t])[0]
             assert nmse(y[t, e], ref) < 5e-4
+
+
+@pytest.mark.parametrize("extra_use", [False, True])
+def test_norm_absorbed_by_gemv(pkg, backend, orc, extra_use):
+    """RMS_NORM -> MUL(w) consumed only by single-token GEMVs is folded into the GEMV
+    prologues (deferred norm); with an extra non-GEMV consumer it is materialised."""
+    tid = NAMES["q4_K"]
+    rng = np.random.default_rng(31)
+    K, M1, M2 = 2048, 384, 128
+    w1, rb = rand_quant(tid, M1, K, rng)
+    w2, _ = rand_quant(tid, M2, K, rng)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    nw = rng.uniform(0.5, 1.5, K).astype(np.float32)
+    before = backend.stats()["nodes_fused"]
+
+    def build(ctx):
+        tx = ctx.new_tensor("f32", K, 1)
+        tn = ctx.new_tensor("f32", K)
+        t1 = ctx.new_tensor(tid, K, M1)
+        t2 = ctx.new_tensor(tid, K, M2)
+        cur = ctx.mul(ctx.rms_norm(tx, 1e-5), tn)
+        outs = [ctx.mul_mat(t1, cur), ctx.mul_mat(t2, cur)]
+        if extra_use:
+            outs.append(ctx.scale(cur, 2.0))
+        return outs, [(tx, x), (tn, nw), (t1, w1), (t2, w2)]
+
+    res = run(pkg, backend, build)
+    xn = orc.rms_norm(x, 1e-5) * nw
+    for y, w, M in ((res[0], w1, M1), (res[1], w2, M2)):
+        ref = orc.mul_mat(tid, w, rb, xn, exact=True)
+        assert nmse(y.reshape(1, M), ref) < 5e-4
+    if extra_use:
+        assert nmse(res[2].reshape(1, K), 2.0 * xn) < 1e-10
+    else:
+        assert backend.stats()["nodes_fused"] >= before + 2, "norm was not deferred"
