@@ -57,6 +57,13 @@ double ggml_backend_mi355x_time_mmvq(ggml_backend_t backend, const struct ggml_t
 /* Launch-geometry overrides for tuning sweeps (0 = built-in choice):
  * idx 0/1 = GEMV lanes-per-row / units-per-lane, 2/3 = the same for the fused SwiGLU GEMV. */
 void ggml_backend_mi355x_set_tune(int idx, int value);
+/* Debug: phase timestamps (s_memtime) of the first workgroup of the instrumented kernels,
+ * recorded while tune index 6 is set: slot s (0 decode flash-attn, 1 GEMV, 2 QKV) at
+ * out[s*128 + wave*8 + phase]. Read-and-clear; returns n or -1. */
+int ggml_backend_mi355x_trace_read(unsigned long long * out, int n);
+/* Debug: {start, end} s_memrealtime (100 MHz) of every workgroup of the last GEMV launch
+ * recorded while tune index 6 == 2, at out[2*block]. Read-and-clear; returns n or -1. */
+int ggml_backend_mi355x_trace_blocks_read(unsigned long long * out, int n);
 #ifdef __cplusplus
 }
 #endif

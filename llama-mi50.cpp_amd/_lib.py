@@ -72,6 +72,8 @@ def load():
     _sig(lib, "ggml_backend_mi355x_stats", None, P, ctypes.POINTER(ctypes.c_uint64))
     _sig(lib, "ggml_backend_mi355x_time_mmvq", ctypes.c_double, P, P, P, I, P, P, I)
     _sig(lib, "ggml_backend_mi355x_set_tune", None, I, I)
+    _sig(lib, "ggml_backend_mi355x_trace_read", I, P, I)
+    _sig(lib, "ggml_backend_mi355x_trace_blocks_read", I, P, I)
     # graph builder
     _sig(lib, "mxg_init", P)
     _sig(lib, "mxg_free", None, P)

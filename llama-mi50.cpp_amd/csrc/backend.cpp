@@ -421,6 +421,45 @@ extern "C" double ggml_backend_mi355x_time_mmvq(ggml_backend_t b, const ggml_ten
     return mx::time_mmvq(s, w, w2, n_w, x, dst, iters);
 }
 
+namespace mx {
+static unsigned long long * g_trace_dev = nullptr;
+unsigned long long * mx_trace_slot(int slot) {
+    if (!g_tune[6]) return nullptr;
+    if (!g_trace_dev) {
+        HIP_CHECK(hipMalloc((void **) &g_trace_dev, 16 * 128 * sizeof(unsigned long long)));
+        HIP_CHECK(hipMemset(g_trace_dev, 0, 16 * 128 * sizeof(unsigned long long)));
+    }
+    return g_trace_dev + slot * 128;
+}
+}
+
+namespace mx {
+static unsigned long long * g_trace_blk = nullptr;
+unsigned long long * mx_trace_blocks() {
+    if (g_tune[6] != 2) return nullptr;
+    if (!g_trace_blk) HIP_CHECK(hipMalloc((void **) &g_trace_blk, 2 * 65536 * sizeof(unsigned long long)));
+    return g_trace_blk;
+}
+}
+
+extern "C" int ggml_backend_mi355x_trace_blocks_read(unsigned long long * out, int n) {
+    if (!mx::g_trace_blk) return -1;
+    if (n > 2 * 65536) n = 2 * 65536;
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(out, mx::g_trace_blk, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemset(mx::g_trace_blk, 0, 2 * 65536 * sizeof(unsigned long long)));
+    return n;
+}
+
+extern "C" int ggml_backend_mi355x_trace_read(unsigned long long * out, int n) {
+    if (!mx::g_trace_dev) return -1;
+    if (n > 16 * 128) n = 16 * 128;
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(out, mx::g_trace_dev, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemset(mx::g_trace_dev, 0, 16 * 128 * sizeof(unsigned long long)));   // read-and-clear
+    return n;
+}
+
 extern "C" void ggml_backend_mi355x_set_tune(int idx, int value) {
     if (idx >= 0 && idx < 16) mx::g_tune[idx] = value;
 }

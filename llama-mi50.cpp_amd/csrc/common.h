@@ -117,25 +117,101 @@ static inline int64_t mx_ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b
 // ---------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------
+namespace mx {
+// host: trace buffer of kernel slot (0 flash-attn decode, 1 GEMV, 2 QKV), null unless
+// tracing is on (tune index 6)
+unsigned long long * mx_trace_slot(int slot);
+// host: per-workgroup {start, end} s_memrealtime pairs of the last traced launch (tune 6 == 2)
+unsigned long long * mx_trace_blocks();
+}
 #if defined(__HIPCC__)
 
+// Cross-lane reductions on DPP (gfx9 data-parallel primitives: quad_perm, half/row
+// mirror, row_bcast15/31) instead of ds_bpermute: no LDS round trip per step.
+// dpp_*_group<N>: reduction over aligned groups of N lanes; the result is in every
+// lane for N <= 16 and in the LAST lane of each group for N = 32, 64.
+template <int CTRL, int ROWM = 0xF>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROWM, 0xF, false));
+}
+template <int CTRL, int ROWM = 0xF>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWM, 0xF, false);
+}
+template <int N>
+__device__ __forceinline__ float dpp_sum_group(float v) {
+    if constexpr (N >= 2) v += dpp_f<0xB1>(0.f, v);          // quad_perm [1,0,3,2]
+    if constexpr (N >= 4) v += dpp_f<0x4E>(0.f, v);          // quad_perm [2,3,0,1]
+    if constexpr (N >= 8) v += dpp_f<0x141>(0.f, v);         // row_half_mirror
+    if constexpr (N >= 16) v += dpp_f<0x140>(0.f, v);        // row_mirror
+    if constexpr (N >= 32) v += dpp_f<0x142, 0xA>(0.f, v);   // row_bcast15 -> rows 1, 3
+    if constexpr (N >= 64) v += dpp_f<0x143, 0xC>(0.f, v);   // row_bcast31 -> rows 2, 3
+    return v;
+}
+template <int N>
+__device__ __forceinline__ float dpp_max_group(float v) {
+    if constexpr (N >= 2) v = fmaxf(v, dpp_f<0xB1>(-INFINITY, v));
+    if constexpr (N >= 4) v = fmaxf(v, dpp_f<0x4E>(-INFINITY, v));
+    if constexpr (N >= 8) v = fmaxf(v, dpp_f<0x141>(-INFINITY, v));
+    if constexpr (N >= 16) v = fmaxf(v, dpp_f<0x140>(-INFINITY, v));
+    if constexpr (N >= 32) v = fmaxf(v, dpp_f<0x142, 0xA>(-INFINITY, v));
+    if constexpr (N >= 64) v = fmaxf(v, dpp_f<0x143, 0xC>(-INFINITY, v));
+    return v;
+}
+template <int N>
+__device__ __forceinline__ int dpp_sum_group_i(int v) {
+    if constexpr (N >= 2) v += dpp_i<0xB1>(0, v);
+    if constexpr (N >= 4) v += dpp_i<0x4E>(0, v);
+    if constexpr (N >= 8) v += dpp_i<0x141>(0, v);
+    if constexpr (N >= 16) v += dpp_i<0x140>(0, v);
+    if constexpr (N >= 32) v += dpp_i<0x142, 0xA>(0, v);
+    if constexpr (N >= 64) v += dpp_i<0x143, 0xC>(0, v);
+    return v;
+}
+__device__ __forceinline__ float lane_bcast(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Debug phase tracing (tools/opbench.py --trace): an instrumented kernel gets a device
+// pointer (null unless tracing) for its first workgroup and records s_memtime per wave at
+// phase boundaries: ptr[wave * 8 + phase].
+#define MX_TRACE(ptr, ph) do { if ((ptr) && (threadIdx.x & 63) == 0) \
+    (ptr)[(threadIdx.x >> 6) * 8 + (ph)] = __builtin_amdgcn_s_memtime(); } while (0)
+
+// per-workgroup start/end (100 MHz s_memrealtime, comparable across XCDs)
+#define MX_TRACE_BLK(ptr, which) do { if ((ptr) && threadIdx.x == 0) \
+    (ptr)[2 * (blockIdx.x + blockIdx.y * gridDim.x) + (which)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+
+// reductions over W lanes with the result in every lane
 template <int W = MX_WAVE>
 __device__ __forceinline__ float wave_sum(float v) {
+    if constexpr (W == 64) return lane_bcast(dpp_sum_group<64>(v), 63);
+    else if constexpr (W <= 16) return dpp_sum_group<W>(v);
+    else {
 #pragma unroll
-    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
-    return v;
+        for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+        return v;
+    }
 }
 template <int W = MX_WAVE>
 __device__ __forceinline__ float wave_max(float v) {
+    if constexpr (W == 64) return lane_bcast(dpp_max_group<64>(v), 63);
+    else if constexpr (W <= 16) return dpp_max_group<W>(v);
+    else {
 #pragma unroll
-    for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, W));
-    return v;
+        for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, W));
+        return v;
+    }
 }
 template <int W = MX_WAVE>
 __device__ __forceinline__ int wave_sum_i(int v) {
+    if constexpr (W == 64) return __builtin_amdgcn_readlane(dpp_sum_group_i<64>(v), 63);
+    else if constexpr (W <= 16) return dpp_sum_group_i<W>(v);
+    else {
 #pragma unroll
-    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
-    return v;
+        for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+        return v;
+    }
 }
 
 // block-wide sum for blockDim.x multiple of 64, <= 1024; lds >= 16 floats

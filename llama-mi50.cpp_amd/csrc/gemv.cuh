@@ -33,7 +33,26 @@ struct LdsAct {
     float * s;
 };
 
-__host__ __device__ inline size_t gemv_lds_bytes(int64_t K) { return (size_t) K + (size_t) (K / 32) * 8 + 64; }
+// activation source of a GEMV, compile-time (each mode keeps only its own registers).
+// *_LDS modes stage the f32 x (and norm weight) into LDS by LDS-DMA before the weight
+// loads are issued and quantise from LDS afterwards: no registers, no wait on x.
+enum { XS_F32 = 0, XS_NORM = 1, XS_Q8 = 2, XS_F32_LDS = 3, XS_NORM_LDS = 4 };
+
+__host__ __device__ inline size_t gemv_lds_base(int64_t K) { return ((size_t) K + (size_t) (K / 32) * 8 + 64 + 15) & ~(size_t) 15; }
+__host__ __device__ inline size_t gemv_lds_bytes(int64_t K, int mode = XS_Q8) {
+    return gemv_lds_base(K) + (mode == XS_F32_LDS || mode == XS_NORM_LDS ? 4 * (size_t) K : 0) + (mode == XS_NORM_LDS ? 4 * (size_t) K : 0);
+}
+__host__ __device__ inline float * gemv_lds_red(char * smem, int64_t K) { return (float *) (smem + K + (K / 32) * 8); }
+// Staging mode for a source. LDS-DMA moves only ~25 GB/s per CU, so it loses on the
+// one-block-per-CU grids of the layer GEMVs (the register path's x loads ride along
+// with the weights) and wins on the huge lm_head grid, where the register path's VGPRs
+// cost occupancy (tools/opbench.py --trace, profiles/r01).
+inline int gemv_mode(const XStage & xs, int64_t K, int64_t nrows = 0) {
+    if (xs.q8) return XS_Q8;
+    const bool big = nrows >= 32768;
+    if (xs.norm) return big && gemv_lds_bytes(K, XS_NORM_LDS) <= 65536 ? XS_NORM_LDS : XS_NORM;
+    return big && gemv_lds_bytes(K, XS_F32_LDS) <= 65536 ? XS_F32_LDS : XS_F32;
+}
 
 __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
     LdsAct a;
@@ -49,7 +68,7 @@ __device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) 
     float amax = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
-    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, dpp_f<0xB1>(-INFINITY, amax));   // partner lane tid ^ 1
     const float dd = amax / 127.0f;
     const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
     int sum = 0, pk[4];
@@ -64,7 +83,7 @@ __device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) 
         }
         pk[j] = w;
     }
-    sum += __shfl_xor(sum, 1, 64);
+    sum += dpp_i<0xB1>(0, sum);
     *(int4 *) (a.q + 16 * hg) = make_int4(pk[0], pk[1], pk[2], pk[3]);
     if ((hg & 1) == 0) {
         a.d[hg >> 1] = dd;
@@ -76,72 +95,135 @@ __device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) 
 // Three sources: a q8 activation already in memory (copied), f32 x (quantised), or
 // f32 x through RMS norm · nw (K <= 2*16*NT: two 16-value halves per thread held
 // across the block reduction).
-template <int NT>
-__device__ __forceinline__ void stage_x(const XStage & xs, int64_t K, LdsAct a, float * red) {
-    const int t = threadIdx.x;
-    const int nhg = (int) (K / 16);
-    if (xs.q8) {
-        const int nq = (int) (K / 16), nb = (int) (K / 32);
-        for (int i = t; i < nq; i += NT) ((int4 *) a.q)[i] = ((const int4 *) xs.q8)[i];
-        for (int i = t; i < nb; i += NT) { a.d[i] = xs.q8d[i]; a.s[i] = xs.q8s[i]; }
-    } else if (xs.norm) {
-        float v[2][16];
+// Split in two because vector-memory loads retire in issue order: issue() starts the
+// activation loads BEFORE the weight stream is issued, finish() (after the weight loads
+// are in flight) waits only for them, quantises into LDS and ends with a barrier.
+__host__ __device__ constexpr int stage_hpt(int NT) { return NT >= 512 ? 1 : 2; }   // f32 half-groups held per thread
+
+template <int NT, int MODE>
+struct StageRegs {
+    static constexpr int HPT = stage_hpt(NT);
+    float v[MODE == XS_F32 || MODE == XS_NORM ? HPT : 1][16];
+    float w[MODE == XS_NORM ? HPT : 1][16];
+};
+
+typedef __attribute__((address_space(3))) void * lds_ptr_t;
+
+// q8 source: global -> LDS by LDS-DMA (global_load_lds), no registers held; each wave
+// moves 64 lanes x `B` bytes per instruction to a wave-uniform LDS address
+template <int NT, int B>
+__device__ __forceinline__ void dma_to_lds(const void * src, void * dst, int nbytes) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n = nbytes / B;
+    for (int c = wave * 64; c < n; c += NT) {
+        if (c + lane < n) {
+            const void * g = (const char *) src + (size_t) (c + lane) * B;
+            const lds_ptr_t l = (lds_ptr_t) ((char *) dst + c * B);
+            if constexpr (B == 16) __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+            else __builtin_amdgcn_global_load_lds(g, l, 4, 0, 0);
+        }
+    }
+}
+
+__device__ __forceinline__ void load_half(int hg, float (&dst)[16], const float * src) {
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+        const float4 f = *(const float4 *) (src + 16 * hg + j);
+        dst[j] = f.x; dst[j + 1] = f.y; dst[j + 2] = f.z; dst[j + 3] = f.w;
+    }
+}
+
+// unconditional loads at clamped indices (no partially initialised arrays: the registers
+// must stay registers); out-of-range entries are ignored by stage_finish
+template <int NT, int MODE>
+__device__ __forceinline__ void stage_issue(const XStage & xs, int K, const LdsAct & a, StageRegs<NT, MODE> & r) {
+    if constexpr (MODE == XS_Q8) {
+        dma_to_lds<NT, 16>(xs.q8, a.q, K);
+        dma_to_lds<NT, 4>(xs.q8d, a.d, K / 32 * 4);
+        dma_to_lds<NT, 4>(xs.q8s, a.s, K / 32 * 4);
+    } else if constexpr (MODE == XS_F32_LDS || MODE == XS_NORM_LDS) {
+        char * stg = (char *) a.q + gemv_lds_base(K);
+        dma_to_lds<NT, 16>(xs.x, stg, 4 * K);
+        if constexpr (MODE == XS_NORM_LDS) dma_to_lds<NT, 16>(xs.nw, stg + 4 * K, 4 * K);
+    } else {
+        const int t = threadIdx.x, nhg = K / 16;
+#pragma unroll
+        for (int h = 0; h < StageRegs<NT, MODE>::HPT; ++h) {
+            const int hg = min(t + NT * h, nhg - 1);
+            load_half(hg, r.v[h], xs.x);
+            if constexpr (MODE == XS_NORM) load_half(hg, r.w[h], xs.nw);
+        }
+    }
+}
+
+template <int NT, int MODE>
+__device__ __forceinline__ void stage_finish(const XStage & xs, int K, const LdsAct & a, float * red, StageRegs<NT, MODE> & r) {
+    constexpr int HPT = StageRegs<NT, MODE>::HPT;
+    const int t = threadIdx.x, nhg = K / 16;
+    if constexpr (MODE == XS_Q8) {
+        // the LDS-DMA of stage_issue lands before the barrier (vmcnt wait)
+    } else if constexpr (MODE == XS_F32_LDS || MODE == XS_NORM_LDS) {
+        const float * xf = (const float *) ((const char *) a.q + gemv_lds_base(K));
+        __syncthreads();                      // staged x (and norm weight) visible
+        float scale = 1.0f;
+        if constexpr (MODE == XS_NORM_LDS) {
+            float ss = 0.f;
+            for (int i = 4 * t; i < K; i += 4 * NT) {
+                const float4 f = *(const float4 *) (xf + i);
+                ss += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+            }
+            ss = wave_sum(ss);
+            if ((t & 63) == 0) red[t >> 6] = ss;
+            __syncthreads();
+            ss = 0.f;
+#pragma unroll
+            for (int wv = 0; wv < NT / 64; ++wv) ss += red[wv];
+            scale = 1.0f / sqrtf(ss / (float) K + xs.eps);
+        }
+        for (int hg = t; hg < nhg; hg += NT) {   // nhg is even: partner lanes stay paired
+            float v2[16];
+            load_half(hg, v2, xf);
+            if constexpr (MODE == XS_NORM_LDS) {
+                float w2[16];
+                load_half(hg, w2, xf + K);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v2[j] = (v2[j] * scale) * w2[j];
+            }
+            q8_half(v2, hg, a);
+        }
+    } else if constexpr (MODE == XS_NORM) {
+        // K <= 16 * HPT * NT (GEMV2_MAX_NORM_K checks it for the 256-thread kernels)
         float ss = 0.f;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int hg = t + NT * h;
-            if (hg < nhg) {
+        for (int h = 0; h < HPT; ++h) {
+            float sh = 0.f;
 #pragma unroll
-                for (int j = 0; j < 16; j += 4) {
-                    const float4 f = *(const float4 *) (xs.x + 16 * hg + j);
-                    v[h][j] = f.x; v[h][j + 1] = f.y; v[h][j + 2] = f.z; v[h][j + 3] = f.w;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) v[h][j] = 0.f;
-            }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) ss += v[h][j] * v[h][j];
+            for (int j = 0; j < 16; ++j) sh += r.v[h][j] * r.v[h][j];
+            ss += t + NT * h < nhg ? sh : 0.f;
         }
         ss = wave_sum(ss);
         if ((t & 63) == 0) red[t >> 6] = ss;
         __syncthreads();
         ss = 0.f;
 #pragma unroll
-        for (int w = 0; w < NT / 64; ++w) ss += red[w];
+        for (int wv = 0; wv < NT / 64; ++wv) ss += red[wv];
         const float scale = 1.0f / sqrtf(ss / (float) K + xs.eps);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < HPT; ++h) {
             const int hg = t + NT * h;
             if (hg < nhg) {
 #pragma unroll
-                for (int j = 0; j < 16; j += 4) {
-                    const float4 w = *(const float4 *) (xs.nw + 16 * hg + j);
-                    v[h][j] = (v[h][j] * scale) * w.x; v[h][j + 1] = (v[h][j + 1] * scale) * w.y;
-                    v[h][j + 2] = (v[h][j + 2] * scale) * w.z; v[h][j + 3] = (v[h][j + 3] * scale) * w.w;
-                }
-                q8_half(v[h], hg, a);
+                for (int j = 0; j < 16; ++j) r.v[h][j] = (r.v[h][j] * scale) * r.w[h][j];
+                q8_half(r.v[h], hg, a);
             }
         }
     } else {
-        for (int hg0 = 0; hg0 < nhg; hg0 += 2 * NT) {
-            float v[2][16];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int hg = hg0 + t + NT * h;
-                if (hg < nhg) {
-#pragma unroll
-                    for (int j = 0; j < 16; j += 4) {
-                        const float4 f = *(const float4 *) (xs.x + 16 * hg + j);
-                        v[h][j] = f.x; v[h][j + 1] = f.y; v[h][j + 2] = f.z; v[h][j + 3] = f.w;
-                    }
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int hg = hg0 + t + NT * h;
-                if (hg < nhg) q8_half(v[h], hg, a);
-            }
+        for (int h = 0; h < HPT; ++h) if (t + NT * h < nhg) q8_half(r.v[h], t + NT * h, a);
+        for (int hg = t + HPT * NT; hg < nhg; hg += NT) {
+            float v2[16];
+            load_half(hg, v2, xs.x);
+            q8_half(v2, hg, a);
         }
     }
     __syncthreads();
@@ -306,35 +388,53 @@ template <int QT> __host__ __device__ constexpr bool gemv2_type_ok() {
 }
 
 // One row's partial dot over its units, LPR lanes per row, UPL units per lane in
-// flight; weight loads for the first batch are issued before `stage` runs.
-template <int QT, int LPR, int UPL, int NM, typename Stage>
+// flight. Order: activation loads (stager.issue), weight loads of the first batch,
+// activation quantisation into LDS (stager.finish, waits only for its own loads),
+// dot products.
+template <int QT, int UPL, int NM>
+__device__ __forceinline__ void w2_load_batch(const char * const (&rows)[NM], int u0, int lpr, int units, W2<QT> (&r)[NM][UPL]) {
+#pragma unroll
+    for (int j = 0; j < UPL; ++j)
+#pragma unroll
+        for (int m = 0; m < NM; ++m) w2_load<QT>(rows[m], min(u0 + j * lpr, units - 1), r[m][j]);
+}
+
+template <int QT, int UPL, int NM>
+__device__ __forceinline__ void w2_dot_batch(const W2<QT> (&r)[NM][UPL], int u0, int lpr, int units, const LdsAct & a, float (&acc)[NM]) {
+#pragma unroll
+    for (int j = 0; j < UPL; ++j) {
+        if (u0 + j * lpr < units) {
+#pragma unroll
+            for (int m = 0; m < NM; ++m) acc[m] += w2_dot<QT>(r[m][j], u0 + j * lpr, a);
+        }
+    }
+}
+
+// One row's partial dot over its units, LPR lanes per row, UPL units per lane per batch.
+// Order: activation loads (stage_issue), weight batch 0, activation quantisation into
+// LDS (stage_finish, waits only for its own loads), dot products; later batches load and
+// compute in turn (a two-deep register pipeline measured slower: it costs occupancy).
+template <int QT, int LPR, int UPL, int NM, int NT, int MODE>
 __device__ __forceinline__ void gemv_rows(const char * const (&rows)[NM], int units, int sub, const LdsAct & a,
-                                          Stage && stage, float (&acc)[NM]) {
+                                          const XStage & xs, int K, float * red, float (&acc)[NM]) {
     W2<QT> r[NM][UPL];
 #pragma unroll
     for (int m = 0; m < NM; ++m) acc[m] = 0.f;
-    // block-uniform trip count: stage() holds a barrier
-    const int n_iter = (units + LPR * UPL - 1) / (LPR * UPL);
+    StageRegs<NT, MODE> sr;
+    stage_issue<NT, MODE>(xs, K, a, sr);
+    // block-uniform trip count: stage_finish holds a barrier
+    constexpr int STEP = LPR * UPL;
+    const int n_iter = (units + STEP - 1) / STEP;
     for (int it = 0; it < n_iter; ++it) {
-        const int u0 = it * LPR * UPL + sub;
-#pragma unroll
-        for (int j = 0; j < UPL; ++j)
-#pragma unroll
-            for (int m = 0; m < NM; ++m) w2_load<QT>(rows[m], min(u0 + j * LPR, units - 1), r[m][j]);
-        if (it == 0) stage();
-#pragma unroll
-        for (int j = 0; j < UPL; ++j) {
-            if (u0 + j * LPR < units) {
-#pragma unroll
-                for (int m = 0; m < NM; ++m) acc[m] += w2_dot<QT>(r[m][j], u0 + j * LPR, a);
-            }
-        }
+        w2_load_batch<QT, UPL, NM>(rows, it * STEP + sub, LPR, units, r);
+        if (it == 0) stage_finish<NT, MODE>(xs, K, a, red, sr);
+        w2_dot_batch<QT, UPL, NM>(r, it * STEP + sub, LPR, units, a, acc);
     }
-    if (n_iter == 0) stage();
+    if (n_iter == 0) stage_finish<NT, MODE>(xs, K, a, red, sr);
+    // row sum over the LPR lanes: in every lane for LPR <= 16, in the group's last lane
+    // (sub == LPR - 1) for LPR = 32, 64
 #pragma unroll
-    for (int m = 0; m < NM; ++m)
-#pragma unroll
-        for (int o = LPR / 2; o > 0; o >>= 1) acc[m] += __shfl_xor(acc[m], o, 64);
+    for (int m = 0; m < NM; ++m) acc[m] = dpp_sum_group<LPR>(acc[m]);
 }
 
 }  // namespace mx

@@ -17,6 +17,8 @@
 
 namespace mx {
 
+extern int g_tune[16];
+
 constexpr int FA_TILE = 256;
 constexpr int FA_MAXG = 8;
 
@@ -30,7 +32,11 @@ struct FaArgs {
     float scale, softcap, max_bias, m0, m1f;
     uint32_t n_head_log2;
     int k_aligned;                          // K rows 16-byte aligned → vector loads
+    unsigned long long * trace;             // debug: phase timestamps (MX_TRACE)
+    unsigned long long * trace_blk;
 };
+
+#define FA_TRACE(ph) MX_TRACE((blockIdx.x == 0 && blockIdx.y == 0) ? p.trace : nullptr, ph)
 
 template <typename T> __device__ __forceinline__ float ldkv(const T * p);
 template <> __device__ __forceinline__ float ldkv<uint16_t>(const uint16_t * p) { return h2f(*p); }
@@ -199,6 +205,8 @@ struct FaOut {
     int direct;
 };
 
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void h8(const uint4 v, float (&f)[8]) {
     f[0] = h2f((uint16_t) (v.x & 0xFFFF)); f[1] = h2f((uint16_t) (v.x >> 16));
     f[2] = h2f((uint16_t) (v.y & 0xFFFF)); f[3] = h2f((uint16_t) (v.y >> 16));
@@ -214,17 +222,22 @@ __global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
     constexpr int KQ = 64 / D8;                // key subsets of a wave in P·V
     constexpr int KPL = 64 / KQ;               // V rows per lane
     constexpr bool V_EARLY = D <= 128;         // V loads issued with K (register budget)
-    __shared__ float qs[G][D];
-    __shared__ float pw[4][G][64];
+    __shared__ __align__(16) _Float16 qs[G][D];
+    __shared__ __align__(16) float pw[4][G][64];
     __shared__ float wm[4][G], wl[4][G];
-    __shared__ float wo[4][G][D];
+    __shared__ __align__(16) float wo[4][G][D];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int Hkv = (int) p.Hkv, n_q = (int) p.n_q, n_kv = (int) p.n_kv;
+    // G = query heads per workgroup (a divisor of the GQA group Gt = H/Hkv): splitting a
+    // GQA group over workgroups trades K/V re-reads (L2) for shorter per-wave chains
+    const int Gt = (int) (p.H / p.Hkv), NGB = Gt / G;
     const int bx = blockIdx.x;
     const int hk = bx % Hkv;
-    const int iq1 = (bx / Hkv) % n_q;
-    const int iq3 = bx / (Hkv * n_q);
+    const int gb = (bx / Hkv) % NGB;
+    const int iq1 = (bx / (Hkv * NGB)) % n_q;
+    const int iq3 = bx / (Hkv * NGB * n_q);
+    const int hb = hk * Gt + gb * G;                    // first query head of this workgroup
     const int split = blockIdx.y;
     const int kw0 = split * FW_CH + wave * 64;          // first key of this wave
     const int key = kw0 + lane;
@@ -232,6 +245,19 @@ __global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
     const char * vb = p.v + hk * p.v2 + (iq3 % (int) p.ns) * p.v3;
     const int vc = lane % D8, vq = lane / D8;           // P·V: 16-byte chunk, key subset
 
+    FA_TRACE(0);
+    MX_TRACE_BLK(p.trace_blk, 0);
+    // q first: loads retire in issue order, so the LDS fill below waits only for these
+    constexpr int QPT = (G * D + 255) / 256;
+    float qreg[QPT];
+#pragma unroll
+    for (int j = 0; j < QPT; ++j) {
+        const int i = tid + 256 * j;
+        qreg[j] = i < G * D ? *(const float *) (p.q + iq1 * p.q1 + (hb + i / D) * p.q2 + iq3 * p.q3 + (i % D) * 4) : 0.f;
+    }
+    const bool live = key < n_kv;
+    float mv = 0.f;
+    if (p.mask && live) mv = h2f(((const uint16_t *) (p.mask + iq1 * p.m1 + (iq3 % (int) p.mne3) * p.m3))[key]);
     uint4 kr[NKL];
     {
         const uint4 * src = (const uint4 *) (kb + (size_t) min(key, n_kv - 1) * p.k1);
@@ -245,31 +271,32 @@ __global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
             vr[j] = *(const uint4 *) (vb + (size_t) min(kw0 + vq * KPL + j, n_kv - 1) * p.v1 + vc * 16);
     };
     if constexpr (V_EARLY) load_v();
-    const bool live = key < n_kv;
-    float mv = 0.f;
-    if (p.mask && live) mv = h2f(((const uint16_t *) (p.mask + iq1 * p.m1 + (iq3 % (int) p.mne3) * p.m3))[key]);
-    for (int i = tid; i < G * D; i += 256) {
-        const int g = i / D, d = i % D;
-        const float x = *(const float *) (p.q + iq1 * p.q1 + (hk * G + g) * p.q2 + iq3 * p.q3 + d * 4);
-        qs[g][d] = (float) (_Float16) x;   // the CPU vec-dot rounds q to the K type
+#pragma unroll
+    for (int j = 0; j < QPT; ++j) {
+        const int i = tid + 256 * j;
+        if (i < G * D) qs[i / D][i % D] = (_Float16) qreg[j];   // the CPU vec-dot rounds q to the K type
     }
     __syncthreads();
+    FA_TRACE(1);
     if constexpr (!V_EARLY) load_v();
-    // ---- scores (lane = key) and wave softmax, one head at a time (bounded live ranges)
+    // ---- scores (lane = key) and wave softmax, one head at a time (bounded live ranges):
+    // q·k as packed f16 pairs with f32 accumulation (v_dot2_f32_f16), q broadcast from LDS
 #pragma unroll 1
     for (int g = 0; g < G; ++g) {
-        float acc = 0.f;
+        uint4 qv[NKL];
+#pragma unroll
+        for (int j = 0; j < NKL; ++j) qv[j] = *(const uint4 *) &qs[g][8 * j];
+        float a4[4] = {0.f, 0.f, 0.f, 0.f};   // four independent chains
 #pragma unroll
         for (int j = 0; j < NKL; ++j) {
-            float kv[8];
-            h8(kr[j], kv);
-            const float4 q0 = *(const float4 *) &qs[g][8 * j];
-            const float4 q1 = *(const float4 *) &qs[g][8 * j + 4];
-            acc += q0.x * kv[0] + q0.y * kv[1] + q0.z * kv[2] + q0.w * kv[3]
-                 + q1.x * kv[4] + q1.y * kv[5] + q1.z * kv[6] + q1.w * kv[7];
+            a4[0] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kr[j].x), __builtin_bit_cast(h2_t, qv[j].x), a4[0], false);
+            a4[1] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kr[j].y), __builtin_bit_cast(h2_t, qv[j].y), a4[1], false);
+            a4[2] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kr[j].z), __builtin_bit_cast(h2_t, qv[j].z), a4[2], false);
+            a4[3] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kr[j].w), __builtin_bit_cast(h2_t, qv[j].w), a4[3], false);
         }
+        const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         float s = -INFINITY;
-        const int h = hk * G + g;
+        const int h = hb + g;
         float m = mv;
         if (p.mask && p.mne2 > 1)
             m = live ? h2f(((const uint16_t *) (p.mask + iq1 * p.m1 + (h % (int) p.mne2) * p.m2 + (iq3 % (int) p.mne3) * p.m3))[key]) : 0.f;
@@ -286,38 +313,55 @@ __global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
         pw[wave][g][lane] = e;
         if (lane == 0) { wm[wave][g] = mx; wl[wave][g] = l; }
     }
+    FA_TRACE(2);
     __syncthreads();
-    // ---- P·V: lane = (16-byte chunk vc, key subset vq), one head at a time
-#pragma unroll 1
-    for (int g = 0; g < G; ++g) {
-        float o[8];
+    FA_TRACE(3);
+    // ---- P·V: lane = (16-byte chunk vc, key subset vq); the G heads share each V row
+    float o[G][8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = 0.f;
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int j = 0; j < KPL; ++j) {
+        for (int i = 0; i < 8; ++i) o[g][i] = 0.f;
+#pragma unroll
+    for (int j4 = 0; j4 < KPL; j4 += 4) {
+        float4 w4[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) w4[g] = *(const float4 *) &pw[wave][g][vq * KPL + j4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
             float v[8];
-            h8(vr[j], v);
-            const float w = pw[wave][g][vq * KPL + j];
+            h8(vr[j4 + jj], v);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] += w * v[i];
+            for (int g = 0; g < G; ++g) {
+                const float w = jj == 0 ? w4[g].x : (jj == 1 ? w4[g].y : (jj == 2 ? w4[g].z : w4[g].w));
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[g][i] += w * v[i];
+            }
         }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int off = D8; off < 64; off <<= 1) o[i] += __shfl_xor(o[i], off, 64);
-        if (vq == 0) {
-            *(float4 *) &wo[wave][g][vc * 8] = make_float4(o[0], o[1], o[2], o[3]);
-            *(float4 *) &wo[wave][g][vc * 8 + 4] = make_float4(o[4], o[5], o[6], o[7]);
+            for (int off = D8; off < 64; off <<= 1) o[g][i] += __shfl_xor(o[g][i], off, 64);
+    if (vq == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            *(float4 *) &wo[wave][g][vc * 8] = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
+            *(float4 *) &wo[wave][g][vc * 8 + 4] = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
         }
     }
+    FA_TRACE(4);
     __syncthreads();
+    FA_TRACE(5);
     // ---- merge the four waves
     const int rows = (int) (p.ns * p.n_q * p.H);
-    const int row0 = (iq3 * n_q + iq1) * (int) p.H + hk * G;
+    const int row0 = (iq3 * n_q + iq1) * (int) p.H + hb;
     for (int i = tid; i < G * D; i += 256) {
         const int g = i / D, d = i % D;
         float M = fmaxf(fmaxf(wm[0][g], wm[1][g]), fmaxf(wm[2][g], wm[3][g]));
-        const int h = hk * G + g;
+        const int h = hb + g;
         const float sk = (fo.direct && fo.sinks) ? fo.sinks[h] : -INFINITY;
         M = fmaxf(M, sk);
         float L = 0.f, O = 0.f;
@@ -339,6 +383,8 @@ __global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
             }
         }
     }
+    FA_TRACE(6);
+    MX_TRACE_BLK(p.trace_blk, 1);
 }
 
 // Merge the split partials of one output row (block = row, 64 threads). All loads of
@@ -543,12 +589,20 @@ void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
     b.ns = q->ne[3];
     // kernel indexes K/V by (iq3 % ns): pass kv stream count through k3 stride when ns==1
     if (k->ne[3] == 1) { b.k3 = 0; b.v3 = 0; }
+    b.trace = mx_trace_slot(0);
+    b.trace_blk = mx_trace_blocks();
     b.k_aligned = ((uintptr_t) k->data % 16 == 0) && k->nb[1] % 16 == 0 && k->nb[2] % 16 == 0 && k->nb[3] % 16 == 0;
     const float * psk = sk ? (const float *) sk->data : nullptr;
     if (fa_use_dec(dst)) {
-        const int G = (int) (q->ne[2] / k->ne[2]);
+        const int Gt = (int) (q->ne[2] / k->ne[2]);
         const FaOut fo{psk, (char *) dst->data, dst->nb[1], dst->nb[2], dst->nb[3], nsplit == 1};
-#define DEC(DD, GG) if (D == DD && G == GG) k_fattn_dec<DD, GG><<<grid, 256, 0, c.st>>>(b, fo); else
+        // heads per workgroup: one while the grid is small (short caches), the whole
+        // GQA group once there are enough splits to fill the chip
+        const int64_t blocks_full = k->ne[2] * q->ne[1] * q->ne[3] * nsplit;
+        int G = blocks_full >= 128 ? Gt : 1;
+        if (g_tune[7]) G = std::min(g_tune[7], Gt);
+        const dim3 gridd((unsigned) (q->ne[1] * k->ne[2] * (Gt / G) * q->ne[3]), (unsigned) nsplit);
+#define DEC(DD, GG) if (D == DD && G == GG) k_fattn_dec<DD, GG><<<gridd, 256, 0, c.st>>>(b, fo); else
 #define DECG(DD) DEC(DD, 1) DEC(DD, 2) DEC(DD, 4) DEC(DD, 8)
         DECG(64) DECG(128) DECG(256) MX_ABORT("fattn dec D=%d G=%d", D, G);
 #undef DECG

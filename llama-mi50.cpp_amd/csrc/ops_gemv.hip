@@ -17,12 +17,14 @@ struct G2Args {
     int nrows, units, K;
     XStage xs;
     int8_t * q8o; float * q8od; float * q8os;   // EPI 1 with 8 waves: q8 form of the output
+    unsigned long long * trace;                 // debug (MX_TRACE), workgroup 0
+    unsigned long long * trace_blk;             // debug (MX_TRACE_BLK), every workgroup
 };
 
 // EPI 0 store, 1 SwiGLU(w, w2), 2 + residual. W waves per block; with W = 8 and
 // LPR = 16 a block owns 32 consecutive rows and (q8o != null) also emits the q8
 // activation of its 32 outputs for the next GEMV (the FFN down projection).
-template <int QT, int LPR, int UPL, int EPI, int W>
+template <int QT, int LPR, int UPL, int EPI, int W, int MODE>
 __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     extern __shared__ __align__(16) char smem[];
     __shared__ float o32[32];
@@ -37,28 +39,30 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     rows[0] = p.w + rr * p.w_row;
     if constexpr (NM == 2) rows[1] = p.w2 + rr * p.w_row;
     const LdsAct a = lds_act(smem, p.K);
-    float * red = (float *) (smem + gemv_lds_bytes(p.K) - 64);
+    float * red = gemv_lds_red(smem, p.K);
     float acc[NM];
-    gemv_rows<QT, LPR, UPL, NM>(rows, p.units, sub, a, [&] { stage_x<64 * W>(p.xs, p.K, a, red); }, acc);
+    unsigned long long * tr = blockIdx.x == 0 ? p.trace : nullptr;
+    MX_TRACE(tr, 0);
+    MX_TRACE_BLK(p.trace_blk, 0);
+    gemv_rows<QT, LPR, UPL, NM, 64 * W, MODE>(rows, p.units, sub, a, p.xs, p.K, red, acc);
+    MX_TRACE(tr, 3);
     float v = acc[0];
     if constexpr (EPI == 1) v = (v / (1.0f + expf(-v))) * acc[1];
     if constexpr (EPI == 2) v += valid ? p.res[row] : 0.f;
-    if (sub == 0 && valid) p.dst[row] = v;
+    if (sub == LPR - 1 && valid) p.dst[row] = v;
+    MX_TRACE(tr, 4);
+    MX_TRACE_BLK(p.trace_blk, 1);
     if constexpr (W * RPW == 32) {
         if (p.q8o) {     // block-uniform
-            if (sub == 0) o32[row & 31] = v;
+            if (sub == LPR - 1) o32[row & 31] = v;
             __syncthreads();
             if (wave == 0 && lane < 32) {
                 const float x = o32[lane];
-                float amax = fabsf(x);
-#pragma unroll
-                for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 32));
+                const float amax = lane_bcast(dpp_max_group<32>(fabsf(x)), 31);
                 const float dd = amax / 127.0f;
                 const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
                 const int qi = (int) roundf(x * id);
-                int sum = qi;
-#pragma unroll
-                for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
+                const int sum = __builtin_amdgcn_readlane(dpp_sum_group_i<32>(qi), 31);
                 p.q8o[blockIdx.x * 32 + lane] = (int8_t) qi;
                 if (lane == 0) { p.q8od[blockIdx.x] = dd; p.q8os[blockIdx.x] = dd * (float) sum; }
             }
@@ -70,19 +74,29 @@ template <int QT, int LPR, int UPL, int EPI, int W = 4>
 static void launch_cfg(hipStream_t st, const G2Args & p) {
     constexpr int RPB = W * (64 / LPR);
     const unsigned grid = (unsigned) ((p.nrows + RPB - 1) / RPB);
-    k_gemv2<QT, LPR, UPL, EPI, W><<<grid, 64 * W, gemv_lds_bytes(p.K), st>>>(p);
+    const int mode = gemv_mode(p.xs, p.K, p.nrows);
+    const size_t lds = gemv_lds_bytes(p.K, mode);
+    switch (mode) {
+        case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_NORM_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_LDS><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_F32_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32_LDS><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_NORM: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM><<<grid, 64 * W, lds, st>>>(p); break;
+        default: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32><<<grid, 64 * W, lds, st>>>(p); break;
+    }
 }
 
 template <int QT, int EPI>
 static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
     if constexpr (EPI == 1) {
-        if (p.q8o) return launch_cfg<QT, 16, 2, 1, 8>(st, p);   // 32 rows per block
+        if (p.q8o) {   // 32 rows per block; g_tune[4] picks the geometry (sweeps)
+            if (g_tune[4] == 1) return launch_cfg<QT, 16, 2, 1, 8>(st, p);
+            return launch_cfg<QT, 32, 1, 1, 16>(st, p);   // best in the ffn sweep
+        }
     }
     constexpr bool FULL = QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q6_K;   // full tuning grid
     if constexpr (FULL) {
 #define CFG(L, U) if (lpr == L && upl == U) return launch_cfg<QT, L, U, EPI>(st, p);
         CFG(16, 2) CFG(16, 4) CFG(32, 2) CFG(32, 4) CFG(64, 2) CFG(64, 4)
-        if constexpr (EPI != 1) { CFG(16, 8) CFG(32, 8) CFG(64, 8) }
 #undef CFG
     }
     constexpr int U = EPI == 1 ? 2 : 4;
@@ -135,6 +149,8 @@ void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, cons
     p.K = (int) w->ne[0];
     p.units = units_of(w->type, w->ne[0]);
     p.xs = xs;
+    p.trace = mx_trace_slot(1);
+    p.trace_blk = mx_trace_blocks();
     const bool glu = w2 != nullptr;
     if (q8out) {
         MX_ASSERT(glu && p.nrows % 32 == 0);

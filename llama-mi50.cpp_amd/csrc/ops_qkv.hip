@@ -27,6 +27,8 @@ struct QkvArgs {
     const int32_t * pos; const float * ff;
     int n_dims;
     float theta_scale, freq_scale, ext_factor, attn_factor, corr0, corr1;
+    unsigned long long * trace;    // debug (MX_TRACE), workgroup 0
+    unsigned long long * trace_blk;
 };
 
 __device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i) {
@@ -34,7 +36,7 @@ __device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i)
 }
 
 // LPR = 16: the RoPE pair (rows 2i, 2i+1) sits 16 lanes apart in one wave
-template <int QTA, int QTV>
+template <int QTA, int QTV, int MODE>
 __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     extern __shared__ __align__(16) char smem[];
     constexpr int LPR = 16, UPL = 4;
@@ -47,11 +49,15 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     const bool valid = row < p.rows[m];
     const char * rows[1] = {p.w[m] + (int64_t) (valid ? row : p.rows[m] - 1) * p.w_row[m]};
     const LdsAct a = lds_act(smem, p.K);
-    float * red = (float *) (smem + gemv_lds_bytes(p.K) - 64);
+    float * red = gemv_lds_red(smem, p.K);
     float acc[1];
-    auto stage = [&] { stage_x<256>(p.xs, p.K, a, red); };
-    if (m == 2) gemv_rows<QTV, LPR, UPL, 1>(rows, p.units_v, sub, a, stage, acc);   // block-uniform branch
-    else gemv_rows<QTA, LPR, UPL, 1>(rows, p.units_a, sub, a, stage, acc);
+    unsigned long long * tr = blockIdx.x == 0 ? p.trace : nullptr;
+    MX_TRACE(tr, 0);
+    MX_TRACE_BLK(p.trace_blk, 0);
+    if (m == 2) gemv_rows<QTV, LPR, UPL, 1, 256, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, acc);   // block-uniform branch
+    else gemv_rows<QTA, LPR, UPL, 1, 256, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, acc);
+    MX_TRACE(tr, 3);
+    MX_TRACE_BLK(p.trace_blk, 1);
     const float v = acc[0];
     const float pv = __shfl_xor(v, 16, 64);
     if (sub != 0 || !valid) return;
@@ -81,6 +87,7 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     const float r = odd ? x0 * sn + x1 * cs : x0 * cs - x1 * sn;
     if (m == 0) p.q_out[row] = r;
     else *(uint16_t *) (p.kc + read_idx(p.kidx, p.kidx64, 0) * p.kc_nb1 + row * 2) = f2h(r);
+    MX_TRACE(tr, 4);
 }
 
 static const ggml_tensor * base_of(const ggml_tensor * t) {
@@ -170,6 +177,8 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     p.pos = (const int32_t *) rq->src[1]->data;
     p.ff = rq->src[2] ? (const float *) rq->src[2]->data : nullptr;
     p.n_dims = n_dims;
+    p.trace = mx_trace_slot(2);
+    p.trace_blk = mx_trace_blocks();
     const int n_ctx_orig = mx_op_param<int32_t>(rq, 4);
     const float base = mx_op_param<float>(rq, 5);
     p.freq_scale = mx_op_param<float>(rq, 6);
@@ -181,16 +190,24 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
 
     const int ta = wq->type, tv = wv->type;
     void (*kern)(QkvArgs) = nullptr;
-#define QKV(TA, TV) if (ta == TA && tv == TV) kern = k_qkv_rope_store<TA, TV>;
+#define QKV(TA, TV) if (ta == TA && tv == TV) kern = k_qkv_rope_store<TA, TV, XS_NORM>;
     QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
     QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
     QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
 #undef QKV
     if (!kern) return 0;
     if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs)) return 0;
+    const int mode = gemv_mode(p.xs, p.K);
+    if (mode != XS_NORM) {   // the fused block normally follows attn_norm; other sources
+#define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8> : k_qkv_rope_store<TA, TV, XS_F32>;
+        QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
+        QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
+        QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
+#undef QKV
+    }
     for (int j = i; j <= last; ++j) act_cache_invalidate(c.s, g->nodes[j]);
     const dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
-    hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K), c.st, p);
+    hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K, mode), c.st, p);
     return last - i + 1;
 }
 

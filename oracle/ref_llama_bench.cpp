@@ -9,6 +9,7 @@
 // -ngl > 0 with GGML_BACKEND_PATH=libggml-mi355x.so runs the reference libllama on the
 // MI355X backend unmodified (the drop-in check).
 #include "llama.h"
+#include "ggml-backend.h"
 
 #include <algorithm>
 #include <chrono>
@@ -24,7 +25,7 @@ static double now_s() {
 
 int main(int argc, char ** argv) {
     std::string model, tok_in, logits_out;
-    int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0;
+    int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0, incremental = 0;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() { return std::string(argv[++i]); };
@@ -36,10 +37,14 @@ int main(int argc, char ** argv) {
         else if (a == "-fa") fa = std::stoi(next());
         else if (a == "-c") n_ctx = std::stoi(next());
         else if (a == "--logits") { tok_in = next(); logits_out = next(); }
+        else if (a == "--incremental") incremental = 1;   // logits mode: one token per llama_decode
     }
     llama_log_set([](ggml_log_level, const char *, void *) {}, nullptr);
     llama_backend_init();
     ggml_backend_load_all();
+    for (size_t i = 0; i < ggml_backend_dev_count(); ++i)
+        fprintf(stderr, "device %zu: %s (%s)\n", i, ggml_backend_dev_name(ggml_backend_dev_get(i)),
+                ggml_backend_dev_description(ggml_backend_dev_get(i)));
     llama_model_params mp = llama_model_default_params();
     mp.n_gpu_layers = ngl;
     llama_model * m = llama_model_load_from_file(model.c_str(), mp);
@@ -64,7 +69,17 @@ int main(int argc, char ** argv) {
     llama_context * ctx = llama_init_from_model(m, cp);
     if (!ctx) { fprintf(stderr, "context failed\n"); return 1; }
 
-    if (!toks.empty()) {
+    if (!toks.empty() && incremental) {
+        FILE * f = fopen(logits_out.c_str(), "wb");
+        for (size_t i = 0; i < toks.size(); ++i) {
+            llama_token t = toks[i];
+            if (llama_decode(ctx, llama_batch_get_one(&t, 1)) != 0) { fprintf(stderr, "decode failed\n"); return 1; }
+            llama_synchronize(ctx);
+            fwrite(llama_get_logits_ith(ctx, -1), sizeof(float), n_vocab, f);
+        }
+        fclose(f);
+        printf("{\"n_tokens\": %zu, \"n_vocab\": %d, \"incremental\": 1}\n", toks.size(), n_vocab);
+    } else if (!toks.empty()) {
         llama_batch b = llama_batch_init((int) toks.size(), 0, 1);
         for (size_t i = 0; i < toks.size(); ++i) {
             b.token[i] = toks[i]; b.pos[i] = (llama_pos) i; b.n_seq_id[i] = 1; b.seq_id[i][0] = 0; b.logits[i] = 1;

@@ -1,0 +1,100 @@
+"""Drop-in parity: the reference's own libllama (oracle/_ref, built from /root/reference
+sources) runs a GGUF unmodified with libggml-mi355x.so loaded through
+GGML_BACKEND_PATH and all layers offloaded (-ngl 99); its logits must match the same
+libllama on the reference CPU backend (-ngl 0). Also: this package's own runner on the
+same GGUF against the reference CPU logits.
+
+Tolerance: NMSE 2e-3 on whole-model logits (the reference's test-backend-ops bound for
+full graphs); prefill (one ubatch, MFMA GEMM path) and incremental decode
+(one token per llama_decode: GEMV / decode-FA / fused QKV path) are both checked.
+Synthetic GGUFs come from tools/gguf_synth.py (random weights, seeded)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from qgen import nmse
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref", "ref-llama-bench")
+LIB = os.path.join(ROOT, "llama-mi50.cpp_amd", "lib", "libggml-mi355x.so")
+TOL = 2e-3
+
+
+def _need_ref():
+    if not os.path.exists(REF):
+        pytest.skip("oracle/_ref/ref-llama-bench not built")
+
+
+@pytest.fixture(scope="module")
+def ggufs(tmp_path_factory):
+    d = tmp_path_factory.mktemp("gguf")
+    out = {}
+    for shape, recipe in [("tiny", "q4_k_m"), ("small", "q4_k_m"), ("small", "q4_0"), ("small", "q8_0"), ("tiny_moe", "q4_k_m")]:
+        path = str(d / f"{shape}_{recipe}.gguf")
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gguf_synth.py"), "--shape", shape,
+                        "--recipe", recipe, "--out", path], check=True, timeout=300)
+        out[(shape, recipe)] = path
+    return out
+
+
+def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False):
+    tf = tmp_path / "toks.i32"
+    of = tmp_path / f"logits_{ngl}_{fa}_{int(incremental)}.f32"
+    np.asarray(toks, np.int32).tofile(tf)
+    env = dict(os.environ)
+    if ngl > 0:
+        env["GGML_BACKEND_PATH"] = LIB
+    cmd = [REF, "-m", gguf, "-t", "8", "-ngl", str(ngl), "-fa", str(fa), "--logits", str(tf), str(of)]
+    if incremental:
+        cmd.append("--incremental")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n_vocab = int(r.stdout.strip().splitlines()[-1].split('"n_vocab": ')[1].split(",")[0].rstrip("}"))
+    return np.fromfile(of, np.float32).reshape(len(toks), n_vocab), r.stderr
+
+
+CASES = [("tiny", "q4_k_m"), ("small", "q4_k_m"), ("small", "q4_0"), ("small", "q8_0"), ("tiny_moe", "q4_k_m")]
+
+
+@pytest.mark.parametrize("shape,recipe", CASES)
+@pytest.mark.parametrize("fa", [1, 0])
+def test_dropin_prefill(ggufs, tmp_path, shape, recipe, fa):
+    _need_ref()
+    toks = np.random.default_rng(7).integers(0, 1000, 40)
+    cpu, _ = run_ref(tmp_path, ggufs[(shape, recipe)], toks, 0, fa)
+    gpu, log = run_ref(tmp_path, ggufs[(shape, recipe)], toks, 99, fa)
+    assert "MI355X" in log, "the MI355X backend was not loaded:\n" + log[-1000:]
+    assert np.all(np.isfinite(gpu))
+    assert nmse(gpu, cpu) < TOL
+
+
+@pytest.mark.parametrize("shape,recipe", [("tiny", "q4_k_m"), ("small", "q4_k_m"), ("small", "q4_0")])
+@pytest.mark.parametrize("fa", [1, 0])
+def test_dropin_incremental_decode(ggufs, tmp_path, shape, recipe, fa):
+    _need_ref()
+    toks = np.random.default_rng(8).integers(0, 1000, 24)
+    cpu, _ = run_ref(tmp_path, ggufs[(shape, recipe)], toks, 0, fa, incremental=True)
+    gpu, log = run_ref(tmp_path, ggufs[(shape, recipe)], toks, 99, fa, incremental=True)
+    assert "MI355X" in log
+    assert nmse(gpu, cpu) < TOL
+
+
+@pytest.mark.parametrize("shape,recipe", [("small", "q4_k_m"), ("tiny_moe", "q4_k_m")])
+def test_runner_matches_reference_cpu(pkg, backend, ggufs, tmp_path, shape, recipe):
+    """This package's Llama runner (graph builder + executor) on the same GGUF."""
+    _need_ref()
+    toks = np.random.default_rng(9).integers(0, 1000, 24).astype(np.int32)
+    cpu, _ = run_ref(tmp_path, ggufs[(shape, recipe)], toks, 0, 1)
+    m = pkg.Model.load_gguf(backend, ggufs[(shape, recipe)])
+    s = pkg.Session(m, n_ctx=256, flash_attn=True)
+    pre = s.decode_all(toks)
+    s.reset()
+    inc = np.stack([s.decode(toks[i:i + 1]) for i in range(len(toks))])
+    s.free(); m.free()
+    assert nmse(pre, cpu) < TOL
+    assert nmse(inc, cpu) < TOL

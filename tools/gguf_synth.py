@@ -24,6 +24,8 @@ SHAPES = {
                       n_ctx=2048, rope_base=10000.0),
     "tiny": dict(n_vocab=1024, n_embd=256, n_layer=2, n_head=4, n_head_kv=2, n_ff=512, n_ctx=1024,
                  rope_base=10000.0),
+    "small": dict(n_vocab=4096, n_embd=1024, n_layer=4, n_head=8, n_head_kv=2, n_ff=2816, n_ctx=2048,
+                  rope_base=500000.0),
     "tiny_moe": dict(n_vocab=1024, n_embd=256, n_layer=2, n_head=4, n_head_kv=2, n_ff=512, n_ctx=1024,
                      rope_base=10000.0, n_expert=4, n_expert_used=2),
 }

@@ -68,6 +68,64 @@ def case_gemv(pkg, be, rng, tname, K, M, glu=False, add=False):
     return ctx, graphs
 
 
+def case_ffn(pkg, be, rng, tname="q4_K", tdown="q4_K", K=4096, F=14336):
+    """ffn_norm-less FFN block: gate/up SwiGLU GEMV (+q8 of its output) -> down + residual."""
+    tid, tdn = NAMES[tname], NAMES[tdown]
+    wg, _ = rand_quant(tid, F, K, rng)
+    wd, _ = rand_quant(tdn, K, F, rng)
+    n = copies_for(2 * len(wg) + len(wd))
+    ctx = pkg.Context()
+    x = ctx.new_tensor("f32", K, 1)
+    graphs, ws = [], []
+    for _ in range(n):
+        tg, tu, td = ctx.new_tensor(tid, K, F), ctx.new_tensor(tid, K, F), ctx.new_tensor(tdn, F, K)
+        ws += [(tg, wg), (tu, wg), (td, wd)]
+        h = ctx.swiglu_split(ctx.mul_mat(tg, x), ctx.mul_mat(tu, x))
+        graphs.append(ctx.add(ctx.mul_mat(td, h), x))
+    graphs = [ctx.build(o) for o in graphs]
+    ctx.alloc(be)
+    for t, w in ws:
+        t.set(w)
+    x.set(rng.standard_normal(K).astype(np.float32))
+    return ctx, graphs
+
+
+def case_attn_in(pkg, be, rng, K=4096, H=32, Hkv=8, hd=128, n_ctx=512, tv="q6_K"):
+    """attn_norm -> Q/K/V GEMVs -> RoPE(q, k) -> KV-cache stores: the fused QKV kernel."""
+    tq = NAMES["q4_K"]
+    wq, _ = rand_quant(tq, H * hd, K, rng)
+    wk, _ = rand_quant(tq, Hkv * hd, K, rng)
+    wv, _ = rand_quant(NAMES[tv], Hkv * hd, K, rng)
+    n = copies_for(len(wq) + len(wk) + len(wv))
+    ctx = pkg.Context()
+    x = ctx.new_tensor("f32", K, 1)
+    nw = ctx.new_tensor("f32", K)
+    pos = ctx.new_tensor("i32", 1)
+    kidx = ctx.new_tensor("i64", 1)
+    graphs, ws = [], []
+    for _ in range(n):
+        a, b, c = ctx.new_tensor(tq, K, H * hd), ctx.new_tensor(tq, K, Hkv * hd), ctx.new_tensor(NAMES[tv], K, Hkv * hd)
+        ws += [(a, wq), (b, wk), (c, wv)]
+        kc = ctx.new_tensor("f16", Hkv * hd, n_ctx)
+        vc = ctx.new_tensor("f16", Hkv * hd, n_ctx)
+        cur = ctx.mul(ctx.rms_norm(x, 1e-5), nw)
+        q = ctx.rope_ext(ctx.reshape(ctx.mul_mat(a, cur), hd, H, 1), pos, None, hd, 0, 8192, 500000.0)
+        v = ctx.mul_mat(c, cur)
+        k = ctx.rope_ext(ctx.reshape(ctx.mul_mat(b, cur), hd, Hkv, 1), pos, None, hd, 0, 8192, 500000.0)
+        sk = ctx.set_rows(kc, ctx.reshape(k, Hkv * hd, 1), kidx)
+        sv = ctx.set_rows(vc, v, kidx)
+        graphs.append((q, sk, sv))
+    graphs = [ctx.build(*o) for o in graphs]
+    ctx.alloc(be)
+    for t, w in ws:
+        t.set(w)
+    x.set(rng.standard_normal(K).astype(np.float32))
+    nw.set(np.ones(K, np.float32))
+    pos.set(np.array([17], np.int32))
+    kidx.set(np.array([17], np.int64))
+    return ctx, graphs
+
+
 def case_fa(pkg, be, rng, n_kv, H=32, Hkv=8, D=128):
     ctx = pkg.Context()
     q = ctx.new_tensor("f32", D, 1, H)
@@ -105,6 +163,9 @@ CASES = {
     "down_q4k_add": lambda p, b, r: case_gemv(p, b, r, "q4_K", 14336, 4096, add=True),
     "down_q6k_add": lambda p, b, r: case_gemv(p, b, r, "q6_K", 14336, 4096, add=True),
     "lm_head_q6k": lambda p, b, r: case_gemv(p, b, r, "q6_K", 4096, 128256),
+    "attn_in": lambda p, b, r: case_attn_in(p, b, r),
+    "ffn_q4k": lambda p, b, r: case_ffn(p, b, r),
+    "ffn_q4k_q6k": lambda p, b, r: case_ffn(p, b, r, tdown="q6_K"),
     "fa_256": lambda p, b, r: case_fa(p, b, r, 256),
     "fa_1024": lambda p, b, r: case_fa(p, b, r, 1024),
     "fa_4096": lambda p, b, r: case_fa(p, b, r, 4096),
@@ -120,6 +181,9 @@ def main():
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--iters", type=int, default=ITERS)
     ap.add_argument("--sweep", action="store_true", help="GEMV cases under every (lanes/row, units/lane) geometry")
+    ap.add_argument("--trace", action="store_true", help="print phase timestamps of workgroup 0")
+    ap.add_argument("--trace-blocks", action="store_true", help="GEMV cases: per-workgroup start/end spread")
+    ap.add_argument("--sweep-glu8", action="store_true", help="ffn cases under every q8-emitting SwiGLU geometry")
     args = ap.parse_args()
     pkg = load_package()
     lib = pkg._lib.load()
@@ -128,9 +192,55 @@ def main():
     names = []
     for name in args.only or list(CASES):
         cfgs = [None]
-        if args.sweep and not name.startswith(("fa_", "rms")):
+        if args.sweep and not name.startswith(("fa_", "rms", "ffn")):
             cfgs = [c for c in SWEEP if not (name.startswith("glu") and c[1] == 8)]
         ctx, graphs = CASES[name](pkg, be, rng)
+        if args.sweep_glu8 and name.startswith("ffn"):
+            for v in range(4):
+                lib.ggml_backend_mi355x_set_tune(4, v)
+                separator(pkg, be)
+                for it in range(args.iters):
+                    ctx.compute(be, graphs[it % len(graphs)])
+                be.synchronize()
+                names.append(f"{name}@glu8v{v}")
+            lib.ggml_backend_mi355x_set_tune(4, 0)
+            ctx.free()
+            continue
+        if args.trace:
+            import ctypes
+            lib.ggml_backend_mi355x_set_tune(6, 1)
+            buf = (ctypes.c_ulonglong * 2048)()
+            lib.ggml_backend_mi355x_trace_read(buf, 2048)        # clear
+            for it in range(3):
+                ctx.compute(be, graphs[it % len(graphs)])
+            be.synchronize()
+            lib.ggml_backend_mi355x_trace_read(buf, 2048)
+            lib.ggml_backend_mi355x_set_tune(6, 0)
+            for slot, sname in enumerate(["fa_dec", "gemv", "qkv"]):
+                for w in range(16):
+                    t = [buf[slot * 128 + w * 8 + k] for k in range(8)]
+                    if t[0] == 0:
+                        continue
+                    print(f"trace {name} {sname} wave{w}: " + " ".join(str(x - t[0]) if x else "-" for x in t[1:]), flush=True)
+        if args.trace_blocks:
+            import ctypes
+            lib.ggml_backend_mi355x_set_tune(6, 2)
+            for it in range(3):
+                ctx.compute(be, graphs[it % len(graphs)])
+            be.synchronize()
+            n = 2 * 65536
+            buf = (ctypes.c_ulonglong * n)()
+            lib.ggml_backend_mi355x_trace_blocks_read(buf, n)
+            lib.ggml_backend_mi355x_set_tune(6, 0)
+            a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 2).astype(np.int64)
+            a = a[(a[:, 0] > 0) & (a[:, 1] > 0)]
+            if len(a):
+                t0 = a[:, 0].min()
+                st, en = (a[:, 0] - t0) * 10, (a[:, 1] - t0) * 10   # ns
+                dur = en - st
+                print(f"blocks {name}: n={len(a)} start[p50,p90,max]={np.percentile(st,50):.0f},{np.percentile(st,90):.0f},{st.max():.0f}ns "
+                      f"end[min,p50,max]={en.min():.0f},{np.percentile(en,50):.0f},{en.max():.0f}ns dur[p10,p50,p90]={np.percentile(dur,10):.0f},"
+                      f"{np.percentile(dur,50):.0f},{np.percentile(dur,90):.0f}ns", flush=True)
         for cfg in cfgs:
             base = 2 if name.startswith("glu") else 0
             lib.ggml_backend_mi355x_set_tune(base, cfg[0] if cfg else 0)
