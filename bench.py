@@ -10,10 +10,14 @@ single-token decodes of random tokens, each followed by a device synchronise and
 logits copy-back. value = generated tokens / wall time. pp512 (one 512-token prefill,
 test_prompt :1962) is reported beside it.
 
-Multi-GPU (torchrun, one process per GPU): layer split — rank r owns a
-contiguous block of layers of its own replica-sized slice; see DESIGN.md. With
---gpus N > 1 every rank runs its own tg128 stream and value is the job aggregate
-("replicas" — decode of one sequence does not speed up with layer split).
+Multi-GPU (torchrun, one process per GPU, --mode pipeline, the default for N > 1): the
+layer split of SURVEY §8e. Rank r owns layers [r*L/N, (r+1)*L/N) of ONE model; the
+hidden state of each token goes to rank r+1 by RCCL point-to-point send/recv over xGMI.
+N sequences are decoded at once (one per pipeline slot), so every GPU is busy and the
+per-GPU work (128 tokens x L layers) is the same at every N ("weak"); value = all
+sequences' generated tokens / max wall time over ranks. --mode replicas runs a whole
+model per GPU instead. --model picks the BASELINE.json config (llama3_8b, llama3_70b,
+mixtral_8x7b, tinyllama).
 """
 import argparse
 import ctypes
@@ -41,7 +45,7 @@ def dist_setup(n_gpus):
         import torch
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("MX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         tdist.init_process_group(backend=backend)
@@ -53,7 +57,7 @@ def barrier(dist, local):
     if dist is None:
         return
     import torch
-    if torch.cuda.is_available():
+    if dist.get_backend() == "nccl":
         torch.cuda.synchronize(local)
     dist.barrier()
 
@@ -92,10 +96,11 @@ def roofline_glu(pkg, be, model, iters=256):
     launch streams from HBM, not the 256 MiB MALL). Algorithmic bytes per launch = both
     Q4_K weight matrices + the f32 activation."""
     lib = pkg._lib.load()
-    n_layer = model.hp.n_layer
+    l0, l1 = model.stage
+    n_layer = l1 - l0
     P = ctypes.c_void_p
-    wg = (P * n_layer)(*[model.layer_tensor(i, "ffn_gate") for i in range(n_layer)])
-    wu = (P * n_layer)(*[model.layer_tensor(i, "ffn_up") for i in range(n_layer)])
+    wg = (P * n_layer)(*[model.layer_tensor(i, "ffn_gate") for i in range(l0, l1)])
+    wu = (P * n_layer)(*[model.layer_tensor(i, "ffn_up") for i in range(l0, l1)])
     t0 = pkg.Tensor(None, wg[0])
     K, M = t0.ne[0], t0.ne[1]
     ctx = pkg.Context()
@@ -107,7 +112,7 @@ def roofline_glu(pkg, be, model, iters=256):
     bytes_per_launch = 2 * t0.nbytes() + K * 4
     ctx.free()
     achieved = bytes_per_launch / (us * 1e-6) / 1e9
-    return {"bound": "hbm", "kernel": f"k_gemv2 SwiGLU (ffn gate+up, Q4_K {K}->{M} x2, cycled over {n_layer} layers)",
+    return {"bound": "hbm", "kernel": f"k_gemv2 SwiGLU (ffn gate+up, {K}->{M} x2, cycled over {n_layer} layers)",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(us, 2)}
@@ -137,6 +142,100 @@ def cpu_baseline(args):
         return {"value": None, "unit": "tok/s", "cores": threads, "kind": "reference", "sample": f"failed: {e}"}
 
 
+MODELS = {  # BASELINE.json configs -> (shape name in the package, default recipe, label)
+    "llama3_8b": ("LLAMA3_8B", "q4_k_m", "Llama-3-8B"),
+    "llama3_70b": ("LLAMA3_70B", "q4_k_m", "Llama-3-70B"),
+    "mixtral_8x7b": ("MIXTRAL_8X7B", "q5_k_m", "Mixtral-8x7B"),
+    "tinyllama": ("TINYLLAMA_1B", "q4_0", "TinyLlama-1.1B"),
+}
+
+
+class PipelineStage:
+    """One rank of the layer split: layers [l0, l1) of the model, the hidden
+    state handed to the next rank by RCCL point-to-point send/recv over xGMI. S sequences
+    are kept in flight so that every stage works on a different sequence at a time
+    (llama-bench tg feeds random tokens, so no token travels backwards)."""
+
+    def __init__(self, pkg, dist, rank, world, local, shape, recipe, fa, n_ctx, n_seq, seed=1234):
+        import torch
+        self.dist, self.rank, self.world = dist, rank, world
+        L = shape["n_layer"]
+        self.l0, self.l1 = rank * L // world, (rank + 1) * L // world
+        self.be = pkg.Backend(local % max(pkg.device_count(), 1))
+        self.model = pkg.Model.random_stage(self.be, shape, (self.l0, self.l1), recipe, seed=seed)
+        self.sessions = [pkg.Session(self.model, n_ctx=n_ctx, n_ubatch=512, flash_attn=fa) for _ in range(n_seq)]
+        self.n_embd = shape["n_embd"]
+        self.torch = torch
+        # MX_PIPE_HOST=1: hand-off through pinned host buffers (gloo; lets several ranks
+        # share one GPU for testing). Default: device buffers, RCCL over xGMI.
+        self.host = os.environ.get("MX_PIPE_HOST") == "1"
+        self.dev = torch.device("cpu") if self.host else torch.device("cuda", local)
+        mk = (lambda: torch.empty((512, self.n_embd), dtype=torch.float32).pin_memory()) if self.host else \
+             (lambda: torch.empty((512, self.n_embd), dtype=torch.float32, device=self.dev))
+        self.hin = mk()
+        self.hout = [mk(), mk()]
+        self.pending = [None, None]
+        self.flip = 0
+
+    @property
+    def first(self):
+        return self.rank == 0
+
+    @property
+    def last(self):
+        return self.rank == self.world - 1
+
+    def item(self, si, tokens):
+        """Run one ubatch of sequence si through this stage (recv -> compute -> send)."""
+        n = len(tokens)
+        hin = 0
+        if not self.first:
+            self.dist.recv(self.hin[:n], src=self.rank - 1)
+            if not self.host:
+                self.torch.cuda.current_stream(self.dev).synchronize()
+            hin = self.hin.data_ptr()
+        s = self.sessions[si]
+        if self.last:
+            s.decode_stage(tokens=tokens if self.first else None, h_in=hin, n_tokens=n, want_logits=True)
+            return
+        b = self.flip
+        self.flip ^= 1
+        if self.pending[b] is not None:
+            self.pending[b].wait()
+        s.decode_stage(tokens=tokens if self.first else None, h_in=hin, n_tokens=n, h_out=self.hout[b].data_ptr())
+        self.pending[b] = self.dist.isend(self.hout[b][:n], dst=self.rank + 1)
+
+    def drain(self):
+        for w in self.pending:
+            if w is not None:
+                w.wait()
+        self.pending = [None, None]
+        if not self.host:
+            self.torch.cuda.synchronize(self.dev)
+
+    def tg(self, rng, n_vocab, n_gen):
+        for s in self.sessions:
+            s.reset()
+        toks = rng.integers(0, n_vocab, size=(len(self.sessions), n_gen), dtype=np.int32)
+        for k in range(n_gen):
+            for si in range(len(self.sessions)):
+                self.item(si, toks[si, k:k + 1])
+        self.drain()
+
+    def pp(self, rng, n_vocab, n_tok):
+        s = self.sessions[0]
+        s.reset()
+        toks = rng.integers(0, n_vocab, size=n_tok, dtype=np.int32)
+        for i in range(0, n_tok, 512):
+            self.item(0, toks[i:i + 512])
+        self.drain()
+
+    def free(self):
+        for s in self.sessions:
+            s.free()
+        self.model.free()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,7 +243,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tg", type=int, default=128)
     ap.add_argument("--pp", type=int, default=512)
-    ap.add_argument("--recipe", default="q4_k_m")
+    ap.add_argument("--model", default="llama3_8b", choices=sorted(MODELS))
+    ap.add_argument("--recipe", default=None)
+    ap.add_argument("--mode", default="auto", choices=["auto", "single", "pipeline", "replicas"],
+                    help="N>1: pipeline = layer split over the ranks (default), replicas = one model per GPU")
+    ap.add_argument("--seqs", type=int, default=0, help="pipeline: sequences in flight (default = number of GPUs)")
     ap.add_argument("--no-fa", action="store_true", help="llama-bench -fa 0 graph (KQ mul_mat + softmax)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-pp", type=int, default=32)
@@ -153,48 +256,79 @@ def main():
     args = ap.parse_args()
 
     world, rank, local, dist = dist_setup(args.gpus)
+    mode = args.mode if args.mode != "auto" else ("pipeline" if world > 1 else "single")
     from mi355x_pkg import load_package
     pkg = load_package()
-    be = pkg.Backend(local if world > 1 else 0)
-    model = pkg.Model.random(be, pkg.LLAMA3_8B, args.recipe, seed=1234 + rank)
-    n_vocab = model.hp.n_vocab
-    sess = pkg.Session(model, n_ctx=max(args.pp, args.tg) + 256, n_ubatch=512, flash_attn=not args.no_fa)
+    shape_name, def_recipe, label = MODELS[args.model]
+    shape = getattr(pkg, shape_name)
+    recipe = args.recipe or def_recipe
+    n_ctx = max(args.pp, args.tg) + 256
     rng = np.random.default_rng(42 + rank)
+    n_vocab = shape["n_vocab"]
+
+    if mode == "pipeline":
+        n_seq = args.seqs or world
+        stage = PipelineStage(pkg, dist, rank, world, local, shape, recipe, not args.no_fa, n_ctx, n_seq)
+        be, model = stage.be, stage.model
+        run_tg = lambda: stage.tg(rng, n_vocab, args.tg)   # noqa: E731
+        tokens_per_step = n_seq * args.tg                  # whole job (all ranks together)
+    else:
+        be = pkg.Backend(local if world > 1 else 0)
+        model = pkg.Model.random(be, shape, recipe, seed=1234 + rank)
+        sess = pkg.Session(model, n_ctx=n_ctx, n_ubatch=512, flash_attn=not args.no_fa)
+        run_tg = lambda: tg_step(sess, rng, n_vocab, args.tg)   # noqa: E731
+        tokens_per_step = args.tg                                # per rank; summed below
 
     for _ in range(args.warmup):
-        tg_step(sess, rng, n_vocab, args.tg)
+        run_tg()
     barrier(dist, local)
     be.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        tg_step(sess, rng, n_vocab, args.tg)
+        run_tg()
     be.synchronize()
     barrier(dist, local)
     dt = max_over_ranks(dist, time.perf_counter() - t0)
-    tokens = sum_over_ranks(dist, args.steps * args.tg)
+    if mode == "pipeline":
+        tokens = args.steps * tokens_per_step
+    else:
+        tokens = sum_over_ranks(dist, args.steps * tokens_per_step)
     tg_value = tokens / dt
 
     # pp512 beside it (not the headline value)
     pp_tok_s = None
     if args.pp > 0:
-        toks = rng.integers(0, n_vocab, size=args.pp, dtype=np.int32)
-        sess.reset(); sess.decode(toks)  # warm the prefill graph
-        reps = 3
-        be.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            sess.reset()
-            sess.decode(toks)
-        be.synchronize()
-        pp_tok_s = reps * args.pp / (time.perf_counter() - t1)
+        if mode == "pipeline":
+            stage.pp(rng, n_vocab, args.pp)   # warm
+            barrier(dist, local)
+            t1 = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                stage.pp(rng, n_vocab, args.pp)
+            barrier(dist, local)
+            pp_tok_s = reps * args.pp / max_over_ranks(dist, time.perf_counter() - t1)
+        else:
+            toks = rng.integers(0, n_vocab, size=args.pp, dtype=np.int32)
+            sess.reset(); sess.decode(toks)  # warm the prefill graph
+            reps = 3
+            be.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                sess.reset()
+                sess.decode(toks)
+            be.synchronize()
+            pp_tok_s = reps * args.pp / (time.perf_counter() - t1)
 
     stats = be.stats()
-    decode_bytes = model.decode_bytes()
-    roof = None if args.skip_roofline else roofline_glu(pkg, be, model)
-    cpu = cpu_baseline(args) if (rank == 0 and world == 1) else None
+    # weights one decoded token reads (all stages together)
+    decode_bytes = int(sum_over_ranks(dist, model.decode_bytes())) if mode == "pipeline" else model.decode_bytes()
+    roof = None if (args.skip_roofline or shape.get("n_expert")) else roofline_glu(pkg, be, model)
+    cpu = cpu_baseline(args) if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
 
     if rank == 0:
-        per_gpu_tg = tg_value / world
+        per_gpu_bytes_s = decode_bytes * tg_value / world
+        par = {"single": "single", "replicas": f"replicas x{world}",
+               "pipeline": f"layer split x{world} (RCCL p2p hidden-state hand-off), {tokens_per_step // max(args.tg, 1)} sequences in flight"}[mode]
         out = {
             "metric": METRIC,
             "value": round(tg_value, 2),
@@ -206,22 +340,25 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "q4_K/q6_K weights, int8 x int8 dot (sdot4) + f32 accumulate",
-            "data": "synthetic (random Q4_K_M weights generated on device, random tokens)",
-            "config": {"workload": "Llama-3-8B Q4_K_M tg128 decode (llama-bench test_gen), 1 sequence per GPU",
-                       "model_shape": "llama3-8b", "recipe": args.recipe, "tg": args.tg, "pp": args.pp,
-                       "flash_attn": not args.no_fa, "parallelism": f"replicas x{world}" if world > 1 else "single"},
+            "dtype": "quantised weights (%s), int8 x int8 dot (v_dot4) + f32 accumulate" % recipe,
+            "data": "synthetic (random %s weights generated on device, random tokens)" % recipe,
+            "config": {"workload": f"{label} {recipe.upper()} tg{args.tg} decode (llama-bench test_gen)",
+                       "model_shape": args.model, "recipe": recipe, "tg": args.tg, "pp": args.pp,
+                       "flash_attn": not args.no_fa, "parallelism": par},
             "pp512_tok_s": round(pp_tok_s, 1) if pp_tok_s else None,
             "decode_bytes_per_token": decode_bytes,
-            "decode_roofline": {"achieved_GBs": round(decode_bytes * per_gpu_tg / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
-                                "frac": round(decode_bytes * per_gpu_tg / 1e9 / HBM_PEAK_GBS, 4)},
+            "decode_roofline": {"achieved_GBs": round(per_gpu_bytes_s / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
+                                "frac": round(per_gpu_bytes_s / 1e9 / HBM_PEAK_GBS, 4)},
             "roofline": roof,
             "cpu_baseline": cpu,
             "executor": stats,
         }
         print(json.dumps(out), flush=True)
-    sess.free()
-    model.free()
+    if mode == "pipeline":
+        stage.free()
+    else:
+        sess.free()
+        model.free()
     if dist is not None:
         dist.destroy_process_group()
 

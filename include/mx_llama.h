@@ -27,6 +27,13 @@ typedef struct mxr_context mxr_context;
  * recipe: "q4_k_m" (Q4_K + Q6_K for attn_v/ffn_down on use_more_bits layers and
  * output, src/llama-quant.cpp:185-187,302-303,358-365), "q4_0", "q5_k_m", "q8_0", "f16". */
 mxr_model * mxr_model_random(ggml_backend_t backend, const mxr_hparams * hp, const char * recipe, uint64_t seed);
+/* Pipeline stage of the same model: layers [layer_begin, layer_end) only (token_embd with
+ * the first stage, output_norm/output with the last). Weights are seeded per (layer,
+ * tensor), so the stages of a split hold exactly the layers of mxr_model_random's model
+ * (the layer split of src/llama-model.cpp:2599-2609 across processes/GPUs). */
+mxr_model * mxr_model_random_stage(ggml_backend_t backend, const mxr_hparams * hp, const char * recipe, uint64_t seed,
+                                   int32_t layer_begin, int32_t layer_end);
+void        mxr_model_stage(const mxr_model * m, int32_t * layer_begin, int32_t * layer_end);
 /* Weights from a GGUF file (llama architecture) */
 mxr_model * mxr_model_load_gguf(ggml_backend_t backend, const char * path);
 void        mxr_model_free(mxr_model * m);
@@ -49,6 +56,12 @@ int32_t       mxr_context_pos(const mxr_context * c);
  * Returns 0 on success. Blocks until the device finished (llama_decode + synchronize). */
 int32_t mxr_decode(mxr_context * c, const int32_t * tokens, int32_t n_tokens, float * logits);
 /* all-token logits variant (n_tokens x n_vocab), for parity tests */
+/* One ubatch through this stage: the first stage reads `tokens`, later ones the previous
+ * stage's hidden state `h_in` (f32 [n_tokens][n_embd], device or host pointer); a
+ * non-last stage writes its hidden state to `h_out`, the last one the last token's
+ * logits. Synchronous. */
+int32_t mxr_decode_stage(mxr_context * c, const int32_t * tokens, const void * h_in, int32_t n_tokens, void * h_out,
+                         float * logits);
 int32_t mxr_decode_all_logits(mxr_context * c, const int32_t * tokens, int32_t n_tokens, float * logits);
 
 #ifdef __cplusplus

@@ -9,3 +9,8 @@ from .ggml import Backend, Context, Tensor, row_bytes  # noqa: F401
 from .llama import Model, Session, LLAMA3_8B, LLAMA3_70B, TINYLLAMA_1B, MIXTRAL_8X7B  # noqa: F401
 
 LIB_PATH = _lib.LIB_PATH
+
+
+def device_count():
+    """MI355X devices the backend sees (initialises HIP)."""
+    return int(_lib.load().ggml_backend_mi355x_get_device_count())

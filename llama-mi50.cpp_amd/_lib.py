@@ -115,6 +115,8 @@ def load():
     _sig(lib, "mxg_backend_free", None, P)
     # llama runner
     _sig(lib, "mxr_model_random", P, P, ctypes.POINTER(MxrHparams), ctypes.c_char_p, ctypes.c_uint64)
+    _sig(lib, "mxr_model_random_stage", P, P, ctypes.POINTER(MxrHparams), ctypes.c_char_p, ctypes.c_uint64, I, I)
+    _sig(lib, "mxr_model_stage", None, P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32))
     _sig(lib, "mxr_model_load_gguf", P, P, ctypes.c_char_p)
     _sig(lib, "mxr_model_free", None, P)
     _sig(lib, "mxr_model_hparams", None, P, ctypes.POINTER(MxrHparams))
@@ -127,6 +129,7 @@ def load():
     _sig(lib, "mxr_context_pos", ctypes.c_int32, P)
     _sig(lib, "mxr_decode", ctypes.c_int32, P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, ctypes.POINTER(ctypes.c_float))
     _sig(lib, "mxr_decode_all_logits", ctypes.c_int32, P, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, ctypes.POINTER(ctypes.c_float))
+    _sig(lib, "mxr_decode_stage", ctypes.c_int32, P, ctypes.POINTER(ctypes.c_int32), P, ctypes.c_int32, P, ctypes.POINTER(ctypes.c_float))
     _lib = lib
     return lib
 

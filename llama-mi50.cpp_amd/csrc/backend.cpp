@@ -161,6 +161,7 @@ static void be_free(ggml_backend_t b) {
     if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
     if (s->scratch.base) hipFree(s->scratch.base);
     if (s->act.base) hipFree(s->act.base);
+    if (s->f16.base) hipFree(s->f16.base);
     hipStreamDestroy(s->stream);
     delete s;  // the ggml_backend struct lives inside Stream
 }

@@ -83,6 +83,10 @@ struct Stream {
     Scratch scratch;
     Scratch act;                       // ring of quantised activations (act_cache)
     ActCacheEntry act_cache[4];
+    // f16 copy of the last prefill GEMM activation (q/k/v and gate/up share one)
+    Scratch f16;
+    const void * f16_src = nullptr;
+    int64_t f16_key[4] = {0, 0, 0, 0};       // K, ncols, nb1, kp
     int act_next = 0;
     size_t act_slot = 0;               // bytes per ring slot
     GraphCache gcache;
@@ -152,6 +156,7 @@ ActQ * act_cache_alloc(Stream * s, const ggml_tensor * t);   // reserve a slot f
 ActQ * act_cache_alloc_raw(Stream * s, const void * data, int64_t ne0, int64_t ncols, size_t bytes);
 const ActQ * act_cache_find(Stream * s, const ggml_tensor * t);   // q8 form of t, if cached
 bool mmvq_small_batch_ok(const ggml_tensor * mm);             // MUL_MAT runs on the GEMV path
+size_t mmq_act_bytes(const ggml_tensor * mm);                 // f16 activation bytes of a prefill GEMM (0: none)
 // consumer count of every tensor in the graph being executed
 using UseCount = std::unordered_map<const ggml_tensor *, int>;
 // decode Q/K/V projections + RoPE + KV-cache stores in one launch; returns nodes consumed

@@ -288,9 +288,10 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     s->n_graph_compute++;
     if (s->abort_cb && s->abort_cb(s->abort_data)) { *status = GGML_STATUS_ABORTED; return; }
 
-    size_t need = 0, slot = 0;
+    size_t need = 0, slot = 0, f16need = 0;
     for (int i = 0; i < g->n_nodes; ++i) {
         need = std::max(need, scratch_bytes(g->nodes[i]));
+        if (g->nodes[i]->op == GGML_OP_MUL_MAT) f16need = std::max(f16need, mmq_act_bytes(g->nodes[i]));
         if (g->nodes[i]->op == GGML_OP_MUL_MAT && mmvq_small_batch_ok(g->nodes[i])) slot = std::max(slot, act_slot_bytes(g->nodes[i]->src[1]));
         if (g->nodes[i]->op == GGML_OP_MUL && mx_nrows(g->nodes[i]) <= 8) slot = std::max(slot, act_slot_bytes(g->nodes[i]));
     }
@@ -300,6 +301,14 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         s->act_slot = (slot + 4095) & ~(size_t) 4095;
         HIP_CHECK(hipMalloc((void **) &s->act.base, 4 * s->act_slot));
         s->act.cap = 4 * s->act_slot;
+        s->gcache.key.clear();
+    }
+    if (f16need > s->f16.cap) {
+        HIP_CHECK(hipStreamSynchronize(s->stream));
+        if (s->f16.base) HIP_CHECK(hipFree(s->f16.base));
+        HIP_CHECK(hipMalloc((void **) &s->f16.base, f16need));
+        s->f16.cap = f16need;
+        s->f16_src = nullptr;
         s->gcache.key.clear();
     }
     if (need > s->scratch.cap) {

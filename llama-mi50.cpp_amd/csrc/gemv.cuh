@@ -36,7 +36,12 @@ struct LdsAct {
 // activation source of a GEMV, compile-time (each mode keeps only its own registers).
 // *_LDS modes stage the f32 x (and norm weight) into LDS by LDS-DMA before the weight
 // loads are issued and quantise from LDS afterwards: no registers, no wait on x.
-enum { XS_F32 = 0, XS_NORM = 1, XS_Q8 = 2, XS_F32_LDS = 3, XS_NORM_LDS = 4 };
+// *_H2 modes hold two 16-value halves per thread (K up to 32 * threads); the plain modes
+// one (K <= 16 * threads, e.g. n_embd 4096 on 256 threads) and so half the registers,
+// which is occupancy on the large grids.
+enum { XS_F32 = 0, XS_NORM = 1, XS_Q8 = 2, XS_F32_LDS = 3, XS_NORM_LDS = 4, XS_F32_H2 = 5, XS_NORM_H2 = 6 };
+__host__ __device__ constexpr bool xs_norm(int m) { return m == XS_NORM || m == XS_NORM_H2; }
+__host__ __device__ constexpr bool xs_f32reg(int m) { return m == XS_F32 || m == XS_F32_H2; }
 
 __host__ __device__ inline size_t gemv_lds_base(int64_t K) { return ((size_t) K + (size_t) (K / 32) * 8 + 64 + 15) & ~(size_t) 15; }
 __host__ __device__ inline size_t gemv_lds_bytes(int64_t K, int mode = XS_Q8) {
@@ -47,11 +52,12 @@ __host__ __device__ inline float * gemv_lds_red(char * smem, int64_t K) { return
 // one-block-per-CU grids of the layer GEMVs (the register path's x loads ride along
 // with the weights) and wins on the huge lm_head grid, where the register path's VGPRs
 // cost occupancy (tools/opbench.py --trace, profiles/r01).
-inline int gemv_mode(const XStage & xs, int64_t K, int64_t nrows = 0) {
+inline int gemv_mode(const XStage & xs, int64_t K, int64_t nrows = 0, int nt = 256) {
     if (xs.q8) return XS_Q8;
     const bool big = nrows >= 32768;
-    if (xs.norm) return big && gemv_lds_bytes(K, XS_NORM_LDS) <= 65536 ? XS_NORM_LDS : XS_NORM;
-    return big && gemv_lds_bytes(K, XS_F32_LDS) <= 65536 ? XS_F32_LDS : XS_F32;
+    const bool h2 = K > 16 * nt;
+    if (xs.norm) return big && gemv_lds_bytes(K, XS_NORM_LDS) <= 65536 ? XS_NORM_LDS : (h2 ? XS_NORM_H2 : XS_NORM);
+    return big && gemv_lds_bytes(K, XS_F32_LDS) <= 65536 ? XS_F32_LDS : (h2 ? XS_F32_H2 : XS_F32);
 }
 
 __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
@@ -98,13 +104,11 @@ __device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) 
 // Split in two because vector-memory loads retire in issue order: issue() starts the
 // activation loads BEFORE the weight stream is issued, finish() (after the weight loads
 // are in flight) waits only for them, quantises into LDS and ends with a barrier.
-__host__ __device__ constexpr int stage_hpt(int NT) { return NT >= 512 ? 1 : 2; }   // f32 half-groups held per thread
-
 template <int NT, int MODE>
 struct StageRegs {
-    static constexpr int HPT = stage_hpt(NT);
-    float v[MODE == XS_F32 || MODE == XS_NORM ? HPT : 1][16];
-    float w[MODE == XS_NORM ? HPT : 1][16];
+    static constexpr int HPT = (MODE == XS_F32_H2 || MODE == XS_NORM_H2) ? 2 : 1;   // f32 halves per thread
+    float v[HPT][16];
+    float w[xs_norm(MODE) ? HPT : 1][16];
 };
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
@@ -151,7 +155,7 @@ __device__ __forceinline__ void stage_issue(const XStage & xs, int K, const LdsA
         for (int h = 0; h < StageRegs<NT, MODE>::HPT; ++h) {
             const int hg = min(t + NT * h, nhg - 1);
             load_half(hg, r.v[h], xs.x);
-            if constexpr (MODE == XS_NORM) load_half(hg, r.w[h], xs.nw);
+            if constexpr (xs_norm(MODE)) load_half(hg, r.w[h], xs.nw);
         }
     }
 }
@@ -191,7 +195,7 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
             }
             q8_half(v2, hg, a);
         }
-    } else if constexpr (MODE == XS_NORM) {
+    } else if constexpr (xs_norm(MODE)) {
         // K <= 16 * HPT * NT (GEMV2_MAX_NORM_K checks it for the 256-thread kernels)
         float ss = 0.f;
 #pragma unroll
@@ -407,6 +411,9 @@ __device__ __forceinline__ void w2_dot_batch(const W2<QT> (&r)[NM][UPL], int u0,
 #pragma unroll
             for (int m = 0; m < NM; ++m) acc[m] += w2_dot<QT>(r[m][j], u0 + j * lpr, a);
         }
+        // keep the scheduler from hoisting every unit's LDS activation reads at once
+        // (that costs ~16 VGPRs per unit, i.e. occupancy)
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 

@@ -123,6 +123,7 @@ hipStream_t stream_of_backend(ggml_backend_t b) { return mx::stream_of(b)->strea
 struct mxr_model {
     ggml_backend_t be = nullptr;
     mxr_hparams hp{};
+    int l0 = 0, l1 = 0;               // pipeline stage: layers [l0, l1) of hp.n_layer
     mxg_context * wctx = nullptr;
     ggml_tensor * tok_embd = nullptr, * out_norm = nullptr, * output = nullptr;
     std::vector<Layer> layers;
@@ -134,6 +135,7 @@ struct GraphInst {
     ggml_cgraph * g = nullptr;
     ggml_tensor * tokens = nullptr, * pos = nullptr, * kidx = nullptr, * vidx = nullptr, * mask = nullptr, * out_ids = nullptr;
     ggml_tensor * logits = nullptr;
+    ggml_tensor * hin = nullptr, * hout = nullptr;   // stage hand-off (pipeline layer split)
     char * in_base = nullptr; size_t in_bytes = 0;
     int n_tokens = 0, n_kv = 0, n_out = 0;
     uint64_t last_use = 0;
@@ -169,7 +171,7 @@ static void create_weights(mxr_model * m, const char * recipe) {
     const int hd = h.n_embd / h.n_head;
     const int nkv = hd * h.n_head_kv;
     m->tok_embd = nullptr;
-    for (int i = 0; i < h.n_layer; ++i) {
+    for (int i = m->l0; i < m->l1; ++i) {
         Layer L;
         char nm[96];
         const bool more = use_more_bits(i, h.n_layer);
@@ -197,38 +199,57 @@ static void create_weights(mxr_model * m, const char * recipe) {
         }
         m->layers.push_back(L);
     }
-    m->tok_embd = wt(m, "token_embd.weight", temb, h.n_embd, h.n_vocab);
-    m->out_norm = wt(m, "output_norm.weight", GGML_TYPE_F32, h.n_embd, 1);
-    m->output = wt(m, "output.weight", tout, h.n_embd, h.n_vocab);
+    if (m->l0 == 0) m->tok_embd = wt(m, "token_embd.weight", temb, h.n_embd, h.n_vocab);
+    if (m->l1 == h.n_layer) {
+        m->out_norm = wt(m, "output_norm.weight", GGML_TYPE_F32, h.n_embd, 1);
+        m->output = wt(m, "output.weight", tout, h.n_embd, h.n_vocab);
+    }
 }
 
 extern "C" {
 
-mxr_model * mxr_model_random(ggml_backend_t be, const mxr_hparams * hp, const char * recipe, uint64_t seed) {
+mxr_model * mxr_model_random_stage(ggml_backend_t be, const mxr_hparams * hp, const char * recipe, uint64_t seed,
+                                   int32_t layer_begin, int32_t layer_end) {
+    if (layer_begin < 0 || layer_end > hp->n_layer || layer_begin >= layer_end) return nullptr;
     auto * m = new mxr_model();
     m->be = be;
     m->hp = *hp;
+    m->l0 = layer_begin;
+    m->l1 = layer_end;
     if (m->hp.n_ctx_train <= 0) m->hp.n_ctx_train = 8192;
     m->wctx = mxg_init();
     create_weights(m, recipe);
     ggml_backend_buffer_type_t buft = be->device->iface.get_buffer_type(be->device);
     if (mxg_alloc(m->wctx, buft) != 0) { mxg_free(m->wctx); delete m; return nullptr; }
     hipStream_t st = stream_of_backend(be);
-    uint64_t s = seed * 1000003ULL;
-    auto fill = [&](ggml_tensor * t, bool norm) {
+    // one seed per (layer, tensor): a stage holds exactly the weights of the same
+    // layers of the whole model
+    const uint64_t base = seed * 1000003ULL;
+    auto fill = [&](ggml_tensor * t, bool norm, uint64_t slot) {
         if (!t) return;
         if (norm) mx::fill_const_f32(t, 1.0f, st);
-        else mx::fill_random_tensor(t, ++s, st);
+        else mx::fill_random_tensor(t, base + slot, st);
     };
-    fill(m->tok_embd, false); fill(m->out_norm, true); fill(m->output, false);
-    for (auto & L : m->layers) {
-        fill(L.attn_norm, true); fill(L.ffn_norm, true);
-        fill(L.wq, false); fill(L.wk, false); fill(L.wv, false); fill(L.wo, false);
-        fill(L.gate, false); fill(L.up, false); fill(L.down, false);
-        fill(L.gate_inp, false); fill(L.gate_exps, false); fill(L.up_exps, false); fill(L.down_exps, false);
+    fill(m->tok_embd, false, 1); fill(m->out_norm, true, 0); fill(m->output, false, 2);
+    for (size_t k = 0; k < m->layers.size(); ++k) {
+        const Layer & L = m->layers[k];
+        const uint64_t b = 64 + 16 * (uint64_t) (m->l0 + k);
+        fill(L.attn_norm, true, 0); fill(L.ffn_norm, true, 0);
+        fill(L.wq, false, b + 0); fill(L.wk, false, b + 1); fill(L.wv, false, b + 2); fill(L.wo, false, b + 3);
+        fill(L.gate, false, b + 4); fill(L.up, false, b + 5); fill(L.down, false, b + 6);
+        fill(L.gate_inp, false, b + 7); fill(L.gate_exps, false, b + 8); fill(L.up_exps, false, b + 9); fill(L.down_exps, false, b + 10);
     }
     HIP_CHECK(hipStreamSynchronize(st));
     return m;
+}
+
+mxr_model * mxr_model_random(ggml_backend_t be, const mxr_hparams * hp, const char * recipe, uint64_t seed) {
+    return mxr_model_random_stage(be, hp, recipe, seed, 0, hp->n_layer);
+}
+
+void mxr_model_stage(const mxr_model * m, int32_t * layer_begin, int32_t * layer_end) {
+    *layer_begin = m->l0;
+    *layer_end = m->l1;
 }
 
 mxr_model * mxr_model_load_gguf(ggml_backend_t be, const char * path) {
@@ -249,6 +270,8 @@ mxr_model * mxr_model_load_gguf(ggml_backend_t be, const char * path) {
     h.norm_eps = (float) kv("attention.layer_norm_rms_epsilon", 1e-5);
     h.n_expert = (int) kv("expert_count", 0);
     h.n_expert_used = (int) kv("expert_used_count", 0);
+    m->l0 = 0;
+    m->l1 = h.n_layer;
     m->wctx = mxg_init();
     std::map<std::string, ggml_tensor *> byname;
     for (auto & t : g.tensors) {
@@ -314,8 +337,8 @@ static void add_bytes(const ggml_tensor * t, int64_t * acc, int64_t * by_type) {
 }
 
 ggml_tensor * mxr_model_layer_tensor(const mxr_model * m, int32_t il, const char * which) {
-    if (!m || il < 0 || il >= (int32_t) m->layers.size() || !which) return nullptr;
-    const Layer & L = m->layers[il];
+    if (!m || il < m->l0 || il >= m->l1 || !which) return nullptr;
+    const Layer & L = m->layers[il - m->l0];
     const std::string w = which;
     if (w == "attn_norm") return L.attn_norm;
     if (w == "attn_q") return L.wq;
@@ -332,8 +355,7 @@ ggml_tensor * mxr_model_layer_tensor(const mxr_model * m, int32_t il, const char
 int64_t mxr_model_decode_bytes(const mxr_model * m) {
     int64_t acc = 0;
     add_bytes(m->out_norm, &acc, nullptr);
-    if (m->output != m->tok_embd) add_bytes(m->output, &acc, nullptr);
-    else acc += (int64_t) mx_nbytes(m->output);
+    if (m->output) acc += (int64_t) mx_nbytes(m->output);   // (tied embeddings: read as the lm_head)
     for (auto & L : m->layers) {
         for (auto t : {L.attn_norm, L.wq, L.wk, L.wv, L.wo, L.ffn_norm, L.gate, L.up, L.down, L.gate_inp}) add_bytes(t, &acc, nullptr);
         if (L.gate_exps) {  // MoE: only n_expert_used of n_expert expert matrices are read per token
@@ -366,7 +388,7 @@ mxr_context * mxr_context_new(mxr_model * m, int32_t n_ctx, int32_t n_ubatch, in
     c->kvctx = mxg_init();
     const mxr_hparams & h = m->hp;
     const int nkv = h.n_embd / h.n_head * h.n_head_kv;
-    for (int i = 0; i < h.n_layer; ++i) {
+    for (int i = m->l0; i < m->l1; ++i) {
         char nm[64];
         snprintf(nm, sizeof nm, "cache_k_l%d", i);
         ggml_tensor * k = mxg_new_tensor_4d(c->kvctx, GGML_TYPE_F16, nkv, c->n_ctx, 1, 1);
@@ -421,15 +443,21 @@ static GraphInst * build_graph(mxr_context * c, int n_tokens, int n_kv, int n_ou
         gi->out_ids = mxg_new_tensor_4d(ictx, GGML_TYPE_I32, n_out, 1, 1, 1); mxg_set_input(gi->out_ids); mxg_set_name(gi->out_ids, "inp_out_ids");
     }
 
-    ggml_tensor * inpL = mxg_get_rows(ctx, m->tok_embd, gi->tokens);
+    const bool first = m->l0 == 0, last = m->l1 == h.n_layer;
+    if (!first) {   // pipeline stage > 0: the previous stage's hidden state comes in
+        gi->hin = mxg_new_tensor_4d(ictx, GGML_TYPE_F32, h.n_embd, n_tokens, 1, 1);
+        mxg_set_input(gi->hin); mxg_set_name(gi->hin, "inp_embd");
+    }
+    ggml_tensor * inpL = first ? mxg_get_rows(ctx, m->tok_embd, gi->tokens) : gi->hin;
     ggml_tensor * kq_mask = c->fa ? mxg_cast(ctx, gi->mask, GGML_TYPE_F16) : gi->mask;
     const float kq_scale = 1.0f / sqrtf((float) hd);
     std::vector<ggml_tensor *> order;  // explicit expansion order (ggml_build_forward_expand calls)
     ggml_cgraph * g = nullptr;
     auto expand = [&](ggml_tensor * t) { if (!g) g = mxg_build(ctx, t); else mxg_expand(ctx, g, t); };
 
-    for (int il = 0; il < h.n_layer; ++il) {
+    for (int il = 0; il < (int) m->layers.size(); ++il) {
         const Layer & L = m->layers[il];
+        const int il_global = m->l0 + il;
         ggml_tensor * inpSA = inpL;
         ggml_tensor * cur = mxg_binary(ctx, GGML_OP_MUL, mxg_rms_norm(ctx, inpL, h.norm_eps), L.attn_norm);
         ggml_tensor * Q = mxg_mul_mat(ctx, L.wq, cur);
@@ -479,7 +507,7 @@ static GraphInst * build_graph(mxr_context * c, int n_tokens, int n_kv, int n_ou
         }
         expand(cur);
         cur = mxg_mul_mat(ctx, L.wo, cur);
-        if (il == h.n_layer - 1 && gi->out_ids) {
+        if (il_global == h.n_layer - 1 && gi->out_ids) {
             cur = mxg_get_rows(ctx, cur, gi->out_ids);
             inpSA = mxg_get_rows(ctx, inpSA, gi->out_ids);
         }
@@ -518,11 +546,17 @@ static GraphInst * build_graph(mxr_context * c, int n_tokens, int n_kv, int n_ou
         cur = mxg_binary(ctx, GGML_OP_ADD, cur, ffn_inp);
         inpL = cur;
     }
-    ggml_tensor * cur = mxg_binary(ctx, GGML_OP_MUL, mxg_rms_norm(ctx, inpL, h.norm_eps), m->out_norm);
-    cur = mxg_mul_mat(ctx, m->output, cur);
-    mxg_set_output(cur);
-    gi->logits = cur;
-    expand(cur);
+    if (last) {
+        ggml_tensor * cur = mxg_binary(ctx, GGML_OP_MUL, mxg_rms_norm(ctx, inpL, h.norm_eps), m->out_norm);
+        cur = mxg_mul_mat(ctx, m->output, cur);
+        mxg_set_output(cur);
+        gi->logits = cur;
+        expand(cur);
+    } else {        // hand the hidden state to the next stage
+        mxg_set_output(inpL);
+        gi->hout = inpL;
+        expand(inpL);
+    }
     gi->g = g;
     // no CPU fallback in this driver: every node must be supported by the device
     for (int i = 0; i < g->n_nodes; ++i) {
@@ -539,7 +573,7 @@ static GraphInst * build_graph(mxr_context * c, int n_tokens, int n_kv, int n_ou
     // inputs are contiguous in one buffer: remember base + extent
     gi->in_base = (char *) gi->tokens->data;
     char * end = gi->in_base;
-    for (ggml_tensor * t : {gi->tokens, gi->pos, gi->kidx, gi->vidx, gi->mask, gi->out_ids}) {
+    for (ggml_tensor * t : {gi->tokens, gi->pos, gi->kidx, gi->vidx, gi->mask, gi->out_ids}) {   // hin: device hand-off, not staged
         if (!t) continue;
         MX_ASSERT((char *) t->data >= gi->in_base);
         end = std::max(end, (char *) t->data + mx_nbytes(t));
@@ -566,7 +600,8 @@ static GraphInst * get_graph(mxr_context * c, int n_tokens, int n_kv, int n_out)
     return g;
 }
 
-static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_tokens, bool all_logits, float * out) {
+static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_tokens, bool all_logits, float * out,
+                             const void * h_in = nullptr, void * h_out = nullptr) {
     const mxr_hparams & h = c->m->hp;
     if (c->pos + n_tokens > c->n_ctx) return -1;
     const int used = c->pos + n_tokens;
@@ -583,7 +618,8 @@ static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_toke
     // the previous upload may still be in flight on the stream
     mxg_synchronize(c->m->be);
     auto at = [&](ggml_tensor * t) { return c->h_in + ((char *) t->data - g->in_base); };
-    memcpy(at(g->tokens), tokens, n_tokens * sizeof(int32_t));
+    if (tokens) memcpy(at(g->tokens), tokens, n_tokens * sizeof(int32_t));
+    else memset(at(g->tokens), 0, n_tokens * sizeof(int32_t));   // later pipeline stages: unused
     int32_t * pos = (int32_t *) at(g->pos);
     int64_t * kidx = (int64_t *) at(g->kidx);
     for (int i = 0; i < n_tokens; ++i) { pos[i] = c->pos + i; kidx[i] = c->pos + i; }
@@ -602,10 +638,16 @@ static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_toke
     if (g->out_ids) ((int32_t *) at(g->out_ids))[0] = n_tokens - 1;
     ggml_backend_t be = c->m->be;
     be->iface.set_tensor_async(be, g->tokens, c->h_in, 0, g->in_bytes);
+    hipStream_t st_be = stream_of_backend(be);
+    if (g->hin) {   // previous stage's hidden state (device or host pointer)
+        if (!h_in) return -4;
+        HIP_CHECK(hipMemcpyAsync(g->hin->data, h_in, mx_nbytes(g->hin), hipMemcpyDefault, st_be));
+    }
     ggml_status st = be->iface.graph_compute(be, g->g);
     if (st != GGML_STATUS_SUCCESS) return -3;
+    if (g->hout && h_out) HIP_CHECK(hipMemcpyAsync(h_out, g->hout->data, mx_nbytes(g->hout), hipMemcpyDefault, st_be));
     const size_t lbytes = (size_t) n_out * h.n_vocab * sizeof(float);
-    if (out) {
+    if (out && g->logits) {
         if (c->h_logits_cap < lbytes) {
             if (c->h_logits) HIP_CHECK(hipHostFree(c->h_logits));
             HIP_CHECK(hipHostMalloc((void **) &c->h_logits, lbytes, hipHostMallocDefault));
@@ -614,7 +656,7 @@ static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_toke
         be->iface.get_tensor_async(be, g->logits, c->h_logits, 0, lbytes);
     }
     mxg_synchronize(be);
-    if (out) memcpy(out, c->h_logits, lbytes);
+    if (out && g->logits) memcpy(out, c->h_logits, lbytes);
     c->pos += n_tokens;
     return 0;
 }
@@ -629,6 +671,12 @@ int32_t mxr_decode(mxr_context * c, const int32_t * tokens, int32_t n_tokens, fl
         if (r != 0) return r;
     }
     return 0;
+}
+
+int32_t mxr_decode_stage(mxr_context * c, const int32_t * tokens, const void * h_in, int32_t n_tokens, void * h_out,
+                         float * logits) {
+    if (n_tokens > c->n_ubatch) return -5;
+    return decode_ubatch(c, tokens, n_tokens, false, logits, h_in, h_out);
 }
 
 int32_t mxr_decode_all_logits(mxr_context * c, const int32_t * tokens, int32_t n_tokens, float * logits) {

@@ -553,7 +553,12 @@ static void fa_launch(OpCtx & c, int D, dim3 grid, const FaArgs & a) {
     }
 }
 
+bool fa_mma_ok(const ggml_tensor * dst);
+void fa_mma_run(OpCtx & c, ggml_tensor * dst);
+static bool g_fa_mma_off = getenv("GGML_MI355X_FA_TILE") != nullptr;
+
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
+    if (!g_fa_mma_off && !fa_use_dec(dst) && fa_mma_ok(dst)) { fa_mma_run(c, dst); return; }
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * k = dst->src[1];
     const ggml_tensor * v = dst->src[2];

@@ -1,0 +1,252 @@
+// ops_fattn_mma.hip — FLASH_ATTN_EXT for prefill (many query rows) on CDNA4 matrix cores.
+//
+// Semantics as ops_fattn.hip (ggml-cpu/ops.cpp:8045-8260: q rounded to f16, masked keys
+// skipped, online softmax); the reference GPU path is fattn-mma / fattn-tile
+// (fattn.cu:280-482). Scope: f16 K/V, D in {64, 128}, no softcap / ALiBi / sinks (those
+// keep the tile kernel).
+//
+// MI355X design: one workgroup = 64 query rows of one head, 2 waves x 32 rows. Per tile
+// of 64 keys the workgroup stages K [key][d] and V^T [d][key] (f16) and the mask tile in
+// LDS; each wave computes S = Q K^T with v_mfma_f32_32x32x16_f16 (Q fragments stay in
+// registers for the whole key loop), writes S to LDS, runs the online softmax with two
+// lanes per query row, writes P (f16) back, rescales O and accumulates O += P V with
+// the same MFMA. Key tiles the mask removes entirely (the causal upper triangle) are
+// skipped.
+#include "backend.h"
+
+namespace mx {
+
+typedef _Float16 fhalf8 __attribute__((ext_vector_type(8)));
+typedef float ffloat16v __attribute__((ext_vector_type(16)));
+
+struct FaMmaArgs {
+    const char * q; size_t q1, q2;        // f32 [D, n_q, H]
+    const char * k; size_t k1, k2;        // f16 [D, n_kv, Hkv]
+    const char * v; size_t v1, v2;
+    const char * mask; size_t m1;         // f16 [n_kv, n_q] or null
+    char * dst; size_t d1, d2;            // f32 [D, H, n_q]
+    int n_q, n_kv, H, Hkv;
+    float scale;
+};
+
+constexpr int FM_QT = 64;    // query rows per workgroup
+constexpr int FM_KT = 64;    // keys per tile
+
+template <int D>
+__device__ __forceinline__ int kswz(int row, int chunk) {   // K tile: D/8 16-byte chunks per row
+    constexpr int C = D / 8;
+    return row * C + (chunk ^ (row & (C - 1)));
+}
+__device__ __forceinline__ int vswz(int row, int chunk) {   // V^T tile: 8 chunks (64 keys) per row
+    return row * 8 + (chunk ^ (row & 7));
+}
+
+template <int D>
+__global__ __launch_bounds__(128, 2) void k_fa_mma(FaMmaArgs p) {
+    constexpr int C = D / 8;                 // 16-byte chunks per K row
+    constexpr int NKS = D / 16;              // MFMA k-steps over the head dim
+    constexpr int NDT = D / 32;              // 32-wide output tiles over the head dim
+    __shared__ uint4 ks[FM_KT * C];
+    __shared__ uint4 vts[D * 8];
+    __shared__ uint16_t mk[FM_QT][FM_KT];
+    __shared__ float sbuf[2][32][FM_KT + 1];
+    __shared__ __align__(16) _Float16 pbuf[2][32][FM_KT];
+    __shared__ float arow[2][32], lrow[2][32];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = blockIdx.y, hk = h / (p.H / p.Hkv);
+    const int q0 = blockIdx.x * FM_QT;
+    const int qw = q0 + 32 * wave;           // this wave's first query row
+    const int r32 = lane & 31, hsel = lane >> 5;
+    const char * kb = p.k + (size_t) hk * p.k2;
+    const char * vb = p.v + (size_t) hk * p.v2;
+
+    // Q fragments (A operand: row = query r32, k = 8 dims at 8*hsel within each 16-dim step)
+    fhalf8 qa[NKS];
+    {
+        const int qr = min(qw + r32, p.n_q - 1);
+        const float * qp = (const float *) (p.q + (size_t) qr * p.q1 + (size_t) h * p.q2);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const float4 f0 = *(const float4 *) (qp + 16 * s + 8 * hsel);
+            const float4 f1 = *(const float4 *) (qp + 16 * s + 8 * hsel + 4);
+            qa[s][0] = (_Float16) f0.x; qa[s][1] = (_Float16) f0.y; qa[s][2] = (_Float16) f0.z; qa[s][3] = (_Float16) f0.w;
+            qa[s][4] = (_Float16) f1.x; qa[s][5] = (_Float16) f1.y; qa[s][6] = (_Float16) f1.z; qa[s][7] = (_Float16) f1.w;
+        }
+    }
+    ffloat16v acc_o[NDT];
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc_o[t][e] = 0.f;
+    // softmax state: lane pair (2*row, 2*row+1) owns query row `lane >> 1` of this wave
+    float m_run = -INFINITY, l_run = 0.f;
+    const int srow = lane >> 1, shalf = lane & 1;
+
+    const int n_tiles = (p.n_kv + FM_KT - 1) / FM_KT;
+    for (int kt = 0; kt < n_tiles; ++kt) {
+        const int key0 = kt * FM_KT;
+        // ---- stage the mask tile, K tile and V^T tile
+        int live = 0;
+#pragma unroll
+        for (int j = 0; j < FM_QT * FM_KT / 8 / 128; ++j) {          // 16-byte mask chunks
+            const int u = tid + 128 * j;
+            const int qr = u >> 3, c8 = u & 7;
+            const int qg = q0 + qr, kg = key0 + 8 * c8;
+            uint4 mv;
+            if (p.mask && qg < p.n_q && kg + 8 <= p.n_kv) {
+                mv = *(const uint4 *) (p.mask + (size_t) qg * p.m1 + (size_t) kg * 2);
+            } else {
+                uint16_t tmp[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const bool in = qg < p.n_q && kg + i < p.n_kv;
+                    tmp[i] = !in ? (uint16_t) 0xFC00 : (p.mask ? ((const uint16_t *) (p.mask + (size_t) qg * p.m1))[kg + i] : (uint16_t) 0);
+                }
+                mv = *(uint4 *) tmp;
+            }
+            *(uint4 *) &mk[qr][8 * c8] = mv;
+            // a tile is live if any entry is not -inf (0xFC00)
+            const uint32_t w4[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) live |= ((w4[i] & 0xFFFF) != 0xFC00) | ((w4[i] >> 16) != 0xFC00);
+        }
+        if (!__syncthreads_or(live)) continue;   // the whole tile is masked out for these rows
+#pragma unroll
+        for (int j = 0; j < FM_KT * C / 128; ++j) {
+            const int u = tid + 128 * j;
+            const int kr = u / C, c = u % C;
+            const int kg = min(key0 + kr, p.n_kv - 1);
+            ks[kswz<D>(kr, c)] = *(const uint4 *) (kb + (size_t) kg * p.k1 + 16 * c);
+            const uint4 vv = *(const uint4 *) (vb + (size_t) kg * p.v1 + 16 * c);
+            const uint16_t * vh = (const uint16_t *) &vv;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int d = 8 * c + i;
+                ((uint16_t *) &vts[vswz(d, kr >> 3)])[kr & 7] = vh[i];
+            }
+        }
+        __syncthreads();
+        // ---- S = Q K^T for this wave's 32 rows x 64 keys
+        ffloat16v acc_s[2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc_s[n][e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const uint4 kv = ks[kswz<D>(32 * n + r32, 2 * s + hsel)];
+                acc_s[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[s], *(const fhalf8 *) &kv, acc_s[n], 0, 0, 0);
+            }
+        }
+        // scale + mask -> LDS (C layout: row = (e&3) + 8(e>>2) + 4 hsel, col = key r32)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+                const int col = 32 * n + r32;
+                const float mval = h2f(mk[32 * wave + row][col]);
+                sbuf[wave][row][col] = mval == -INFINITY ? -INFINITY : acc_s[n][e] * p.scale + mval;
+            }
+        __syncthreads();
+        // ---- online softmax: two lanes per row, 32 keys each
+        {
+            float sv[32];
+            float mt = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) { sv[i] = sbuf[wave][srow][32 * shalf + i]; mt = fmaxf(mt, sv[i]); }
+            mt = fmaxf(mt, dpp_f<0xB1>(-INFINITY, mt));
+            const float m_new = fmaxf(m_run, mt);
+            const float alpha = m_run == m_new ? 1.0f : expf(m_run - m_new);
+            float lt = 0.f;
+#pragma unroll
+            for (int i = 0; i < 32; i += 8) {
+                fhalf8 ph;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float pv = m_new == -INFINITY ? 0.f : expf(sv[i + j] - m_new);
+                    lt += pv;
+                    ph[j] = (_Float16) pv;
+                }
+                *(fhalf8 *) &pbuf[wave][srow][32 * shalf + i] = ph;
+            }
+            lt += dpp_f<0xB1>(0.f, lt);
+            l_run = l_run * alpha + lt;
+            m_run = m_new;
+            if (shalf == 0) arow[wave][srow] = alpha;
+        }
+        __syncthreads();
+        // ---- O = O * alpha + P V
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const float al = arow[wave][(e & 3) + 8 * (e >> 2) + 4 * hsel];
+#pragma unroll
+            for (int t = 0; t < NDT; ++t) acc_o[t][e] *= al;
+        }
+#pragma unroll
+        for (int s = 0; s < FM_KT / 16; ++s) {
+            const fhalf8 pa = *(const fhalf8 *) &pbuf[wave][r32][16 * s + 8 * hsel];
+#pragma unroll
+            for (int t = 0; t < NDT; ++t) {
+                const uint4 vv = vts[vswz(32 * t + r32, 2 * s + hsel)];
+                acc_o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, *(const fhalf8 *) &vv, acc_o[t], 0, 0, 0);
+            }
+        }
+        __syncthreads();   // K/V/mask/P buffers are rewritten by the next tile
+    }
+    // ---- normalise and store
+    if (shalf == 0) lrow[wave][srow] = l_run;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+        const int qg = qw + row;
+        if (qg >= p.n_q) continue;
+        const float l = lrow[wave][row];
+        const float inv = l == 0.f ? 0.f : 1.0f / l;
+        float * out = (float *) (p.dst + (size_t) h * p.d1 + (size_t) qg * p.d2);
+#pragma unroll
+        for (int t = 0; t < NDT; ++t) out[32 * t + r32] = acc_o[t][e] * inv;
+    }
+}
+
+bool fa_mma_ok(const ggml_tensor * dst) {
+    const ggml_tensor * q = dst->src[0];
+    const ggml_tensor * k = dst->src[1];
+    const ggml_tensor * v = dst->src[2];
+    const ggml_tensor * m = dst->src[3];
+    if (dst->src[4]) return false;                                        // sinks
+    if (mx_op_param<float>(dst, 1) != 0.0f || mx_op_param<float>(dst, 2) != 0.0f) return false;   // ALiBi, softcap
+    if (q->type != GGML_TYPE_F32 || k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16) return false;
+    const int64_t D = k->ne[0];
+    if ((D != 64 && D != 128) || v->ne[0] != D) return false;
+    if (q->ne[1] < 16 || q->ne[3] != 1 || k->ne[3] != 1 || q->ne[2] % k->ne[2]) return false;
+    if (m && (m->type != GGML_TYPE_F16 || m->ne[2] != 1 || m->ne[3] != 1 || m->nb[1] % 16 || (uintptr_t) m->data % 16)) return false;
+    if (k->nb[1] % 16 || v->nb[1] % 16 || q->nb[1] % 16 || q->nb[0] != 4) return false;
+    if (((uintptr_t) k->data | (uintptr_t) v->data | (uintptr_t) q->data) % 16) return false;
+    if (dst->nb[0] != 4 || k->ne[1] > INT32_MAX / 2 || q->ne[1] > INT32_MAX / 2) return false;
+    return true;
+}
+
+void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * q = dst->src[0];
+    const ggml_tensor * k = dst->src[1];
+    const ggml_tensor * v = dst->src[2];
+    const ggml_tensor * m = dst->src[3];
+    FaMmaArgs p{};
+    p.q = (const char *) q->data; p.q1 = q->nb[1]; p.q2 = q->nb[2];
+    p.k = (const char *) k->data; p.k1 = k->nb[1]; p.k2 = k->nb[2];
+    p.v = (const char *) v->data; p.v1 = v->nb[1]; p.v2 = v->nb[2];
+    if (m) { p.mask = (const char *) m->data; p.m1 = m->nb[1]; }
+    p.dst = (char *) dst->data; p.d1 = dst->nb[1]; p.d2 = dst->nb[2];
+    p.n_q = (int) q->ne[1]; p.n_kv = (int) k->ne[1]; p.H = (int) q->ne[2]; p.Hkv = (int) k->ne[2];
+    p.scale = mx_op_param<float>(dst, 0);
+    dim3 grid((unsigned) mx_ceil_div(p.n_q, FM_QT), (unsigned) p.H);
+    if (k->ne[0] == 64) k_fa_mma<64><<<grid, 128, 0, c.st>>>(p);
+    else k_fa_mma<128><<<grid, 128, 0, c.st>>>(p);
+}
+
+}  // namespace mx

@@ -74,13 +74,15 @@ template <int QT, int LPR, int UPL, int EPI, int W = 4>
 static void launch_cfg(hipStream_t st, const G2Args & p) {
     constexpr int RPB = W * (64 / LPR);
     const unsigned grid = (unsigned) ((p.nrows + RPB - 1) / RPB);
-    const int mode = gemv_mode(p.xs, p.K, p.nrows);
+    const int mode = gemv_mode(p.xs, p.K, p.nrows, 64 * W);
     const size_t lds = gemv_lds_bytes(p.K, mode);
     switch (mode) {
         case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8><<<grid, 64 * W, lds, st>>>(p); break;
         case XS_NORM_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_LDS><<<grid, 64 * W, lds, st>>>(p); break;
         case XS_F32_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32_LDS><<<grid, 64 * W, lds, st>>>(p); break;
         case XS_NORM: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_NORM_H2: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_H2><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_F32_H2: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32_H2><<<grid, 64 * W, lds, st>>>(p); break;
         default: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32><<<grid, 64 * W, lds, st>>>(p); break;
     }
 }

@@ -32,15 +32,24 @@ struct MmqArgs {
     int64_t M, N, K, ne12, r2, r3;
 };
 
-// ---- f32 → f16 activation rows, zero padded to kp --------------------------
+// ---- f32 → f16 activation rows, zero padded to kp (8 values per thread) ------
 __global__ void k_act_f16(const char * __restrict__ x, int64_t K, int64_t ne11, int64_t ne12,
                           size_t nb10, size_t nb11, size_t nb12, size_t nb13, int64_t kp, _Float16 * __restrict__ out) {
     const int64_t col = blockIdx.y;
     const int64_t i11 = col % ne11, i12 = (col / ne11) % ne12, i13 = col / (ne11 * ne12);
     const char * px = x + i11 * nb11 + i12 * nb12 + i13 * nb13;
-    for (int64_t k = blockIdx.x * (int64_t) blockDim.x + threadIdx.x; k < kp; k += (int64_t) gridDim.x * blockDim.x) {
-        out[col * kp + k] = (_Float16) (k < K ? *(const float *) (px + k * nb10) : 0.0f);
+    const int64_t k = 8 * (blockIdx.x * (int64_t) blockDim.x + threadIdx.x);
+    if (k >= kp) return;
+    half8 h;
+    if (nb10 == 4 && k + 8 <= K && ((uintptr_t) (px + 4 * k) % 16) == 0) {
+        const float4 a = *(const float4 *) (px + 4 * k), b = *(const float4 *) (px + 4 * k + 16);
+        h[0] = (_Float16) a.x; h[1] = (_Float16) a.y; h[2] = (_Float16) a.z; h[3] = (_Float16) a.w;
+        h[4] = (_Float16) b.x; h[5] = (_Float16) b.y; h[6] = (_Float16) b.z; h[7] = (_Float16) b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) h[i] = (_Float16) (k + i < K ? *(const float *) (px + (k + i) * nb10) : 0.0f);
     }
+    *(half8 *) (out + col * kp + k) = h;
 }
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 16 + (chunk ^ (row & 15)); }  // in 16-byte units
@@ -271,6 +280,221 @@ __global__ __launch_bounds__(256, 2) void k_mmq(MmqArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined K-quant GEMM (Q4_K / Q5_K / Q6_K, K % 256 == 0): the tile loop of k_mmq with
+// the next K step's global loads (activation chunks + raw super-block bytes) issued
+// into registers before the current step's MFMAs, dequantised into LDS after them, so
+// HBM latency hides behind matrix work. BM weight rows (128, or 64 for small grids so
+// the chip stays filled) × 128 tokens per block, 4 waves 2 × 2.
+// ---------------------------------------------------------------------------
+template <int QT> struct RawW;
+template <> struct RawW<GGML_TYPE_Q4_K> { int4 hd, w; };
+template <> struct RawW<GGML_TYPE_Q5_K> { int4 hd, w, qh; };
+template <> struct RawW<GGML_TYPE_Q6_K> { uint2 la, lb, qh, sc; uint16_t d; };
+
+__device__ __forceinline__ uint2 ldu8(const char * p) {
+    uint2 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 2), 8);
+    return v;
+}
+
+// unit u of the tile: Q4_K/Q5_K (row r = u>>2, 16-byte qs chunk c = u&3 of the half
+// super-block), Q6_K (row r = u>>2, 8-wide l-run t = u&3 of the half n)
+template <int QT>
+__device__ __forceinline__ void raw_load(const MmqArgs & p, const char * wbase, int64_t row, int64_t k0, int c, RawW<QT> & r) {
+    const int64_t rr = row < p.M ? row : p.M - 1;   // clamped: the loads stay branch-free
+    const int64_t sb = k0 >> 8;
+    const int hf = (int) ((k0 >> 7) & 1);
+    if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
+        const char * b = wbase + rr * p.w_row + sb * qsize_of<QT>();
+        r.hd = *(const int4 *) b;
+        r.w = *(const int4 *) (b + (QT == GGML_TYPE_Q4_K ? 16 : 48) + 16 * (4 * hf + c));
+        if constexpr (QT == GGML_TYPE_Q5_K) r.qh = *(const int4 *) (b + 16 + 16 * (c & 1));
+    } else {
+        const char * b = wbase + rr * p.w_row + sb * 210;
+        r.la = ldu8(b + 64 * hf + 8 * c);
+        r.lb = ldu8(b + 64 * hf + 32 + 8 * c);
+        r.qh = ldu8(b + 128 + 32 * hf + 8 * c);
+        r.sc = ldu8(b + 192 + 8 * hf + (c >> 1));
+        r.d = ld_u16(b + 208);
+    }
+}
+
+template <int QT>
+__device__ __forceinline__ void raw_store(const RawW<QT> & r, int k0, bool valid, int rl, int c, uint4 * lds) {
+    if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
+        const int hf = (k0 >> 7) & 1;
+        const int g = 2 * hf + (c >> 1), h = c & 1;
+        // get_scale_min_k4 on the 12 scale bytes held in hd.y..hd.w (register form)
+        auto byte = [&](int j) -> int {
+            const uint32_t v = j < 4 ? (uint32_t) r.hd.y : (j < 8 ? (uint32_t) r.hd.z : (uint32_t) r.hd.w);
+            return (v >> (8 * (j & 3))) & 0xFF;
+        };
+        auto smk = [&](int j, int & sc, int & mn) {
+            if (j < 4) { sc = byte(j) & 63; mn = byte(j + 4) & 63; }
+            else { sc = (byte(j + 4) & 0xF) | ((byte(j - 4) >> 6) << 4); mn = (byte(j + 4) >> 4) | ((byte(j) >> 6) << 4); }
+        };
+        int s0, m0, s1, m1;
+        smk(2 * g, s0, m0);
+        smk(2 * g + 1, s1, m1);
+        const float d = h2f((uint16_t) (r.hd.x & 0xFFFF)), dmin = h2f((uint16_t) ((uint32_t) r.hd.x >> 16));
+        const float d0 = valid ? d * s0 : 0.f, mm0 = valid ? dmin * m0 : 0.f;
+        const float d1 = valid ? d * s1 : 0.f, mm1 = valid ? dmin * m1 : 0.f;
+        const uint32_t wv[4] = {(uint32_t) r.w.x, (uint32_t) r.w.y, (uint32_t) r.w.z, (uint32_t) r.w.w};
+        float lo[16], hi[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t byte = (wv[i >> 2] >> (8 * (i & 3))) & 0xFF;
+            int ql = byte & 0xF, qhh = byte >> 4;
+            if constexpr (QT == GGML_TYPE_Q5_K) {
+                const uint32_t hv[4] = {(uint32_t) r.qh.x, (uint32_t) r.qh.y, (uint32_t) r.qh.z, (uint32_t) r.qh.w};
+                const uint32_t hb = (hv[i >> 2] >> (8 * (i & 3))) & 0xFF;
+                ql += ((hb >> (2 * g)) & 1) << 4;
+                qhh += ((hb >> (2 * g + 1)) & 1) << 4;
+            }
+            lo[i] = d0 * ql - mm0;
+            hi[i] = d1 * qhh - mm1;
+        }
+        const int kl = 64 * (c >> 1) + 16 * h;
+        float t[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = lo[i];
+        st_h8(lds, rl, kl / 8, t);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = lo[8 + i];
+        st_h8(lds, rl, kl / 8 + 1, t);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = hi[i];
+        st_h8(lds, rl, (kl + 32) / 8, t);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = hi[8 + i];
+        st_h8(lds, rl, (kl + 32) / 8 + 1, t);
+    } else {
+        const float d = valid ? h2f(r.d) : 0.f;
+        const uint8_t * la = (const uint8_t *) &r.la, * lb = (const uint8_t *) &r.lb, * hb = (const uint8_t *) &r.qh;
+        const int8_t * scp = (const int8_t *) &r.sc;
+        float v[4][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            v[0][i] = (float) (((la[i] & 0xF) | (((hb[i] >> 0) & 3) << 4)) - 32);
+            v[1][i] = (float) (((lb[i] & 0xF) | (((hb[i] >> 2) & 3) << 4)) - 32);
+            v[2][i] = (float) (((la[i] >> 4) | (((hb[i] >> 4) & 3) << 4)) - 32);
+            v[3][i] = (float) (((lb[i] >> 4) | (((hb[i] >> 6) & 3) << 4)) - 32);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const float sc = d * (float) scp[2 * qq];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[qq][i] *= sc;
+            st_h8(lds, rl, (32 * qq + 8 * c) / 8, v[qq]);
+        }
+    }
+}
+
+template <int QT, int BM>
+__global__ __launch_bounds__(256, 2) void k_mmq2(MmqArgs p) {
+    constexpr int UPT = BM * 4 / 256;           // weight units per thread per K step
+    constexpr int WM = BM / 2;                  // weight rows per wave
+    constexpr int TM = WM / 32;                 // 32-row MFMA tiles per wave (1 or 2)
+    __shared__ uint4 lds_a[MM_BT * MM_BK / 8];
+    __shared__ uint4 lds_b[BM * MM_BK / 8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;    // wave: 64 tokens (wm) x WM weight rows (wn)
+    const int64_t tok0 = (int64_t) blockIdx.x * MM_BT;
+    const int64_t row0 = (int64_t) blockIdx.y * BM;
+    const int64_t ch = blockIdx.z;
+    const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
+    const char * wbase = p.w + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
+    const _Float16 * xbase = p.x + ch * p.N * p.kp;
+    const int64_t nk = p.K / MM_BK;
+
+    float16v acc[2][TM];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    uint4 ra[8];
+    RawW<QT> rw[UPT];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int unit = tid + 256 * it;
+            const int t = unit >> 4, chn = unit & 15;
+            const int64_t tok = min(tok0 + t, p.N - 1);
+            ra[it] = *(const uint4 *) (xbase + tok * p.kp + k0 + 8 * chn);
+        }
+#pragma unroll
+        for (int it = 0; it < UPT; ++it) {
+            const int unit = tid + 256 * it;
+            raw_load<QT>(p, wbase, row0 + (unit >> 2), k0, unit & 3, rw[it]);
+        }
+    };
+    auto store = [&](int64_t k0) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int unit = tid + 256 * it;
+            const int t = unit >> 4, chn = unit & 15;
+            lds_a[swz(t, chn)] = tok0 + t < p.N ? ra[it] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int it = 0; it < UPT; ++it) {
+            const int unit = tid + 256 * it;
+            raw_store<QT>(rw[it], (int) k0, row0 + (unit >> 2) < p.M, unit >> 2, unit & 3, lds_b);
+        }
+    };
+
+    const int r = lane & 31, hsel = lane >> 5;
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int64_t kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) load((kt + 1) * MM_BK);       // next step's bytes in flight during the MFMAs
+#pragma unroll
+        for (int kk = 0; kk < MM_BK; kk += 16) {
+            const int chn = kk / 8 + hsel;
+            half8 a[2], b[TM];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint4 va = lds_a[swz(wm * 64 + i * 32 + r, chn)];
+                a[i] = *(const half8 *) &va;
+            }
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                const uint4 vb = lds_b[swz(wn * WM + j * 32 + r, chn)];
+                b[j] = *(const half8 *) &vb;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < TM; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+        if (kt + 1 < nk) {
+            store((kt + 1) * MM_BK);
+            __syncthreads();
+        }
+    }
+    float * dbase = p.dst + i12 * p.d_c2 + i13 * p.d_c3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            const int64_t wrow = row0 + wn * WM + j * 32 + (lane & 31);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t tok = tok0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+                if (tok < p.N && wrow < p.M) dbase[tok * p.d_col + wrow] = acc[i][j][e];
+            }
+        }
+    }
+}
+
+static bool g_mmq_v1 = getenv("GGML_MI355X_MMQ_V1") != nullptr;
+
 bool mmq_type_ok(int t) {
     switch (t) {
         case GGML_TYPE_Q4_0: case GGML_TYPE_Q4_1: case GGML_TYPE_Q5_0: case GGML_TYPE_Q5_1: case GGML_TYPE_Q8_0:
@@ -294,11 +518,20 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
     const ggml_tensor * x = dst->src[1];
     const int64_t kp = mmq_kp(dst);
     const int64_t ncols = x->ne[1] * x->ne[2] * x->ne[3];
-    _Float16 * xa = (_Float16 *) c.scratch->take(ncols * kp * 2);
-    {
-        dim3 grid((unsigned) std::min<int64_t>(mx_ceil_div(kp, 256), 16), (unsigned) ncols);
+    const size_t abytes = (size_t) ncols * kp * 2;
+    Stream * s = c.s;
+    _Float16 * xa;
+    const int64_t key[4] = {x->ne[0], ncols, (int64_t) x->nb[1], kp};
+    const bool cacheable = s->f16.base && abytes <= s->f16.cap && mx_is_contiguous(x);
+    if (cacheable && s->f16_src == x->data && !memcmp(s->f16_key, key, sizeof key)) {
+        xa = (_Float16 *) s->f16.base;      // same activation as the previous GEMM (q/k/v, gate/up)
+    } else {
+        xa = cacheable ? (_Float16 *) s->f16.base : (_Float16 *) c.scratch->take(abytes);
+        dim3 grid((unsigned) mx_ceil_div(kp, 8 * 256), (unsigned) ncols);
         k_act_f16<<<grid, 256, 0, c.st>>>((const char *) x->data, x->ne[0], x->ne[1], x->ne[2],
                                           x->nb[0], x->nb[1], x->nb[2], x->nb[3], kp, xa);
+        if (cacheable) { s->f16_src = x->data; memcpy(s->f16_key, key, sizeof key); }
+        else s->f16_src = nullptr;
     }
     MmqArgs p{};
     p.w = (const char *) w->data; p.w_row = w->nb[1]; p.w_c2 = w->nb[2]; p.w_c3 = w->nb[3];
@@ -306,6 +539,15 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
     p.dst = (float *) dst->data; p.d_col = dst->nb[1] / 4; p.d_c2 = dst->nb[2] / 4; p.d_c3 = dst->nb[3] / 4;
     p.M = w->ne[1]; p.N = x->ne[1]; p.K = w->ne[0]; p.ne12 = x->ne[2];
     p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
+    const bool kq = w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
+    if (kq && !g_mmq_v1 && p.K % 256 == 0) {
+        const int64_t tiles128 = mx_ceil_div(p.N, MM_BT) * mx_ceil_div(p.M, 128) * (x->ne[2] * x->ne[3]);
+        const int bm = (tiles128 < 512 || g_tune[8] == 64) ? 64 : 128;
+        dim3 g2((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, bm), (unsigned) (x->ne[2] * x->ne[3]));
+#define MQ2(T) case T: if (bm == 64) k_mmq2<T, 64><<<g2, 256, 0, c.st>>>(p); else k_mmq2<T, 128><<<g2, 256, 0, c.st>>>(p); return;
+        switch (w->type) { MQ2(GGML_TYPE_Q4_K) MQ2(GGML_TYPE_Q5_K) MQ2(GGML_TYPE_Q6_K) default: break; }
+#undef MQ2
+    }
     dim3 grid((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, MM_BW), (unsigned) (x->ne[2] * x->ne[3]));
     switch (w->type) {
 #define MQ(T) case T: k_mmq<T><<<grid, 256, 0, c.st>>>(p); break;
@@ -357,6 +599,12 @@ bool mul_mat_supported(const ggml_tensor * dst) {
     }
     if (mx_type(w->type).quant && w->nb[0] != (size_t) mx_type(w->type).size) return false;
     return true;
+}
+
+size_t mmq_act_bytes(const ggml_tensor * dst) {
+    const ggml_tensor * x = dst->src[1];
+    if (dst->op != GGML_OP_MUL_MAT || x->ne[1] <= 8 || !mmq_ok(dst)) return 0;
+    return (size_t) x->ne[1] * x->ne[2] * x->ne[3] * mmq_kp(dst) * 2;
 }
 
 size_t mul_mat_scratch(const ggml_tensor * dst) {

@@ -199,7 +199,8 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs)) return 0;
     const int mode = gemv_mode(p.xs, p.K);
     if (mode != XS_NORM) {   // the fused block normally follows attn_norm; other sources
-#define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8> : k_qkv_rope_store<TA, TV, XS_F32>;
+#define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8> : \
+        mode == XS_NORM_H2 ? k_qkv_rope_store<TA, TV, XS_NORM_H2> : k_qkv_rope_store<TA, TV, XS_F32_H2>;
         QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
         QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
         QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)

@@ -46,6 +46,28 @@ class Model:
         return cls(backend, lib.mxr_model_random(backend.ptr, ctypes.byref(h), recipe.encode(), seed))
 
     @classmethod
+    def random_stage(cls, backend, shape, layers, recipe="q4_k_m", seed=1234):
+        """Pipeline stage holding layers [layers[0], layers[1]) of Model.random's model."""
+        lib = _lib.load()
+        h = hparams(**shape)
+        return cls(backend, lib.mxr_model_random_stage(backend.ptr, ctypes.byref(h), recipe.encode(), seed,
+                                                       int(layers[0]), int(layers[1])))
+
+    @property
+    def stage(self):
+        a, b = ctypes.c_int32(), ctypes.c_int32()
+        self.lib.mxr_model_stage(self.ptr, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    @property
+    def is_first_stage(self):
+        return self.stage[0] == 0
+
+    @property
+    def is_last_stage(self):
+        return self.stage[1] == self.hp.n_layer
+
+    @classmethod
     def load_gguf(cls, backend, path):
         lib = _lib.load()
         return cls(backend, lib.mxr_model_load_gguf(backend.ptr, str(path).encode()))
@@ -92,6 +114,22 @@ class Session:
         r = self.lib.mxr_decode(self.ptr, toks.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(toks), lp)
         if r != 0:
             raise RuntimeError(f"mxr_decode failed ({r})")
+        return self._logits.copy() if want_logits else None
+
+    def decode_stage(self, tokens=None, h_in=0, n_tokens=None, h_out=0, want_logits=False):
+        """One ubatch through a pipeline stage. tokens (first stage) or h_in (an address of
+        f32 [n_tokens, n_embd], device or host) in; h_out (address) or the last token's
+        logits out. Returns the logits (last stage, want_logits) or None."""
+        tp = None
+        if tokens is not None:
+            toks = np.ascontiguousarray(tokens, dtype=np.int32)
+            n_tokens = len(toks)
+            tp = toks.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        lp = self._logits.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if want_logits else None
+        r = self.lib.mxr_decode_stage(self.ptr, tp, ctypes.c_void_p(h_in or None), int(n_tokens),
+                                      ctypes.c_void_p(h_out or None), lp)
+        if r != 0:
+            raise RuntimeError(f"mxr_decode_stage failed ({r})")
         return self._logits.copy() if want_logits else None
 
     def decode_all(self, tokens):

@@ -112,3 +112,58 @@ def test_decode_fusions_fire(pkg, backend, tiny, fa):
     fused = backend.stats()["nodes_fused"] - before
     s.free()
     assert fused >= 12 * TINY["n_layer"], f"only {fused} nodes fused"
+
+
+@pytest.mark.parametrize("split", [1, 2])
+def test_pipeline_stages_match_whole_model(pkg, backend, split):
+    """Layer split: stages [0,s) and [s,L) of the same seeded model, the hidden
+    state handed over between them, give the whole model's logits (decode and prefill)."""
+    full = pkg.Model.random(backend, TINY, "q4_k_m", seed=11)
+    s0 = pkg.Model.random_stage(backend, TINY, (0, split), "q4_k_m", seed=11)
+    s1 = pkg.Model.random_stage(backend, TINY, (split, TINY["n_layer"]), "q4_k_m", seed=11)
+    assert s0.is_first_stage and not s0.is_last_stage and s1.is_last_stage
+    a = pkg.Session(full, n_ctx=256)
+    b0 = pkg.Session(s0, n_ctx=256)
+    b1 = pkg.Session(s1, n_ctx=256)
+    rng = np.random.default_rng(12)
+    toks = rng.integers(0, TINY["n_vocab"], 9).astype(np.int32)
+    # prefill 6 tokens, then 3 single-token steps
+    h = np.empty((6, TINY["n_embd"]), np.float32)
+    b0.decode_stage(tokens=toks[:6], h_out=h.ctypes.data)
+    got = [b1.decode_stage(h_in=h.ctypes.data, n_tokens=6, want_logits=True)]
+    ref = [a.decode(toks[:6])]
+    h1 = np.empty((1, TINY["n_embd"]), np.float32)
+    for t in toks[6:]:
+        b0.decode_stage(tokens=np.array([t], np.int32), h_out=h1.ctypes.data)
+        got.append(b1.decode_stage(h_in=h1.ctypes.data, n_tokens=1, want_logits=True))
+        ref.append(a.decode(np.array([t], np.int32)))
+    for x, y in zip(got, ref):
+        assert np.all(np.isfinite(x))
+        assert nmse(x, y) < 1e-10
+    for o in (a, b0, b1, full, s0, s1):
+        o.free()
+
+
+def test_bench_pipeline_two_ranks_one_gpu(tmp_path):
+    """bench.py's layer-split pipeline end to end with 2 ranks sharing the one GPU of the
+    test box (gloo + pinned host hand-off; the 8-GPU node uses RCCL over xGMI)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MX_DIST_BACKEND="gloo", MX_PIPE_HOST="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--model", "tinyllama", "--tg", "16", "--pp", "64", "--steps", "1", "--warmup", "1",
+           "--skip-roofline", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["value"] > 0 and "layer split" in out["config"]["parallelism"]
+    assert out["pp512_tok_s"] > 0

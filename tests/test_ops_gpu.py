@@ -170,10 +170,11 @@ def test_fused_gate_up_swiglu(pkg, backend, orc, tname):
     assert backend.stats()["nodes_fused"] >= before + 2, "gate/up/GLU fusion did not fire"
 
 
-@pytest.mark.parametrize("n_q,n_kv,H,Hkv", [(1, 256, 32, 8), (1, 700, 8, 8), (5, 512, 8, 2), (64, 300, 4, 4)])
-def test_flash_attn(pkg, backend, orc, n_q, n_kv, H, Hkv):
+@pytest.mark.parametrize("n_q,n_kv,H,Hkv,D", [(1, 256, 32, 8, 128), (1, 700, 8, 8, 128), (5, 512, 8, 2, 128),
+                                               (64, 300, 4, 4, 128), (100, 333, 8, 2, 128), (130, 130, 4, 1, 64),
+                                               (1, 4096, 8, 2, 128), (3, 1000, 4, 2, 64)])
+def test_flash_attn(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
     rng = np.random.default_rng(n_q * 1000 + n_kv)
-    D = 128
     q = rng.standard_normal((H, n_q, D)).astype(np.float32)
     k = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16)
     v = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16)

@@ -68,6 +68,20 @@ def case_gemv(pkg, be, rng, tname, K, M, glu=False, add=False):
     return ctx, graphs
 
 
+def case_gemm(pkg, be, rng, tname, K, M, N=512):
+    """prefill GEMM: M weight rows x N tokens over K."""
+    tid = NAMES[tname]
+    w, _ = rand_quant(tid, M, K, rng)
+    ctx = pkg.Context()
+    x = ctx.new_tensor("f32", K, N)
+    tw = ctx.new_tensor(tid, K, M)
+    g = ctx.build(ctx.mul_mat(tw, x))
+    ctx.alloc(be)
+    tw.set(w)
+    x.set(rng.standard_normal((N, K)).astype(np.float32))
+    return ctx, [g]
+
+
 def case_ffn(pkg, be, rng, tname="q4_K", tdown="q4_K", K=4096, F=14336):
     """ffn_norm-less FFN block: gate/up SwiGLU GEMV (+q8 of its output) -> down + residual."""
     tid, tdn = NAMES[tname], NAMES[tdown]
@@ -164,6 +178,10 @@ CASES = {
     "down_q6k_add": lambda p, b, r: case_gemv(p, b, r, "q6_K", 14336, 4096, add=True),
     "lm_head_q6k": lambda p, b, r: case_gemv(p, b, r, "q6_K", 4096, 128256),
     "attn_in": lambda p, b, r: case_attn_in(p, b, r),
+    "pp_q_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 4096),
+    "pp_gate_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 14336),
+    "pp_down_q6k": lambda p, b, r: case_gemm(p, b, r, "q6_K", 14336, 4096),
+    "pp_k_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 1024),
     "ffn_q4k": lambda p, b, r: case_ffn(p, b, r),
     "ffn_q4k_q6k": lambda p, b, r: case_ffn(p, b, r, tdown="q6_K"),
     "fa_256": lambda p, b, r: case_fa(p, b, r, 256),
