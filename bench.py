@@ -91,10 +91,12 @@ def tg_step(sess, rng, n_vocab, n_gen):
 
 def roofline_glu(pkg, be, model, iters=256):
     """Dominant decode kernel: the fused gate/up SwiGLU GEMV (2.1 GB of the 4.6 GB read
-    per token). Timed with HIP events on the backend's stream over back-to-back launches
-    that cycle through all 32 layers' real ffn_gate/ffn_up weights (4.2 GB, so every
-    launch streams from HBM, not the 256 MiB MALL). Algorithmic bytes per launch = both
-    Q4_K weight matrices + the f32 activation."""
+    per token), launched exactly as in decode (ffn_norm absorbed in the prologue, q8 of
+    the output emitted for the down projection). Timed with HIP events on the backend's
+    stream over back-to-back launches that cycle through all 32 layers' real
+    ffn_gate/ffn_up weights (4.2 GB, so every launch streams from HBM, not the 256 MiB
+    MALL). Algorithmic bytes per launch = both Q4_K weight matrices + the f32 activation
+    and norm weight read + the f32 and q8 outputs written."""
     lib = pkg._lib.load()
     l0, l1 = model.stage
     n_layer = l1 - l0
@@ -109,12 +111,21 @@ def roofline_glu(pkg, be, model, iters=256):
     ctx.alloc(be)
     x.set(np.random.default_rng(7).standard_normal(K).astype(np.float32))
     us = lib.ggml_backend_mi355x_time_mmvq(be.ptr, wg, wu, n_layer, x.ptr, out.ptr, iters)
-    bytes_per_launch = 2 * t0.nbytes() + K * 4
+    bytes_per_launch = 2 * t0.nbytes() + 2 * K * 4 + M * 4 + M + (M // 32) * 8
     ctx.free()
     achieved = bytes_per_launch / (us * 1e-6) / 1e9
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01", "pmc_glu.json")   # scripts/pmc_roofline.sh
+    if os.path.exists(pmc):
+        try:
+            rec = json.load(open(pmc))
+            if rec.get("bytes_per_launch") == int(bytes_per_launch):
+                traffic, traffic_src = rec["hbm_bytes_per_launch"], os.path.relpath(pmc, ROOT)
+        except Exception:  # noqa: BLE001
+            pass
     return {"bound": "hbm", "kernel": f"k_gemv2 SwiGLU (ffn gate+up, {K}->{M} x2, cycled over {n_layer} layers)",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(us, 2)}
 
 
@@ -253,7 +264,17 @@ def main():
     ap.add_argument("--cpu-pp", type=int, default=32)
     ap.add_argument("--cpu-tg", type=int, default=16)
     ap.add_argument("--skip-roofline", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the dominant-kernel timing (for scripts/pmc_roofline.sh's rocprofv3 --pmc passes)")
     args = ap.parse_args()
+    if args.roofline_only:
+        from mi355x_pkg import load_package
+        pkg = load_package()
+        be = pkg.Backend(0)
+        model = pkg.Model.random(be, getattr(pkg, MODELS[args.model][0]), args.recipe or MODELS[args.model][1], seed=1234)
+        print(json.dumps(roofline_glu(pkg, be, model)), flush=True)
+        model.free()
+        return
 
     world, rank, local, dist = dist_setup(args.gpus)
     mode = args.mode if args.mode != "auto" else ("pipeline" if world > 1 else "single")

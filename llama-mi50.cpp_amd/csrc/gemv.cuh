@@ -48,16 +48,20 @@ __host__ __device__ inline size_t gemv_lds_bytes(int64_t K, int mode = XS_Q8) {
     return gemv_lds_base(K) + (mode == XS_F32_LDS || mode == XS_NORM_LDS ? 4 * (size_t) K : 0) + (mode == XS_NORM_LDS ? 4 * (size_t) K : 0);
 }
 __host__ __device__ inline float * gemv_lds_red(char * smem, int64_t K) { return (float *) (smem + K + (K / 32) * 8); }
-// Staging mode for a source. LDS-DMA moves only ~25 GB/s per CU, so it loses on the
-// one-block-per-CU grids of the layer GEMVs (the register path's x loads ride along
-// with the weights) and wins on the huge lm_head grid, where the register path's VGPRs
-// cost occupancy (tools/opbench.py --trace, profiles/r01).
-inline int gemv_mode(const XStage & xs, int64_t K, int64_t nrows = 0, int nt = 256) {
+// Staging mode for a source. Register staging keeps x (and the norm weight) in VGPRs,
+// LDS-DMA staging (~25 GB/s per CU) keeps them out of the register file. Measured on
+// MI355X (tools/opbench.py ffn_block / q_q4k, profiles/r01): grids of one block per CU
+// (the 4096-row projections) are latency-bound and win with registers; grids of several
+// waves' worth per SIMD (SwiGLU, lm_head) win with the occupancy LDS staging buys.
+extern int g_tune[16];
+inline int gemv_mode(const XStage & xs, int64_t K, int64_t n_waves = 0, int nt = 256) {
     if (xs.q8) return XS_Q8;
-    const bool big = nrows >= 32768;
+    bool lds = n_waves >= 2048;
+    if (g_tune[9] == 1) lds = true;    // sweeps
+    if (g_tune[9] == 2) lds = false;
     const bool h2 = K > 16 * nt;
-    if (xs.norm) return big && gemv_lds_bytes(K, XS_NORM_LDS) <= 65536 ? XS_NORM_LDS : (h2 ? XS_NORM_H2 : XS_NORM);
-    return big && gemv_lds_bytes(K, XS_F32_LDS) <= 65536 ? XS_F32_LDS : (h2 ? XS_F32_H2 : XS_F32);
+    if (xs.norm) return lds && gemv_lds_bytes(K, XS_NORM_LDS) <= 65536 ? XS_NORM_LDS : (h2 ? XS_NORM_H2 : XS_NORM);
+    return lds && gemv_lds_bytes(K, XS_F32_LDS) <= 65536 ? XS_F32_LDS : (h2 ? XS_F32_H2 : XS_F32);
 }
 
 __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {

@@ -27,7 +27,6 @@ struct G2Args {
 template <int QT, int LPR, int UPL, int EPI, int W, int MODE>
 __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     extern __shared__ __align__(16) char smem[];
-    __shared__ float o32[32];
     constexpr int NM = EPI == 1 ? 2 : 1;
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -52,19 +51,22 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     if (sub == LPR - 1 && valid) p.dst[row] = v;
     MX_TRACE(tr, 4);
     MX_TRACE_BLK(p.trace_blk, 1);
-    if constexpr (W * RPW == 32) {
-        if (p.q8o) {     // block-uniform
-            if (sub == LPR - 1) o32[row & 31] = v;
+    constexpr int RPB = W * RPW;
+    if constexpr (RPB % 32 == 0 && RPB / 32 <= W) {
+        if (p.q8o) {     // block-uniform: the q8 form of this block's RPB outputs, one wave per 32
+            __shared__ float orow[RPB];
+            if (sub == LPR - 1) orow[row - blockIdx.x * RPB] = v;
             __syncthreads();
-            if (wave == 0 && lane < 32) {
-                const float x = o32[lane];
+            if (wave < RPB / 32 && lane < 32) {
+                const float x = orow[32 * wave + lane];
                 const float amax = lane_bcast(dpp_max_group<32>(fabsf(x)), 31);
                 const float dd = amax / 127.0f;
                 const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
                 const int qi = (int) roundf(x * id);
                 const int sum = __builtin_amdgcn_readlane(dpp_sum_group_i<32>(qi), 31);
-                p.q8o[blockIdx.x * 32 + lane] = (int8_t) qi;
-                if (lane == 0) { p.q8od[blockIdx.x] = dd; p.q8os[blockIdx.x] = dd * (float) sum; }
+                const int blk = blockIdx.x * (RPB / 32) + wave;
+                p.q8o[blk * 32 + lane] = (int8_t) qi;
+                if (lane == 0) { p.q8od[blk] = dd; p.q8os[blk] = dd * (float) sum; }
             }
         }
     }
@@ -74,7 +76,7 @@ template <int QT, int LPR, int UPL, int EPI, int W = 4>
 static void launch_cfg(hipStream_t st, const G2Args & p) {
     constexpr int RPB = W * (64 / LPR);
     const unsigned grid = (unsigned) ((p.nrows + RPB - 1) / RPB);
-    const int mode = gemv_mode(p.xs, p.K, p.nrows, 64 * W);
+    const int mode = gemv_mode(p.xs, p.K, (int64_t) grid * W, 64 * W);
     const size_t lds = gemv_lds_bytes(p.K, mode);
     switch (mode) {
         case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8><<<grid, 64 * W, lds, st>>>(p); break;
@@ -91,8 +93,10 @@ template <int QT, int EPI>
 static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
     if constexpr (EPI == 1) {
         if (p.q8o) {   // 32 rows per block; g_tune[4] picks the geometry (sweeps)
-            if (g_tune[4] == 1) return launch_cfg<QT, 16, 2, 1, 8>(st, p);
-            return launch_cfg<QT, 32, 1, 1, 16>(st, p);   // best in the ffn sweep
+            // tools/opbench.py ffn_block --sweep-glu8: W8 LPR16 UPL2 with LDS-staged norm best
+            if (g_tune[4] == 1) return launch_cfg<QT, 32, 1, 1, 16>(st, p);
+            if (g_tune[4] == 3 && p.nrows % 64 == 0) return launch_cfg<QT, 16, 2, 1, 16>(st, p);
+            return launch_cfg<QT, 16, 2, 1, 8>(st, p);
         }
     }
     constexpr bool FULL = QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q6_K;   // full tuning grid

@@ -82,4 +82,8 @@ void fill_const_f32(const ggml_tensor * t, float v, hipStream_t st) {
     k_fill_const<<<1024, 256, 0, st>>>((float *) t->data, mx_nelements(t), v);
 }
 
+void fill_const_f32_ptr(float * p, int64_t n, float v, hipStream_t st) {
+    k_fill_const<<<1024, 256, 0, st>>>(p, n, v);
+}
+
 }  // namespace mx

@@ -542,7 +542,8 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
     const bool kq = w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
     if (kq && !g_mmq_v1 && p.K % 256 == 0) {
         const int64_t tiles128 = mx_ceil_div(p.N, MM_BT) * mx_ceil_div(p.M, 128) * (x->ne[2] * x->ne[3]);
-        const int bm = (tiles128 < 512 || g_tune[8] == 64) ? 64 : 128;
+        int bm = tiles128 < 512 ? 64 : 128;
+        if (g_tune[8]) bm = g_tune[8];   // sweeps
         dim3 g2((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, bm), (unsigned) (x->ne[2] * x->ne[3]));
 #define MQ2(T) case T: if (bm == 64) k_mmq2<T, 64><<<g2, 256, 0, c.st>>>(p); else k_mmq2<T, 128><<<g2, 256, 0, c.st>>>(p); return;
         switch (w->type) { MQ2(GGML_TYPE_Q4_K) MQ2(GGML_TYPE_Q5_K) MQ2(GGML_TYPE_Q6_K) default: break; }

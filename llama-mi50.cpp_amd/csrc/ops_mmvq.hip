@@ -10,6 +10,8 @@
 
 namespace mx {
 
+void fill_const_f32_ptr(float * p, int64_t n, float v, hipStream_t st);
+
 // ---------------------------------------------------------------------------
 // activation quantisation: column c (flattened i11,i12,i13) → int8 + per-32 d, d·Σq
 // (quantize_q8_1, ggml-cuda/quantize.cu:5-48: d = amax/127, q = round(x/d))
@@ -364,22 +366,43 @@ bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, 
 // MUL_MAT(w, x) (or the fused gate/up GLU when w2 != NULL) with HIP events on the
 // backend's own stream. Returns the average µs per launch.
 // ---------------------------------------------------------------------------
-double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * const * w2, int nw,
+double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * const * w2, int nw_n,
                  const ggml_tensor * x, ggml_tensor * dst, int iters) {
     OpCtx c{s, s->stream, &s->scratch};
-    MX_ASSERT(nw >= 1);
+    MX_ASSERT(nw_n >= 1);
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
     if (g_gemv2 && gemv2_ok(w[0], x, dst)) {
-        // exactly the launch the executor makes; cycling over nw weight sets (e.g. all
-        // layers of a model) so the stream comes from HBM, not the 256 MiB MALL
-        const XStage xs{(const float *) x->data, nullptr, 0.0f, 0};
-        auto launch = [&](int i) { gemv2_launch(c, w[i % nw], w2 ? w2[i % nw] : nullptr, xs, (float *) dst->data, nullptr); };
+        // exactly the launch the executor makes in decode: for the SwiGLU pair, the
+        // ffn_norm absorbed into the prologue and the q8 form of the output emitted for
+        // the down projection; cycling over nw weight sets (e.g. all layers of a model) so
+        // the stream comes from HBM, not the 256 MiB MALL
+        const int64_t K = w[0]->ne[0], M = w[0]->ne[1];
+        float * nw = nullptr;
+        ActQ q8{};
+        char * q8buf = nullptr;
+        if (w2) {
+            HIP_CHECK(hipMalloc((void **) &nw, K * sizeof(float)));
+            fill_const_f32_ptr(nw, K, 1.0f, s->stream);
+            HIP_CHECK(hipMalloc((void **) &q8buf, M + 2 * (M / 32) * sizeof(float) + 512));
+            q8.q = (const int8_t *) q8buf;
+            q8.d = (const float *) (q8buf + ((M + 255) & ~255));
+            q8.s = q8.d + M / 32;
+            q8.kp = M;
+        }
+        const XStage xs = w2 ? XStage{(const float *) x->data, nw, 1e-5f, 1} : XStage{(const float *) x->data, nullptr, 0.0f, 0};
+        const bool use_q8 = w2 && M % 32 == 0;
+        auto launch = [&](int i) {
+            gemv2_launch(c, w[i % nw_n], w2 ? w2[i % nw_n] : nullptr, xs, (float *) dst->data, nullptr, use_q8 ? &q8 : nullptr);
+        };
         for (int i = 0; i < 3; ++i) launch(i);
         HIP_CHECK(hipEventRecord(e0, s->stream));
         for (int i = 0; i < iters; ++i) launch(i);
         HIP_CHECK(hipEventRecord(e1, s->stream));
+        HIP_CHECK(hipEventSynchronize(e1));
+        if (nw) HIP_CHECK(hipFree(nw));
+        if (q8buf) HIP_CHECK(hipFree(q8buf));
     } else {
         const size_t need = quantize_scratch(x);
         if (need > s->scratch.cap) {
@@ -393,8 +416,8 @@ double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * 
         ActQ a = carve((char *) s->scratch.take(act_slot_bytes(x)), x);
         a = quantize_into(c, x, (int8_t *) a.q, (float *) a.d, (float *) a.s);
         auto launch = [&](int i) {
-            MmvArgs p = mmv_args(w[i % nw], x, dst);
-            if (w2) { p.w2 = (const char *) w2[i % nw]->data; mmvq_dispatch<1>(c, w[0]->type, p, a, 1); }
+            MmvArgs p = mmv_args(w[i % nw_n], x, dst);
+            if (w2) { p.w2 = (const char *) w2[i % nw_n]->data; mmvq_dispatch<1>(c, w[0]->type, p, a, 1); }
             else mmvq_dispatch<0>(c, w[0]->type, p, a, 1);
         };
         for (int i = 0; i < 3; ++i) launch(i);

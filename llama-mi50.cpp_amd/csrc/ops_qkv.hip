@@ -197,7 +197,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
 #undef QKV
     if (!kern) return 0;
     if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs)) return 0;
-    const int mode = gemv_mode(p.xs, p.K);
+    const int mode = gemv_mode(p.xs, p.K, 0);
     if (mode != XS_NORM) {   // the fused block normally follows attn_norm; other sources
 #define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8> : \
         mode == XS_NORM_H2 ? k_qkv_rope_store<TA, TV, XS_NORM_H2> : k_qkv_rope_store<TA, TV, XS_F32_H2>;

@@ -140,6 +140,31 @@ def case_attn_in(pkg, be, rng, K=4096, H=32, Hkv=8, hd=128, n_ctx=512, tv="q6_K"
     return ctx, graphs
 
 
+def case_ffn_block(pkg, be, rng, tname="q4_K", tdown="q4_K", K=4096, F=14336):
+    """ffn_norm -> gate/up SwiGLU (norm absorbed, q8 out) -> down + residual: the decode FFN."""
+    tid, tdn = NAMES[tname], NAMES[tdown]
+    wg, _ = rand_quant(tid, F, K, rng)
+    wd, _ = rand_quant(tdn, K, F, rng)
+    n = copies_for(2 * len(wg) + len(wd))
+    ctx = pkg.Context()
+    x = ctx.new_tensor("f32", K, 1)
+    nw = ctx.new_tensor("f32", K)
+    graphs, ws = [], []
+    for _ in range(n):
+        tg, tu, td = ctx.new_tensor(tid, K, F), ctx.new_tensor(tid, K, F), ctx.new_tensor(tdn, F, K)
+        ws += [(tg, wg), (tu, wg), (td, wd)]
+        cur = ctx.mul(ctx.rms_norm(x, 1e-5), nw)
+        h = ctx.swiglu_split(ctx.mul_mat(tg, cur), ctx.mul_mat(tu, cur))
+        graphs.append(ctx.add(ctx.mul_mat(td, h), x))
+    graphs = [ctx.build(o) for o in graphs]
+    ctx.alloc(be)
+    for t, w in ws:
+        t.set(w)
+    x.set(rng.standard_normal(K).astype(np.float32))
+    nw.set(np.ones(K, np.float32))
+    return ctx, graphs
+
+
 def case_fa(pkg, be, rng, n_kv, H=32, Hkv=8, D=128):
     ctx = pkg.Context()
     q = ctx.new_tensor("f32", D, 1, H)
@@ -183,6 +208,7 @@ CASES = {
     "pp_down_q6k": lambda p, b, r: case_gemm(p, b, r, "q6_K", 14336, 4096),
     "pp_k_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 1024),
     "ffn_q4k": lambda p, b, r: case_ffn(p, b, r),
+    "ffn_block": lambda p, b, r: case_ffn_block(p, b, r),
     "ffn_q4k_q6k": lambda p, b, r: case_ffn(p, b, r, tdown="q6_K"),
     "fa_256": lambda p, b, r: case_fa(p, b, r, 256),
     "fa_1024": lambda p, b, r: case_fa(p, b, r, 1024),
@@ -201,6 +227,7 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="GEMV cases under every (lanes/row, units/lane) geometry")
     ap.add_argument("--trace", action="store_true", help="print phase timestamps of workgroup 0")
     ap.add_argument("--trace-blocks", action="store_true", help="GEMV cases: per-workgroup start/end spread")
+    ap.add_argument("--sweep-mm", action="store_true", help="pp_* cases under both GEMM row tiles (64, 128)")
     ap.add_argument("--sweep-glu8", action="store_true", help="ffn cases under every q8-emitting SwiGLU geometry")
     args = ap.parse_args()
     pkg = load_package()
@@ -210,18 +237,32 @@ def main():
     names = []
     for name in args.only or list(CASES):
         cfgs = [None]
+        if args.sweep_mm and name.startswith("pp_"):
+            for bm in (64, 128):
+                lib.ggml_backend_mi355x_set_tune(8, bm)
+                separator(pkg, be)
+                for it in range(args.iters):
+                    ctx.compute(be, graphs[it % len(graphs)])
+                be.synchronize()
+                names.append(f"{name}@bm{bm}")
+            lib.ggml_backend_mi355x_set_tune(8, 0)
+            ctx.free()
+            continue
         if args.sweep and not name.startswith(("fa_", "rms", "ffn")):
             cfgs = [c for c in SWEEP if not (name.startswith("glu") and c[1] == 8)]
         ctx, graphs = CASES[name](pkg, be, rng)
         if args.sweep_glu8 and name.startswith("ffn"):
             for v in range(4):
-                lib.ggml_backend_mi355x_set_tune(4, v)
-                separator(pkg, be)
-                for it in range(args.iters):
-                    ctx.compute(be, graphs[it % len(graphs)])
-                be.synchronize()
-                names.append(f"{name}@glu8v{v}")
+                for mode in range(3):
+                    lib.ggml_backend_mi355x_set_tune(4, v)
+                    lib.ggml_backend_mi355x_set_tune(9, mode)
+                    separator(pkg, be)
+                    for it in range(args.iters):
+                        ctx.compute(be, graphs[it % len(graphs)])
+                    be.synchronize()
+                    names.append(f"{name}@glu8v{v}m{mode}")
             lib.ggml_backend_mi355x_set_tune(4, 0)
+            lib.ggml_backend_mi355x_set_tune(9, 0)
             ctx.free()
             continue
         if args.trace:
