@@ -162,6 +162,8 @@ static void be_free(ggml_backend_t b) {
     if (s->scratch.base) hipFree(s->scratch.base);
     if (s->act.base) hipFree(s->act.base);
     if (s->f16.base) hipFree(s->f16.base);
+    if (s->rope_tab) hipFree(s->rope_tab);
+    if (s->fa_cnt) hipFree(s->fa_cnt);
     hipStreamDestroy(s->stream);
     delete s;  // the ggml_backend struct lives inside Stream
 }
@@ -237,6 +239,9 @@ static ggml_backend_t make_backend(Device * d) {
     s->device = d->id;
     s->name = d->name;
     HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc((void **) &s->rope_tab, MX_ROPE_TAB * sizeof(float2)));   // never inside a capture
+    HIP_CHECK(hipMalloc((void **) &s->fa_cnt, MX_FA_CNT * sizeof(unsigned int)));
+    HIP_CHECK(hipMemset(s->fa_cnt, 0, MX_FA_CNT * sizeof(unsigned int)));
     s->use_graphs = !env_flag("GGML_MI355X_DISABLE_GRAPHS");
     s->use_fusion = !env_flag("GGML_MI355X_DISABLE_FUSION");
     s->backend.guid = (ggml_guid_t) kGuid;

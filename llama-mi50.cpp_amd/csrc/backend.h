@@ -76,6 +76,9 @@ struct DeferredNorm {
     ggml_tensor * mul;
 };
 
+constexpr int MX_ROPE_TAB = 512;   // RoPE dimension pairs the per-token table holds
+constexpr int MX_FA_CNT = 4096;    // decode flash-attn split counters (q rows x KV heads)
+
 struct Stream {
     int device = 0;
     std::vector<DeferredNorm> deferred;
@@ -90,6 +93,13 @@ struct Stream {
     int act_next = 0;
     size_t act_slot = 0;               // bytes per ring slot
     GraphCache gcache;
+    // RoPE cos/sin table of the current token (ops_qkv.hip): computed once per graph
+    // pass by the first fused QKV block, read by all layers' (same position, same params)
+    float * rope_tab = nullptr;        // device, float2 [MX_ROPE_TAB]
+    unsigned int * fa_cnt = nullptr;   // device, zeroed; each decode FA launch leaves it zero
+    bool rope_valid = false;
+    const void * rope_pos = nullptr, * rope_ff = nullptr;
+    int32_t rope_params[11] = {};
     bool use_graphs = true;
     bool use_fusion = true;
     std::string name;

@@ -74,9 +74,15 @@ static bool t_overlaps(const ggml_tensor * a, const ggml_tensor * b) {
 
 XStage xstage_of(Stream * s, const ggml_tensor * x) {
     for (const DeferredNorm & d : s->deferred)
-        if (x->data == d.mul->data && mx_nelements(x) == mx_nelements(d.mul) && mx_is_contiguous(x))
-            return XStage{(const float *) d.norm->src[0]->data, (const float *) d.w->data, mx_op_param<float>(d.norm, 0), 1};
+        if (x->data == d.mul->data && mx_nelements(x) == mx_nelements(d.mul) && mx_is_contiguous(x)) {
+            XStage xs{(const float *) d.norm->src[0]->data, (const float *) d.w->data, mx_op_param<float>(d.norm, 0), 1};
+            xs.dbg = g_tune[11];
+            xs.xcd = g_tune[15] != 1;
+            return xs;
+        }
     XStage xs{(const float *) x->data, nullptr, 0.0f, 0};
+    xs.dbg = g_tune[11];
+    xs.xcd = g_tune[15] != 1;
     if (const ActQ * a = act_cache_find(s, x)) {
         if (a->kp == x->ne[0]) { xs.q8 = a->q; xs.q8d = a->d; xs.q8s = a->s; }
     }
@@ -255,6 +261,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
     }
     act_cache_reset(s);
     s->deferred.clear();
+    s->rope_valid = false;
     for (int i = 0; i < g->n_nodes; ++i) {
         ggml_tensor * n = g->nodes[i];
         if (is_view_op(n->op) || mx_is_empty(n)) continue;

@@ -164,15 +164,35 @@ __device__ __forceinline__ void stage_issue(const XStage & xs, int K, const LdsA
     }
 }
 
-template <int NT, int MODE>
+// Raw workgroup barrier for LDS data: waits for this wave's LDS writes (lgkmcnt) and
+// nothing else. __syncthreads() would also drain the vector-memory counter whenever an
+// LDS-DMA is pending, i.e. wait for every weight load in flight (the whole HBM latency)
+// before the prologue could finish (cdna_hip_programming.md, pipelining across barriers).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) alone
+    __builtin_amdgcn_s_barrier();
+}
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt bits [3:0] + [15:14], expcnt and
+// lgkmcnt at their maxima)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// NW = vector-memory instructions this wave issued after its LDS-DMA (the weight loads
+// of the first batch): the DMA modes wait for the staged activation with vmcnt(NW) —
+// loads retire in issue order — and leave the weight stream in flight.
+template <int NT, int MODE, int NW = 0>
 __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const LdsAct & a, float * red, StageRegs<NT, MODE> & r) {
     constexpr int HPT = StageRegs<NT, MODE>::HPT;
     const int t = threadIdx.x, nhg = K / 16;
     if constexpr (MODE == XS_Q8) {
-        // the LDS-DMA of stage_issue lands before the barrier (vmcnt wait)
+        wait_vmcnt<NW>();                     // the LDS-DMA of stage_issue has landed
     } else if constexpr (MODE == XS_F32_LDS || MODE == XS_NORM_LDS) {
         const float * xf = (const float *) ((const char *) a.q + gemv_lds_base(K));
-        __syncthreads();                      // staged x (and norm weight) visible
+        wait_vmcnt<NW>();
+        lds_barrier();                        // staged x (and norm weight) visible
         float scale = 1.0f;
         if constexpr (MODE == XS_NORM_LDS) {
             float ss = 0.f;
@@ -182,7 +202,7 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
             }
             ss = wave_sum(ss);
             if ((t & 63) == 0) red[t >> 6] = ss;
-            __syncthreads();
+            lds_barrier();
             ss = 0.f;
 #pragma unroll
             for (int wv = 0; wv < NT / 64; ++wv) ss += red[wv];
@@ -211,7 +231,7 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
         }
         ss = wave_sum(ss);
         if ((t & 63) == 0) red[t >> 6] = ss;
-        __syncthreads();
+        lds_barrier();
         ss = 0.f;
 #pragma unroll
         for (int wv = 0; wv < NT / 64; ++wv) ss += red[wv];
@@ -234,7 +254,20 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
             q8_half(v2, hg, a);
         }
     }
-    __syncthreads();
+    lds_barrier();
+}
+
+// XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs
+// (block b -> XCD b % 8), so consecutive blocks — adjacent output rows — land on
+// different XCDs and every 128-B line of the output (and of the KV-cache rows the QKV
+// kernel stores) is written partially by several L2s, each writing back a partial
+// line at the kernel boundary. Remapped, XCD x owns one contiguous run of logical
+// blocks: its outputs are whole lines in one L2 (and its weight rows one contiguous
+// HBM range). `on` = 0 keeps the dispatch order (A/B).
+__device__ __forceinline__ int xcd_block(int b, int G, bool on) {
+    const int G8 = G & ~7;
+    if (!on || b >= G8) return b;
+    return (b & 7) * (G8 >> 3) + (b >> 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -391,6 +424,12 @@ __device__ __forceinline__ float w2_dot(const W2<QT> & r, int u, const LdsAct & 
     return 0.f;
 }
 
+// vector-memory instructions w2_load issues per unit (a lower bound is safe for
+// stage_finish's counted wait: it can only wait longer)
+template <int QT> __host__ __device__ constexpr int w2_loads() {
+    return QT == GGML_TYPE_Q4_K ? 3 : QT == GGML_TYPE_Q5_K ? 5 : QT == GGML_TYPE_Q6_K ? 5 : QT == GGML_TYPE_Q4_0 ? 2 : 3;
+}
+
 template <int QT> __host__ __device__ constexpr bool gemv2_type_ok() {
     return QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K || QT == GGML_TYPE_Q6_K || QT == GGML_TYPE_Q4_0 || QT == GGML_TYPE_Q8_0;
 }
@@ -425,27 +464,72 @@ __device__ __forceinline__ void w2_dot_batch(const W2<QT> (&r)[NM][UPL], int u0,
 // Order: activation loads (stage_issue), weight batch 0, activation quantisation into
 // LDS (stage_finish, waits only for its own loads), dot products; later batches load and
 // compute in turn (a two-deep register pipeline measured slower: it costs occupancy).
-template <int QT, int LPR, int UPL, int NM, int NT, int MODE>
-__device__ __forceinline__ void gemv_rows(const char * const (&rows)[NM], int units, int sub, const LdsAct & a,
-                                          const XStage & xs, int K, float * red, float (&acc)[NM]) {
+// The caller issues the activation loads (stage_issue) so that a kernel with several
+// block-uniform weight-type branches (QKV) issues them once, ahead of the branch: when
+// each arm began with the same activation code, SimplifyCFG hoisted it (and the
+// sum-of-squares waiting on it) above the arms, i.e. above the weight loads.
+// `fence` runs after the prologue's wait for the staged activation: kernels pass the
+// values they loaded (before stage_issue) for their epilogue — residual, KV-cache row
+// index, position — through it, pinning those loads ahead of the weight stream instead
+// of a round trip at the end (the opaque asm keeps the compiler from sinking them).
+struct NoFence { __device__ void operator()() const {} };
+template <int QT, int LPR, int UPL, int NM, int NT, int MODE, typename F = NoFence>
+__device__ __forceinline__ void gemv_rows_staged(const char * const (&rows)[NM], int units, int sub, const LdsAct & a,
+                                                 const XStage & xs, int K, float * red, StageRegs<NT, MODE> & sr, float (&acc)[NM],
+                                                 F fence = F()) {
     W2<QT> r[NM][UPL];
 #pragma unroll
     for (int m = 0; m < NM; ++m) acc[m] = 0.f;
-    StageRegs<NT, MODE> sr;
-    stage_issue<NT, MODE>(xs, K, a, sr);
-    // block-uniform trip count: stage_finish holds a barrier
+    // block-uniform trip count: stage_finish holds a barrier. Batch 0 is peeled so the
+    // prologue sits after the first weight loads in straight-line code: inside the loop
+    // (under it == 0) LICM hoisted the activation amax above the loads, making every
+    // block wait for x (an L2 round trip) before its HBM stream started.
     constexpr int STEP = LPR * UPL;
     const int n_iter = (units + STEP - 1) / STEP;
-    for (int it = 0; it < n_iter; ++it) {
-        w2_load_batch<QT, UPL, NM>(rows, it * STEP + sub, LPR, units, r);
-        if (it == 0) stage_finish<NT, MODE>(xs, K, a, red, sr);
-        w2_dot_batch<QT, UPL, NM>(r, it * STEP + sub, LPR, units, a, acc);
+    __builtin_amdgcn_sched_barrier(0);       // the DMA of stage_issue stays ahead of the weights
+    w2_load_batch<QT, UPL, NM>(rows, sub, LPR, units, r);
+    __builtin_amdgcn_sched_barrier(0);
+    // opaque redefinition of the staged activation registers: nothing computed from them
+    // can move above this point (i.e. above the weight loads), whatever the IR passes do
+    if constexpr (xs_f32reg(MODE) || xs_norm(MODE)) {
+#pragma unroll
+        for (int h = 0; h < StageRegs<NT, MODE>::HPT; ++h)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                asm volatile("" : "+v"(sr.v[h][j]));
+                if constexpr (xs_norm(MODE)) asm volatile("" : "+v"(sr.w[h][j]));
+            }
     }
-    if (n_iter == 0) stage_finish<NT, MODE>(xs, K, a, red, sr);
+    if (!(xs.dbg & 1)) stage_finish<NT, MODE, UPL * NM * w2_loads<QT>()>(xs, K, a, red, sr);
+    fence();                                  // older than the staged x: already landed
+    if (xs.dbg & 2) {                         // timing experiment: consume the loads only
+        for (int it = 0; it < n_iter; ++it) {
+            if (it) w2_load_batch<QT, UPL, NM>(rows, it * STEP + sub, LPR, units, r);
+            const int * wv = (const int *) &r[0][0];
+            int x = 0;
+#pragma unroll
+            for (int j = 0; j < (int) (sizeof(r) / 4); ++j) x ^= wv[j];
+            acc[0] += (float) x;
+        }
+    } else {
+        if (n_iter > 0) w2_dot_batch<QT, UPL, NM>(r, sub, LPR, units, a, acc);
+        for (int it = 1; it < n_iter; ++it) {
+            w2_load_batch<QT, UPL, NM>(rows, it * STEP + sub, LPR, units, r);
+            w2_dot_batch<QT, UPL, NM>(r, it * STEP + sub, LPR, units, a, acc);
+        }
+    }
     // row sum over the LPR lanes: in every lane for LPR <= 16, in the group's last lane
     // (sub == LPR - 1) for LPR = 32, 64
 #pragma unroll
     for (int m = 0; m < NM; ++m) acc[m] = dpp_sum_group<LPR>(acc[m]);
+}
+
+template <int QT, int LPR, int UPL, int NM, int NT, int MODE, typename F = NoFence>
+__device__ __forceinline__ void gemv_rows(const char * const (&rows)[NM], int units, int sub, const LdsAct & a,
+                                          const XStage & xs, int K, float * red, float (&acc)[NM], F fence = F()) {
+    StageRegs<NT, MODE> sr;
+    stage_issue<NT, MODE>(xs, K, a, sr);
+    gemv_rows_staged<QT, LPR, UPL, NM, NT, MODE>(rows, units, sub, a, xs, K, red, sr, acc, fence);
 }
 
 }  // namespace mx

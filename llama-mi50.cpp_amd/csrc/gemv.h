@@ -18,6 +18,10 @@ struct XStage {
     const int8_t * q8 = nullptr;    // q8 activation already in memory (act cache):
     const float * q8d = nullptr;    //   copied, not recomputed
     const float * q8s = nullptr;
+    int dbg = 0;                    // timing experiments only (g_tune[11]): 1 skip the
+                                    // prologue, 2 skip the dot products, 4 skip epilogue math,
+                                    // 8 skip the QKV kernel's KV-cache stores
+    int xcd = 1;                    // XCD-contiguous block order (g_tune[15] = 1 turns it off)
 };
 
 extern int g_tune[16];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)

@@ -509,13 +509,20 @@ static int64_t fa_chunk(const ggml_tensor * dst, int64_t * nsplit_out) {
     return chunk;
 }
 
+bool fa_dec2_ok(const ggml_tensor * dst);
+size_t fa_dec2_scratch(const ggml_tensor * dst);
+void fa_dec2_run(OpCtx & c, ggml_tensor * dst);
+static bool g_fa_dec1 = getenv("GGML_MI355X_FA_DEC1") != nullptr;   // A/B: the v1 decode kernel
+
 size_t flash_attn_scratch(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * v = dst->src[2];
     int64_t nsplit;
     fa_chunk(dst, &nsplit);
     const int64_t rows = q->ne[1] * q->ne[2] * q->ne[3];
-    return nsplit * rows * (v->ne[0] + 2) * sizeof(float) + 4 * 256;
+    size_t need = nsplit * rows * (v->ne[0] + 2) * sizeof(float) + 4 * 256;
+    if (fa_dec2_ok(dst)) need = std::max(need, fa_dec2_scratch(dst));
+    return need;
 }
 
 bool flash_attn_supported(const ggml_tensor * dst) {
@@ -558,6 +565,7 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst);
 static bool g_fa_mma_off = getenv("GGML_MI355X_FA_TILE") != nullptr;
 
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
+    if (!g_fa_dec1 && g_tune[10] != 1 && fa_dec2_ok(dst)) { fa_dec2_run(c, dst); return; }
     if (!g_fa_mma_off && !fa_use_dec(dst) && fa_mma_ok(dst)) { fa_mma_run(c, dst); return; }
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * k = dst->src[1];

@@ -1,0 +1,314 @@
+// ops_fattn_dec.hip — single-token FLASH_ATTN_EXT (decode) on gfx950, v2.
+//
+// Semantics: ggml_compute_forward_flash_attn_ext_f16_one_chunk (ggml-cpu/ops.cpp:
+// 8045-8260): q rounded to f16 (the K vec-dot type), s = (q·k)·scale + mask, keys whose
+// mask is −inf skipped, softmax over keys, O = Σ p·V. Reference GPU: fattn-vec.cuh:21 +
+// the split-KV combine fattn-common.cuh:730-782.
+//
+// Why v2: the first decode kernel gave each lane one key and had it read that key's
+// whole 256-B K row (16 loads, 2 KB apart between lanes): every wave instruction
+// touched 64 cache lines, and at llama-bench tg128's 256-key cache the kernel spent
+// ~5 of its 8.5 µs in the vector-memory pipe of the 32 CUs it ran on.
+// v2 (MI355X-first):
+//  * D/8 lanes share one key row (16 B each, 8 f16 dims): a wave instruction reads
+//    64/(D/8) whole rows — coalesced; q·k partials reduce over the row's lanes by DPP;
+//  * one workgroup = one KV head x all G query heads of its GQA group (K/V read once)
+//    x a split of 64/128-key chunks (online softmax over its chunks), at most 16 splits,
+//    so a short cache still spreads over Hkv x nsplit CUs;
+//  * every load (q, K, V, mask) is issued before any arithmetic: one memory round trip;
+//  * splits merge in the same launch: each workgroup publishes (O, max, sum) and the
+//    last one to arrive (device-scope counter, reset by it for the next launch / graph
+//    replay) combines them — no second kernel, no second launch gap.
+#include "backend.h"
+
+namespace mx { extern int g_tune[16]; }
+
+namespace mx {
+
+struct FaDecArgs {
+    const char * q; size_t q1, q2, q3;
+    const char * k; size_t k1, k2, k3;
+    const char * v; size_t v1, v2, v3;
+    const char * mask; size_t m1, m3; int mne3;
+    char * dst; size_t d1, d2, d3;
+    float * part;                  // [rows][nsplit][G*(D+2)] partials (scratch)
+    unsigned int * cnt;            // per (q row, seq, KV head) arrival counters, zero between launches
+    int n_q, n_kv, H, Hkv, ns_kv, nsplit;
+    float scale;
+};
+
+constexpr int FD_NI = 4;          // key-row load instructions per wave per chunk
+constexpr int FD_MAXSPLIT = 16;   // workgroups per (q row, KV head); longer caches loop over chunks
+
+// G = query heads per workgroup (a divisor of the GQA ratio Gt; K/V are read once per
+// workgroup), NW = waves per workgroup (the chunk is NW x 16/32 keys)
+template <int D, int G, int NW>
+__global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
+    constexpr int NT = 64 * NW;
+    constexpr int LPK = D / 8;            // lanes per key row
+    constexpr int KPI = 64 / LPK;         // keys per wave instruction
+    constexpr int KPW = FD_NI * KPI;      // keys per wave per chunk
+    constexpr int CS = NW * KPW;          // keys per chunk (workgroup)
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    __shared__ float wm[NW][G], wl[NW][G];
+    __shared__ __align__(16) float wo[NW][G][D];
+    __shared__ float sM[G][FD_MAXSPLIT], sF[G][FD_MAXSPLIT], sL[G];
+    __shared__ int s_last;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c = lane % LPK, kq = lane / LPK;
+    const int Gt = p.H / p.Hkv, NGB = Gt / G;
+    const int hk = blockIdx.x % p.Hkv;
+    const int gb = (blockIdx.x / p.Hkv) % NGB;
+    const int iq1 = (blockIdx.x / (p.Hkv * NGB)) % p.n_q;
+    const int iq3 = blockIdx.x / (p.Hkv * NGB * p.n_q);
+    const int split = blockIdx.y;
+    const int hb = hk * Gt + gb * G;                         // first query head
+    const int hslot = hk * NGB + gb;                         // partial / counter slot
+    const char * kb = p.k + (size_t) hk * p.k2 + (size_t) (iq3 % p.ns_kv) * p.k3 + c * 16;
+    const char * vb = p.v + (size_t) hk * p.v2 + (size_t) (iq3 % p.ns_kv) * p.v3 + c * 16;
+    const uint16_t * mrow = (const uint16_t *) (p.mask ? p.mask + (size_t) iq1 * p.m1 + (size_t) (iq3 % p.mne3) * p.m3 : p.k);
+    const int nch = (p.n_kv + CS - 1) / CS, cpb = (nch + p.nsplit - 1) / p.nsplit;
+
+    // q first (it is consumed first): the CPU vec-dot rounds q to the K type (f16)
+    h2v qh[G][4];
+    {
+        float4 qa[G], qb[G];
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const float * qp = (const float *) (p.q + (size_t) iq1 * p.q1 + (size_t) (hb + h) * p.q2 + (size_t) iq3 * p.q3) + 8 * c;
+            qa[h] = *(const float4 *) qp;
+            qb[h] = *(const float4 *) (qp + 4);
+        }
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            qh[h][0] = h2v{(_Float16) qa[h].x, (_Float16) qa[h].y}; qh[h][1] = h2v{(_Float16) qa[h].z, (_Float16) qa[h].w};
+            qh[h][2] = h2v{(_Float16) qb[h].x, (_Float16) qb[h].y}; qh[h][3] = h2v{(_Float16) qb[h].z, (_Float16) qb[h].w};
+        }
+    }
+    // running (max, sum, O) of this wave; O not yet reduced over the wave's key rows
+    float M[G], L[G], o[G][8];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        M[h] = -INFINITY; L[h] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[h][i] = 0.f;
+    }
+    for (int ci = 0; ci < cpb; ++ci) {
+        const int ch = split * cpb + ci;
+        if (ch >= nch) break;                                 // workgroup-uniform
+        const int key0 = ch * CS + wave * KPW + kq;
+        // every load of the chunk first, unconditional (clamped: a load under a branch
+        // costs a wait at the join): mask, K rows, V rows — coalesced, LPK lanes per row
+        uint16_t mraw[FD_NI];
+        uint4 kr[FD_NI], vr[FD_NI];
+#pragma unroll
+        for (int t = 0; t < FD_NI; ++t) mraw[t] = mrow[min(key0 + t * KPI, p.n_kv - 1)];
+#pragma unroll
+        for (int t = 0; t < FD_NI; ++t) kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
+#pragma unroll
+        for (int t = 0; t < FD_NI; ++t) vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
+        __builtin_amdgcn_sched_barrier(0);
+        float mk[FD_NI];
+#pragma unroll
+        for (int t = 0; t < FD_NI; ++t) mk[t] = key0 + t * KPI < p.n_kv ? (p.mask ? h2f(mraw[t]) : 0.f) : -INFINITY;
+        // scores: q·k over the row's LPK lanes (DPP), one per (head, key) in every lane of the row
+        float s[G][FD_NI];
+#pragma unroll
+        for (int t = 0; t < FD_NI; ++t) {
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                float acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[h][0], 0.f, false);
+                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[h][1], acc, false);
+                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[h][2], acc, false);
+                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[h][3], acc, false);
+                acc = dpp_sum_group<LPK>(acc);
+                s[h][t] = mk[t] == -INFINITY ? -INFINITY : acc * p.scale + mk[t];
+            }
+        }
+        // online softmax (the wave's keys of this chunk: xor over the key rows kq)
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            float mc = s[h][0];
+#pragma unroll
+            for (int t = 1; t < FD_NI; ++t) mc = fmaxf(mc, s[h][t]);
+#pragma unroll
+            for (int off = LPK; off < 64; off <<= 1) mc = fmaxf(mc, __shfl_xor(mc, off, 64));
+            const float Mn = fmaxf(M[h], mc);
+            const float a = M[h] == -INFINITY ? 0.f : expf(M[h] - Mn);
+            float pr[FD_NI], lc = 0.f;
+#pragma unroll
+            for (int t = 0; t < FD_NI; ++t) { pr[t] = Mn == -INFINITY ? 0.f : expf(s[h][t] - Mn); lc += pr[t]; }
+#pragma unroll
+            for (int off = LPK; off < 64; off <<= 1) lc += __shfl_xor(lc, off, 64);
+            L[h] = L[h] * a + lc;
+            M[h] = Mn;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[h][i] *= a;
+#pragma unroll
+            for (int t = 0; t < FD_NI; ++t) {
+                const uint32_t vw[4] = {vr[t].x, vr[t].y, vr[t].z, vr[t].w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    o[h][2 * i] += pr[t] * h2f((uint16_t) (vw[i] & 0xFFFF));
+                    o[h][2 * i + 1] += pr[t] * h2f((uint16_t) (vw[i] >> 16));
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int off = LPK; off < 64; off <<= 1) o[h][i] += __shfl_xor(o[h][i], off, 64);
+        if (lane == 0) { wm[wave][h] = M[h]; wl[wave][h] = L[h]; }
+        if (kq == 0) {
+            *(float4 *) &wo[wave][h][8 * c] = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
+            *(float4 *) &wo[wave][h][8 * c + 4] = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
+        }
+    }
+    __syncthreads();
+
+    // ---- merge the four waves: (O, M, L) of this split for the G heads
+    constexpr int PW = G * (D + 2);                          // partial floats per workgroup
+    const int slots = p.Hkv * NGB;
+    float * part = p.part + ((size_t) ((iq3 * p.n_q + iq1) * slots + hslot) * p.nsplit + split) * PW;
+    for (int i = tid; i < G * D; i += NT) {
+        const int h = i / D, d = i % D;
+        float Mw = wm[0][h];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) Mw = fmaxf(Mw, wm[w][h]);
+        float Lw = 0.f, O = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const float f = wm[w][h] == -INFINITY ? 0.f : expf(wm[w][h] - Mw);
+            Lw += wl[w][h] * f;
+            O += wo[w][h][d] * f;
+        }
+        if (p.nsplit == 1) {
+            float * out = (float *) (p.dst + (size_t) (hb + h) * p.d1 + (size_t) iq1 * p.d2 + (size_t) iq3 * p.d3);
+            out[d] = Lw == 0.f ? 0.f : O / Lw;
+        } else {
+            // agent-scope (write-through) stores: visible to every XCD once completed,
+            // without the L2 writeback a __threadfence() release does
+            __hip_atomic_store(part + h * (D + 2) + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d == 0) {
+                __hip_atomic_store(part + h * (D + 2) + D, Mw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(part + h * (D + 2) + D + 1, Lw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (p.nsplit == 1) return;
+
+    // ---- split merge by the last workgroup of this (q row, KV head) to arrive
+    __builtin_amdgcn_s_waitcnt(0);           // this thread's partial stores have completed
+    __syncthreads();                         // ... and every thread's
+    unsigned int * cnt = p.cnt + (iq3 * p.n_q + iq1) * slots + hslot;
+    if (tid == 0) s_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) (p.nsplit - 1);
+    __syncthreads();
+    if (!s_last) return;
+    const float * pb = p.part + (size_t) ((iq3 * p.n_q + iq1) * slots + hslot) * p.nsplit * PW;
+    auto ld = [](const float * a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // (max, sum) of every split in one parallel round trip, then per-split weights
+    for (int i = tid; i < G * p.nsplit; i += NT) {
+        const int h = i / p.nsplit, sp = i % p.nsplit;
+        sM[h][sp] = ld(pb + (size_t) sp * PW + h * (D + 2) + D);
+        sF[h][sp] = ld(pb + (size_t) sp * PW + h * (D + 2) + D + 1);
+    }
+    __syncthreads();
+    if (tid < G) {
+        float Mx = -INFINITY, Ls = 0.f;
+        for (int sp = 0; sp < p.nsplit; ++sp) Mx = fmaxf(Mx, sM[tid][sp]);
+        for (int sp = 0; sp < p.nsplit; ++sp) {
+            const float f = sM[tid][sp] == -INFINITY ? 0.f : expf(sM[tid][sp] - Mx);
+            Ls += sF[tid][sp] * f;
+            sM[tid][sp] = f;                 // now the weight of split sp
+        }
+        sL[tid] = Ls;
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += NT) {
+        const int h = i / D, d = i % D;
+        float ov[FD_MAXSPLIT];
+#pragma unroll
+        for (int sp = 0; sp < FD_MAXSPLIT; ++sp)            // all loads in flight at once
+            ov[sp] = sp < p.nsplit ? ld(pb + (size_t) sp * PW + h * (D + 2) + d) : 0.f;
+        float O = 0.f;
+#pragma unroll
+        for (int sp = 0; sp < FD_MAXSPLIT; ++sp) if (sp < p.nsplit) O += sM[h][sp] * ov[sp];
+        float * out = (float *) (p.dst + (size_t) (hb + h) * p.d1 + (size_t) iq1 * p.d2 + (size_t) iq3 * p.d3);
+        out[d] = sL[h] == 0.f ? 0.f : O / sL[h];
+    }
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch / replay
+}
+
+// eligibility: f16 K/V, D 64/128, GQA ratio 1-8, a plain f16 mask broadcast over heads,
+// no softcap / ALiBi / sinks, few query rows (decode)
+bool fa_dec2_ok(const ggml_tensor * dst) {
+    const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
+    if (q->ne[1] > 4 || k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16) return false;
+    const int64_t D = k->ne[0];
+    if ((D != 64 && D != 128) || v->ne[0] != D) return false;
+    const int64_t G = q->ne[2] / k->ne[2];
+    if (q->ne[2] % k->ne[2] || (G != 1 && G != 2 && G != 4 && G != 8)) return false;
+    if (dst->src[4]) return false;                                        // sinks
+    if (mx_op_param<float>(dst, 1) != 0.0f || mx_op_param<float>(dst, 2) != 0.0f) return false;   // ALiBi, softcap
+    if (m && (m->type != GGML_TYPE_F16 || m->ne[2] > 1)) return false;
+    if (k->nb[1] % 16 || v->nb[1] % 16 || k->nb[2] % 16 || v->nb[2] % 16 || (uintptr_t) k->data % 16 || (uintptr_t) v->data % 16) return false;
+    if (q->nb[1] % 16 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return false;
+    if (q->ne[3] != k->ne[3] && k->ne[3] != 1) return false;
+    if (k->ne[1] > INT32_MAX / 2 || q->ne[1] * q->ne[3] * q->ne[2] > MX_FA_CNT) return false;
+    // longer caches: the split-merging geometry measured slower than the v1 kernel +
+    // combine (fa_1024 12.3 vs 12.6 us, fa_4096 17.5 vs 16.3, opbench on MI355X), so only
+    // the single-split geometry is used unless g_tune[10] = 3 forces the split one
+    if (g_tune[10] != 3 && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;
+    return true;
+}
+
+// launch geometry: a cache that one 16-wave chunk covers (<= 256 keys at D 128, llama-
+// bench tg128) runs as one split with ONE query head per workgroup (Hkv x Gt workgroups,
+// K/V re-read from L2 by the GQA group): no split merge, whose publish / count / gather
+// round trips cost ~4 us; longer caches use 4-wave workgroups over the whole GQA group
+// and up to 16 splits merged in the same launch.
+struct FdCfg { int G, NW, nsplit; };
+static FdCfg fd_cfg(int D, int Gt, int64_t n_kv) {
+    const int cs16 = 16 * FD_NI * (64 / (D / 8)), cs4 = 4 * FD_NI * (64 / (D / 8));
+    if (g_tune[10] == 2 || (g_tune[10] != 3 && n_kv <= cs16)) return {1, 16, (int) mx_ceil_div(n_kv, cs16)};
+    return {Gt, 4, (int) std::min<int64_t>(FD_MAXSPLIT, mx_ceil_div(n_kv, cs4))};
+}
+
+size_t fa_dec2_scratch(const ggml_tensor * dst) {
+    const ggml_tensor * q = dst->src[0], * k = dst->src[1];
+    const int64_t D = k->ne[0];
+    const FdCfg f = fd_cfg((int) D, (int) (q->ne[2] / k->ne[2]), k->ne[1]);
+    return (size_t) (q->ne[1] * q->ne[3] * q->ne[2]) * std::min(f.nsplit, FD_MAXSPLIT) * (D + 2) * sizeof(float) + 256;
+}
+
+void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
+    FaDecArgs a{};
+    a.q = (const char *) q->data; a.q1 = q->nb[1]; a.q2 = q->nb[2]; a.q3 = q->nb[3];
+    a.k = (const char *) k->data; a.k1 = k->nb[1]; a.k2 = k->nb[2]; a.k3 = k->nb[3];
+    a.v = (const char *) v->data; a.v1 = v->nb[1]; a.v2 = v->nb[2]; a.v3 = v->nb[3];
+    if (m) { a.mask = (const char *) m->data; a.m1 = m->nb[1]; a.m3 = m->nb[3]; a.mne3 = (int) m->ne[3]; }
+    else a.mne3 = 1;
+    a.dst = (char *) dst->data; a.d1 = dst->nb[1]; a.d2 = dst->nb[2]; a.d3 = dst->nb[3];
+    a.n_q = (int) q->ne[1]; a.n_kv = (int) k->ne[1]; a.H = (int) q->ne[2]; a.Hkv = (int) k->ne[2];
+    a.ns_kv = (int) k->ne[3];
+    a.scale = mx_op_param<float>(dst, 0);
+    const int D = (int) k->ne[0], Gt = a.H / a.Hkv;
+    const FdCfg f = fd_cfg(D, Gt, a.n_kv);
+    MX_ASSERT(f.nsplit <= FD_MAXSPLIT);
+    a.nsplit = f.nsplit;
+    a.part = (float *) c.scratch->take(fa_dec2_scratch(dst));
+    a.cnt = c.s->fa_cnt;
+    const dim3 grid((unsigned) (a.Hkv * (Gt / f.G) * a.n_q * q->ne[3]), (unsigned) a.nsplit);
+#define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { k_fattn_dec2<DD, GG, NWW><<<grid, 64 * NWW, 0, c.st>>>(a); return; }
+    FD(128, 1, 16) FD(64, 1, 16)
+    FD(128, 4, 4) FD(128, 1, 4) FD(128, 2, 4) FD(128, 8, 4) FD(64, 1, 4) FD(64, 2, 4) FD(64, 4, 4) FD(64, 8, 4)
+#undef FD
+    MX_ABORT("fattn dec2 D=%d G=%d NW=%d", D, f.G, f.NW);
+}
+
+}  // namespace mx

@@ -31,7 +31,8 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane % LPR;
-    const int row = (blockIdx.x * W + wave) * RPW + lane / LPR;
+    const int blk = xcd_block((int) blockIdx.x, (int) gridDim.x, p.xs.xcd);
+    const int row = (blk * W + wave) * RPW + lane / LPR;
     const bool valid = row < p.nrows;
     const int64_t rr = valid ? row : p.nrows - 1;
     const char * rows[NM];
@@ -43,11 +44,16 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     unsigned long long * tr = blockIdx.x == 0 ? p.trace : nullptr;
     MX_TRACE(tr, 0);
     MX_TRACE_BLK(p.trace_blk, 0);
-    gemv_rows<QT, LPR, UPL, NM, 64 * W, MODE>(rows, p.units, sub, a, p.xs, p.K, red, acc);
+    // residual prefetched with the activation: a load issued after the dot products
+    // would add a memory round trip to every workgroup's tail
+    float res = 0.f;
+    if constexpr (EPI == 2) res = p.res[rr];
+    gemv_rows<QT, LPR, UPL, NM, 64 * W, MODE>(rows, p.units, sub, a, p.xs, p.K, red, acc,
+                                              [&] { if constexpr (EPI == 2) asm volatile("" : "+v"(res)); });
     MX_TRACE(tr, 3);
     float v = acc[0];
     if constexpr (EPI == 1) v = (v / (1.0f + expf(-v))) * acc[1];
-    if constexpr (EPI == 2) v += valid ? p.res[row] : 0.f;
+    if constexpr (EPI == 2) v += res;
     if (sub == LPR - 1 && valid) p.dst[row] = v;
     MX_TRACE(tr, 4);
     MX_TRACE_BLK(p.trace_blk, 1);
@@ -55,7 +61,7 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     if constexpr (RPB % 32 == 0 && RPB / 32 <= W) {
         if (p.q8o) {     // block-uniform: the q8 form of this block's RPB outputs, one wave per 32
             __shared__ float orow[RPB];
-            if (sub == LPR - 1) orow[row - blockIdx.x * RPB] = v;
+            if (sub == LPR - 1) orow[row - blk * RPB] = v;
             __syncthreads();
             if (wave < RPB / 32 && lane < 32) {
                 const float x = orow[32 * wave + lane];
@@ -64,9 +70,9 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
                 const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
                 const int qi = (int) roundf(x * id);
                 const int sum = __builtin_amdgcn_readlane(dpp_sum_group_i<32>(qi), 31);
-                const int blk = blockIdx.x * (RPB / 32) + wave;
-                p.q8o[blk * 32 + lane] = (int8_t) qi;
-                if (lane == 0) { p.q8od[blk] = dd; p.q8os[blk] = dd * (float) sum; }
+                const int qb = blk * (RPB / 32) + wave;
+                p.q8o[qb * 32 + lane] = (int8_t) qi;
+                if (lane == 0) { p.q8od[qb] = dd; p.q8os[qb] = dd * (float) sum; }
             }
         }
     }
@@ -105,6 +111,7 @@ static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
         CFG(16, 2) CFG(16, 4) CFG(32, 2) CFG(32, 4) CFG(64, 2) CFG(64, 4)
 #undef CFG
     }
+
     constexpr int U = EPI == 1 ? 2 : 4;
     (void) upl;
     if (lpr == 16) return launch_cfg<QT, 16, U, EPI>(st, p);
@@ -115,6 +122,7 @@ static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
 static int units_of(int type, int64_t K) {
     return (int) (K / ((type == GGML_TYPE_Q4_0 || type == GGML_TYPE_Q8_0) ? 32 : 64));
 }
+
 
 // launch geometry: defaults from the tools/opbench.py sweep on MI355X (profiles/r01/
 // opbench_sweep.txt); g_tune overrides for sweeps

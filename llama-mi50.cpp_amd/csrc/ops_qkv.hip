@@ -25,6 +25,7 @@ struct QkvArgs {
     char * kc; size_t kc_nb1; const char * kidx; int kidx64;
     char * vc; size_t vc_nb1; const char * vidx; int vidx64; int v_trans;
     const int32_t * pos; const float * ff;
+    const float2 * tab;            // RoPE (cos, sin) per dimension pair, k_rope_table
     int n_dims;
     float theta_scale, freq_scale, ext_factor, attn_factor, corr0, corr1;
     unsigned long long * trace;    // debug (MX_TRACE), workgroup 0
@@ -39,11 +40,15 @@ __device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i)
 template <int QTA, int QTV, int MODE>
 __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     extern __shared__ __align__(16) char smem[];
-    constexpr int LPR = 16, UPL = 4;
+    constexpr int LPR = 16, UPLA = 4, UPLV = 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & 15;
-    const int b = blockIdx.x;
-    const int m = b < p.nblk_q ? 0 : (b < p.nblk_q + p.nblk_k ? 1 : 2);
+    // XCD-contiguous order within each matrix's block range (gemv.cuh xcd_block): every
+    // 128-B line of q_out and of the K/V cache rows is then written by one XCD's L2
+    const int m = (int) blockIdx.x < p.nblk_q ? 0 : ((int) blockIdx.x < p.nblk_q + p.nblk_k ? 1 : 2);
+    const int base = m == 0 ? 0 : (m == 1 ? p.nblk_q : p.nblk_q + p.nblk_k);
+    const int nb = m == 0 ? p.nblk_q : (m == 1 ? p.nblk_k : (int) gridDim.x - p.nblk_q - p.nblk_k);
+    const int b = base + ((base & 7) == 0 ? xcd_block((int) blockIdx.x - base, nb, p.xs.xcd) : (int) blockIdx.x - base);
     const int bl = m == 0 ? b : (m == 1 ? b - p.nblk_q : b - p.nblk_q - p.nblk_k);
     const int row = bl * 16 + wave * 4 + (lane >> 4);
     const bool valid = row < p.rows[m];
@@ -54,40 +59,61 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     unsigned long long * tr = blockIdx.x == 0 ? p.trace : nullptr;
     MX_TRACE(tr, 0);
     MX_TRACE_BLK(p.trace_blk, 0);
-    if (m == 2) gemv_rows<QTV, LPR, UPL, 1, 256, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, acc);   // block-uniform branch
-    else gemv_rows<QTA, LPR, UPL, 1, 256, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, acc);
+    // epilogue operands (position, KV-cache row) prefetched ahead of the weight stream:
+    // loaded in the epilogue they were two dependent round trips after the dot products
+    int pos = p.pos[0];
+    // (I64 indices only, see fuse_qkv_rope_store: one branch-free load)
+    int64_t kvrow = ((const int64_t *) (m == 2 ? p.vidx : p.kidx))[m == 2 && p.v_trans ? (valid ? row : 0) : 0];
+    const int d = row % p.n_dims;
+    const bool odd = d & 1;
+    const int i0 = d & ~1;
+    // RoPE cos/sin of this row's dimension pair from the per-token table (k_rope_table):
+    // computed per lane (theta loop + libm sincos) it cost ~2 us per launch
+    float2 csn = p.tab[i0 / 2];
+    auto fence = [&] { asm volatile("" : "+v"(pos)); asm volatile("" : "+v"(kvrow)); asm volatile("" : "+v"(csn.x)); asm volatile("" : "+v"(csn.y)); };
+    StageRegs<256, MODE> sr;
+    stage_issue<256, MODE>(p.xs, p.K, a, sr);
+    if (m == 2) gemv_rows_staged<QTV, LPR, UPLV, 1, 256, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, sr, acc, fence);   // block-uniform branch
+    else gemv_rows_staged<QTA, LPR, UPLA, 1, 256, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, sr, acc, fence);
     MX_TRACE(tr, 3);
     MX_TRACE_BLK(p.trace_blk, 1);
     const float v = acc[0];
     const float pv = __shfl_xor(v, 16, 64);
     if (sub != 0 || !valid) return;
+    if (p.xs.dbg & 4) { if (m == 0) p.q_out[row] = v; return; }
+    if ((p.xs.dbg & 8) && m > 0) return;
     if (m == 2) {
         const uint16_t h = f2h(v);
-        if (p.v_trans) *(uint16_t *) (p.vc + read_idx(p.vidx, p.vidx64, row) * p.vc_nb1) = h;
-        else *(uint16_t *) (p.vc + read_idx(p.vidx, p.vidx64, 0) * p.vc_nb1 + row * 2) = h;
+        if (p.v_trans) *(uint16_t *) (p.vc + kvrow * p.vc_nb1) = h;
+        else *(uint16_t *) (p.vc + kvrow * p.vc_nb1 + row * 2) = h;
         return;
     }
-    const int d = row % p.n_dims;
-    const bool odd = d & 1;
-    const int i0 = d & ~1;
+    const float cs = csn.x, sn = csn.y;
+    const float x0 = odd ? pv : v, x1 = odd ? v : pv;
+    const float r = odd ? x0 * sn + x1 * cs : x0 * cs - x1 * sn;
+    if (m == 0) p.q_out[row] = r;
+    else *(uint16_t *) (p.kc + kvrow * p.kc_nb1 + row * 2) = f2h(r);
+    MX_TRACE(tr, 4);
+}
+
+// (cos θ·m, sin θ·m) for every dimension pair of one position: rope_yarn
+// (ggml-cpu/ops.cpp:5529-5546) with theta by repeated multiplication as rope_cache_init
+// (ops.cpp:5548-5566) — the per-pair values of op_rope, computed once per token.
+__global__ void k_rope_table(QkvArgs p, float2 * tab) {
+    const int i = threadIdx.x + blockIdx.x * blockDim.x;   // pair index
+    if (i >= p.n_dims / 2) return;
     float theta = (float) p.pos[0];
-    for (int k = 0; k < i0 / 2; ++k) theta *= p.theta_scale;
-    if (p.ff) theta /= p.ff[i0 / 2];
-    // rope_yarn (ops.cpp:5529-5546)
+    for (int k = 0; k < i; ++k) theta *= p.theta_scale;
+    if (p.ff) theta /= p.ff[i];
     const float ti = p.freq_scale * theta;
     float th = ti, ms = p.attn_factor;
     if (p.ext_factor != 0.0f) {
-        const float y = (i0 / 2 - p.corr0) / fmaxf(0.001f, p.corr1 - p.corr0);
+        const float y = (i - p.corr0) / fmaxf(0.001f, p.corr1 - p.corr0);
         const float mix = (1.0f - fminf(1.0f, fmaxf(0.0f, y))) * p.ext_factor;
         th = ti * (1 - mix) + theta * mix;
         ms *= 1.0f + 0.1f * logf(1.0f / p.freq_scale);
     }
-    const float cs = cosf(th) * ms, sn = sinf(th) * ms;
-    const float x0 = odd ? pv : v, x1 = odd ? v : pv;
-    const float r = odd ? x0 * sn + x1 * cs : x0 * cs - x1 * sn;
-    if (m == 0) p.q_out[row] = r;
-    else *(uint16_t *) (p.kc + read_idx(p.kidx, p.kidx64, 0) * p.kc_nb1 + row * 2) = f2h(r);
-    MX_TRACE(tr, 4);
+    tab[i] = make_float2(cosf(th) * ms, sinf(th) * ms);
 }
 
 static const ggml_tensor * base_of(const ggml_tensor * t) {
@@ -146,7 +172,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     }
     if (memcmp(rq->op_params, rk->op_params, 11 * sizeof(int32_t)) != 0 || rq->src[1] != rk->src[1] || rq->src[2] != rk->src[2]) return 0;
     const int n_dims = mx_op_param<int32_t>(rq, 1);
-    if (n_dims != rq->ne[0] || n_dims % 2 || (rq->src[2] && rq->src[2]->type != GGML_TYPE_F32)) return 0;
+    if (n_dims != rq->ne[0] || n_dims % 2 || n_dims > 2 * MX_ROPE_TAB || (rq->src[2] && rq->src[2]->type != GGML_TYPE_F32)) return 0;
     // only the fused consumers may read the intermediate results
     if ((mq->flags | mk->flags | mv->flags | rk->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
     if (uses(mq) != 1 || uses(mk) != 1 || uses(mv) != 1 || uses(rk) != 1) return 0;
@@ -159,7 +185,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     if (sv->src[0]->ne[0] == wv->ne[1] && sv->src[0]->ne[1] == 1 && vix->ne[0] == 1 && sv->nb[0] == 2) v_trans = 0;
     else if (sv->src[0]->ne[0] == 1 && sv->src[0]->ne[1] == wv->ne[1] && vix->ne[0] == wv->ne[1] && sv->ne[0] == 1) v_trans = 1;
     else return 0;
-    for (const ggml_tensor * ix : {kix, vix}) if (ix->type != GGML_TYPE_I64 && ix->type != GGML_TYPE_I32) return 0;
+    for (const ggml_tensor * ix : {kix, vix}) if (ix->type != GGML_TYPE_I64) return 0;   // llama's KV indices
 
     QkvArgs p{};
     const ggml_tensor * ws[3] = {wq, wk, wv};
@@ -201,11 +227,20 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     if (mode != XS_NORM) {   // the fused block normally follows attn_norm; other sources
 #define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8> : \
         mode == XS_NORM_H2 ? k_qkv_rope_store<TA, TV, XS_NORM_H2> : k_qkv_rope_store<TA, TV, XS_F32_H2>;
-        QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
+            QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
         QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
         QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
 #undef QKV
     }
+    // the per-token RoPE table: once per graph pass for a (position, params, factors) key
+    Stream * S = c.s;
+    if (!S->rope_valid || S->rope_pos != (const void *) p.pos || S->rope_ff != (const void *) p.ff ||
+        memcmp(S->rope_params, rq->op_params, sizeof(S->rope_params)) != 0) {
+        k_rope_table<<<(n_dims / 2 + 63) / 64, 64, 0, c.st>>>(p, (float2 *) S->rope_tab);
+        S->rope_valid = true; S->rope_pos = p.pos; S->rope_ff = p.ff;
+        memcpy(S->rope_params, rq->op_params, sizeof(S->rope_params));
+    }
+    p.tab = (const float2 *) S->rope_tab;
     for (int j = i; j <= last; ++j) act_cache_invalidate(c.s, g->nodes[j]);
     const dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
     hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K, mode), c.st, p);

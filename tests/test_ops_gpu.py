@@ -172,7 +172,11 @@ def test_fused_gate_up_swiglu(pkg, backend, orc, tname):
 
 @pytest.mark.parametrize("n_q,n_kv,H,Hkv,D", [(1, 256, 32, 8, 128), (1, 700, 8, 8, 128), (5, 512, 8, 2, 128),
                                                (64, 300, 4, 4, 128), (100, 333, 8, 2, 128), (130, 130, 4, 1, 64),
-                                               (1, 4096, 8, 2, 128), (3, 1000, 4, 2, 64)])
+                                               (1, 4096, 8, 2, 128), (3, 1000, 4, 2, 64),
+                                               # decode kernel v2 (ops_fattn_dec.hip): one split (direct
+                                               # store), ragged last split, GQA 8, D 64 with 2 query rows
+                                               (1, 64, 8, 8, 128), (1, 100, 32, 4, 128), (2, 65, 16, 2, 64),
+                                               (4, 1500, 32, 8, 128)])
 def test_flash_attn(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
     rng = np.random.default_rng(n_q * 1000 + n_kv)
     q = rng.standard_normal((H, n_q, D)).astype(np.float32)
@@ -194,6 +198,21 @@ def test_flash_attn(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
     y = run(pkg, backend, build)[0].reshape(n_q, H, D)
     ref = orc.flash_attn(q, k, v, m16, scale)
     assert nmse(y, ref) < 5e-4
+    if n_q <= 4:
+        # the split merge's arrival counters must be back at zero for the next launch
+        y2 = run(pkg, backend, build)[0].reshape(n_q, H, D)
+        assert np.array_equal(y, y2)
+
+
+@pytest.mark.parametrize("n_q,n_kv,H,Hkv,D", [(1, 1500, 32, 8, 128), (2, 700, 8, 2, 64), (1, 300, 8, 8, 128)])
+def test_flash_attn_split_merge(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
+    """decode FA v2's in-launch split merge (ops_fattn_dec.hip), forced with g_tune[10] = 3"""
+    lib = pkg._lib.load()
+    lib.ggml_backend_mi355x_set_tune(10, 3)
+    try:
+        test_flash_attn(pkg, backend, orc, n_q, n_kv, H, Hkv, D)
+    finally:
+        lib.ggml_backend_mi355x_set_tune(10, 0)
 
 
 def test_mul_mat_id(pkg, backend, orc):

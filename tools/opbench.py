@@ -229,6 +229,11 @@ def main():
     ap.add_argument("--trace-blocks", action="store_true", help="GEMV cases: per-workgroup start/end spread")
     ap.add_argument("--sweep-mm", action="store_true", help="pp_* cases under both GEMM row tiles (64, 128)")
     ap.add_argument("--sweep-glu8", action="store_true", help="ffn cases under every q8-emitting SwiGLU geometry")
+    ap.add_argument("--sweep3", action="store_true", help="GEMV v3 cases under every geometry id x workgroups per CU")
+    ap.add_argument("--bpc", nargs="*", type=int, default=[1, 2, 4], help="--sweep3 workgroups per CU")
+    ap.add_argument("--ab", nargs="*", default=None, help="repeat each case under these tune settings, e.g. 14=0 14=1,11=2")
+    ap.add_argument("--dbg", nargs="*", type=int, default=None,
+                    help="timing experiments: repeat each case under these GEMV dbg masks (1 no prologue, 2 no dots, 4 no epilogue math)")
     args = ap.parse_args()
     pkg = load_package()
     lib = pkg._lib.load()
@@ -300,6 +305,45 @@ def main():
                 print(f"blocks {name}: n={len(a)} start[p50,p90,max]={np.percentile(st,50):.0f},{np.percentile(st,90):.0f},{st.max():.0f}ns "
                       f"end[min,p50,max]={en.min():.0f},{np.percentile(en,50):.0f},{en.max():.0f}ns dur[p10,p50,p90]={np.percentile(dur,10):.0f},"
                       f"{np.percentile(dur,50):.0f},{np.percentile(dur,90):.0f}ns", flush=True)
+        if args.sweep3 and not name.startswith(("fa_", "rms", "pp_")):
+            for cfg in range(6):
+                for bpc in args.bpc:
+                    lib.ggml_backend_mi355x_set_tune(12, cfg + 1)
+                    lib.ggml_backend_mi355x_set_tune(13, bpc)
+                    separator(pkg, be)
+                    for it in range(args.iters):
+                        ctx.compute(be, graphs[it % len(graphs)])
+                    be.synchronize()
+                    names.append(f"{name}@c{cfg}b{bpc}")
+            lib.ggml_backend_mi355x_set_tune(12, 0)
+            lib.ggml_backend_mi355x_set_tune(13, 0)
+            ctx.free()
+            continue
+        if args.ab:
+            for spec in args.ab:
+                kv = [tuple(int(x) for x in t.split("=")) for t in spec.split(",") if t]
+                for k, v in kv:
+                    lib.ggml_backend_mi355x_set_tune(k, v)
+                separator(pkg, be)
+                for it in range(args.iters):
+                    ctx.compute(be, graphs[it % len(graphs)])
+                be.synchronize()
+                names.append(f"{name}@{spec}")
+                for k, _ in kv:
+                    lib.ggml_backend_mi355x_set_tune(k, 0)
+            ctx.free()
+            continue
+        if args.dbg:
+            for d in args.dbg:
+                lib.ggml_backend_mi355x_set_tune(11, d)
+                separator(pkg, be)
+                for it in range(args.iters):
+                    ctx.compute(be, graphs[it % len(graphs)])
+                be.synchronize()
+                names.append(f"{name}@dbg{d}")
+            lib.ggml_backend_mi355x_set_tune(11, 0)
+            ctx.free()
+            continue
         for cfg in cfgs:
             base = 2 if name.startswith("glu") else 0
             lib.ggml_backend_mi355x_set_tune(base, cfg[0] if cfg else 0)
