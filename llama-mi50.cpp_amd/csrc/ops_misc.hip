@@ -38,23 +38,22 @@ template <> __device__ __forceinline__ void st<uint16_t>(uint16_t * p, float v) 
 // ---------------------------------------------------------------------------
 // GET_ROWS: dst[:, i10, i11, i12] = dequant(src0[:, idx[i10,i11,i12], i11, i12])
 // ---------------------------------------------------------------------------
+// grid (rows, ne0 / 256): one element per thread, so every thread's few block-byte loads
+// are in flight at once (a 256-thread block looping over a 4096-wide row paid one
+// dependent memory round trip per 256 elements: 12.6 us for the decode's token row)
 template <int QT>
 __global__ void k_get_rows_q(const char * __restrict__ src0, const int32_t * __restrict__ idx, float * __restrict__ dst,
                              T4 s0, T4 s1, T4 d) {
     const int64_t r = blockIdx.x;  // flat index over (i10, i11, i12)
+    const int64_t e = (int64_t) blockIdx.y * blockDim.x + threadIdx.x;
+    if (e >= s0.ne[0]) return;
     const int64_t i10 = r % s1.ne[0];
     const int64_t i11 = (r / s1.ne[0]) % s1.ne[1];
     const int64_t i12 = r / (s1.ne[0] * s1.ne[1]);
     const int32_t i01 = *(const int32_t *) ((const char *) idx + i10 * s1.nb[0] + i11 * s1.nb[1] + i12 * s1.nb[2]);
     const char * row = src0 + i01 * s0.nb[1] + i11 * s0.nb[2] + i12 * s0.nb[3];
     float * out = (float *) ((char *) dst + i10 * d.nb[1] + i11 * d.nb[2] + i12 * d.nb[3]);
-    const int64_t nblk = s0.ne[0] / qk_of<QT>();
-    for (int64_t e = threadIdx.x; e < s0.ne[0]; e += blockDim.x) {
-        const int64_t b = e / qk_of<QT>();
-        const int j = (int) (e % qk_of<QT>());
-        out[e] = dequant_one<QT>(row + b * qsize_of<QT>(), j);
-        (void) nblk;
-    }
+    out[e] = dequant_one<QT>(row + (e / qk_of<QT>()) * qsize_of<QT>(), (int) (e % qk_of<QT>()));
 }
 
 template <typename TS, typename TD>
@@ -85,8 +84,8 @@ void op_get_rows(OpCtx & c, ggml_tensor * dst) {
     const char * a = (const char *) s0->data;
     const int32_t * ix = (const int32_t *) s1->data;
     switch (s0->type) {
-#define GR_Q(T) case T: MX_ASSERT(dst->type == GGML_TYPE_F32); \
-        k_get_rows_q<T><<<grid, blk, 0, c.st>>>(a, ix, (float *) dst->data, g0, g1, gd); break;
+#define GR_Q(T) case T: MX_ASSERT(dst->type == GGML_TYPE_F32 && nr < 65536 * 1024); \
+        k_get_rows_q<T><<<dim3((unsigned) nr, (unsigned) mx_ceil_div(s0->ne[0], 256)), blk, 0, c.st>>>(a, ix, (float *) dst->data, g0, g1, gd); break;
         GR_Q(GGML_TYPE_Q4_0) GR_Q(GGML_TYPE_Q4_1) GR_Q(GGML_TYPE_Q5_0) GR_Q(GGML_TYPE_Q5_1) GR_Q(GGML_TYPE_Q8_0)
         GR_Q(GGML_TYPE_Q4_K) GR_Q(GGML_TYPE_Q5_K) GR_Q(GGML_TYPE_Q6_K)
 #undef GR_Q
