@@ -266,7 +266,14 @@ def main():
     ap.add_argument("--skip-roofline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing (for scripts/pmc_roofline.sh's rocprofv3 --pmc passes)")
+    ap.add_argument("--tune", nargs="*", default=[], help="backend tuning knobs IDX=VAL (A/B experiments)")
     args = ap.parse_args()
+    if args.tune:
+        from mi355x_pkg import load_package
+        lib = load_package()._lib.load()
+        for t in args.tune:
+            k, v = (int(x) for x in t.split("="))
+            lib.ggml_backend_mi355x_set_tune(k, v)
     if args.roofline_only:
         from mi355x_pkg import load_package
         pkg = load_package()
@@ -283,7 +290,11 @@ def main():
     shape_name, def_recipe, label = MODELS[args.model]
     shape = getattr(pkg, shape_name)
     recipe = args.recipe or def_recipe
-    n_ctx = max(args.pp, args.tg) + 256
+    # llama-bench sizes the context per test: n_ctx = n_prompt + n_gen, padded to 256 cells
+    # (src/llama-context.cpp) — tg128 runs in a 256-cell cache, pp512 in a 512-cell one
+    pad256 = lambda n: max(256, (n + 255) // 256 * 256)   # noqa: E731
+    n_ctx_tg, n_ctx_pp = pad256(args.tg), pad256(args.pp)
+    n_ctx = max(n_ctx_tg, n_ctx_pp)
     rng = np.random.default_rng(42 + rank)
     n_vocab = shape["n_vocab"]
 
@@ -296,7 +307,7 @@ def main():
     else:
         be = pkg.Backend(local if world > 1 else 0)
         model = pkg.Model.random(be, shape, recipe, seed=1234 + rank)
-        sess = pkg.Session(model, n_ctx=n_ctx, n_ubatch=512, flash_attn=not args.no_fa)
+        sess = pkg.Session(model, n_ctx=n_ctx_tg, n_ubatch=512, flash_attn=not args.no_fa)
         run_tg = lambda: tg_step(sess, rng, n_vocab, args.tg)   # noqa: E731
         tokens_per_step = args.tg                                # per rank; summed below
 
@@ -329,6 +340,8 @@ def main():
             barrier(dist, local)
             pp_tok_s = reps * args.pp / max_over_ranks(dist, time.perf_counter() - t1)
         else:
+            sess.free()
+            sess = pkg.Session(model, n_ctx=n_ctx_pp, n_ubatch=512, flash_attn=not args.no_fa)
             toks = rng.integers(0, n_vocab, size=args.pp, dtype=np.int32)
             sess.reset(); sess.decode(toks)  # warm the prefill graph
             reps = 3

@@ -78,11 +78,13 @@ XStage xstage_of(Stream * s, const ggml_tensor * x) {
             XStage xs{(const float *) d.norm->src[0]->data, (const float *) d.w->data, mx_op_param<float>(d.norm, 0), 1};
             xs.dbg = g_tune[11];
             xs.xcd = g_tune[15] != 1;
+            xs.drain = g_tune[14] == 1;
             return xs;
         }
     XStage xs{(const float *) x->data, nullptr, 0.0f, 0};
     xs.dbg = g_tune[11];
     xs.xcd = g_tune[15] != 1;
+    xs.drain = g_tune[14] == 1;
     if (const ActQ * a = act_cache_find(s, x)) {
         if (a->kp == x->ne[0]) { xs.q8 = a->q; xs.q8d = a->d; xs.q8s = a->s; }
     }

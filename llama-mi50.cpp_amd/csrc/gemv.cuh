@@ -191,7 +191,8 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
         wait_vmcnt<NW>();                     // the LDS-DMA of stage_issue has landed
     } else if constexpr (MODE == XS_F32_LDS || MODE == XS_NORM_LDS) {
         const float * xf = (const float *) ((const char *) a.q + gemv_lds_base(K));
-        wait_vmcnt<NW>();
+        if (xs.drain) wait_vmcnt<0>();       // A/B (g_tune[14]): prologue after the whole stream
+        else wait_vmcnt<NW>();
         lds_barrier();                        // staged x (and norm weight) visible
         float scale = 1.0f;
         if constexpr (MODE == XS_NORM_LDS) {

@@ -22,6 +22,8 @@ struct XStage {
                                     // prologue, 2 skip the dot products, 4 skip epilogue math,
                                     // 8 skip the QKV kernel's KV-cache stores
     int xcd = 1;                    // XCD-contiguous block order (g_tune[15] = 1 turns it off)
+    int drain = 0;                  // f32 LDS-staged sources: wait for every weight load
+                                    // before the prologue (g_tune[14] = 1; A/B)
 };
 
 extern int g_tune[16];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)
