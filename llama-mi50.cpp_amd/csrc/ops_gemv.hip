@@ -79,10 +79,11 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
 }
 
 template <int QT, int LPR, int UPL, int EPI, int W = 4>
-static void launch_cfg(hipStream_t st, const G2Args & p) {
+static void launch_cfg(hipStream_t st, const G2Args & p, bool regs = false) {
     constexpr int RPB = W * (64 / LPR);
     const unsigned grid = (unsigned) ((p.nrows + RPB - 1) / RPB);
-    const int mode = gemv_mode(p.xs, p.K, (int64_t) grid * W, 64 * W);
+    // regs: register staging of x even on a large grid (the q8-emitting SwiGLU)
+    const int mode = gemv_mode(p.xs, p.K, regs && g_tune[9] == 0 ? 0 : (int64_t) grid * W, 64 * W);
     const size_t lds = gemv_lds_bytes(p.K, mode);
     switch (mode) {
         case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8><<<grid, 64 * W, lds, st>>>(p); break;
@@ -100,8 +101,11 @@ static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
     if constexpr (EPI == 1) {
         if (p.q8o) {   // 32 rows per block; g_tune[4] picks the geometry (sweeps)
             // tools/opbench.py ffn_block --sweep-glu8: W8 LPR16 UPL2 with LDS-staged norm best
+            // default 8 waves x 16 lanes x 2 units, x staged by LDS-DMA. The 16-wave form with
+            // x in registers timed 0.5 us faster alone (profiles/r01/opbench_glu8_sweep.txt)
+            // but 2 % slower in the decode (589 vs 600 tok/s, scripts/ab_bench.sh 4=3 vs 4=0)
             if (g_tune[4] == 1) return launch_cfg<QT, 32, 1, 1, 16>(st, p);
-            if (g_tune[4] == 3 && p.nrows % 64 == 0) return launch_cfg<QT, 16, 2, 1, 16>(st, p);
+            if (g_tune[4] == 3 && p.nrows % 64 == 0) return launch_cfg<QT, 16, 2, 1, 16>(st, p, true);
             return launch_cfg<QT, 16, 2, 1, 8>(st, p);
         }
     }

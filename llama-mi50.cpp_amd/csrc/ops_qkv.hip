@@ -36,21 +36,24 @@ __device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i)
     return is64 ? ((const int64_t *) p)[i] : (int64_t) ((const int32_t *) p)[i];
 }
 
-// LPR = 16: the RoPE pair (rows 2i, 2i+1) sits 16 lanes apart in one wave
-template <int QTA, int QTV, int MODE>
+// Geometry: LA lanes x UA units per row for Q/K (LA <= 32: the RoPE pair, rows 2i and
+// 2i+1, sits LA lanes apart in one wave), LV x UV for V (no pairing). Rows per block =
+// 4 waves x 64/L.
+template <int QTA, int QTV, int MODE, int LA = 16, int UA = 4, int LV = 16, int UV = 4>
 __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
+    static_assert(LA <= 32, "RoPE pairs must share a wave");
     extern __shared__ __align__(16) char smem[];
-    constexpr int LPR = 16, UPLA = 4, UPLV = 4;
+    constexpr int RBA = 4 * (64 / LA), RBV = 4 * (64 / LV);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int sub = lane & 15;
     // XCD-contiguous order within each matrix's block range (gemv.cuh xcd_block): every
     // 128-B line of q_out and of the K/V cache rows is then written by one XCD's L2
     const int m = (int) blockIdx.x < p.nblk_q ? 0 : ((int) blockIdx.x < p.nblk_q + p.nblk_k ? 1 : 2);
     const int base = m == 0 ? 0 : (m == 1 ? p.nblk_q : p.nblk_q + p.nblk_k);
     const int nb = m == 0 ? p.nblk_q : (m == 1 ? p.nblk_k : (int) gridDim.x - p.nblk_q - p.nblk_k);
-    const int b = base + ((base & 7) == 0 ? xcd_block((int) blockIdx.x - base, nb, p.xs.xcd) : (int) blockIdx.x - base);
-    const int bl = m == 0 ? b : (m == 1 ? b - p.nblk_q : b - p.nblk_q - p.nblk_k);
-    const int row = bl * 16 + wave * 4 + (lane >> 4);
+    const int bl = (base & 7) == 0 ? xcd_block((int) blockIdx.x - base, nb, p.xs.xcd) : (int) blockIdx.x - base;
+    const int L = m == 2 ? LV : LA;
+    const int sub = lane % L;
+    const int row = m == 2 ? bl * RBV + wave * (64 / LV) + lane / LV : bl * RBA + wave * (64 / LA) + lane / LA;
     const bool valid = row < p.rows[m];
     const char * rows[1] = {p.w[m] + (int64_t) (valid ? row : p.rows[m] - 1) * p.w_row[m]};
     const LdsAct a = lds_act(smem, p.K);
@@ -73,13 +76,13 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     auto fence = [&] { asm volatile("" : "+v"(pos)); asm volatile("" : "+v"(kvrow)); asm volatile("" : "+v"(csn.x)); asm volatile("" : "+v"(csn.y)); };
     StageRegs<256, MODE> sr;
     stage_issue<256, MODE>(p.xs, p.K, a, sr);
-    if (m == 2) gemv_rows_staged<QTV, LPR, UPLV, 1, 256, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, sr, acc, fence);   // block-uniform branch
-    else gemv_rows_staged<QTA, LPR, UPLA, 1, 256, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, sr, acc, fence);
+    if (m == 2) gemv_rows_staged<QTV, LV, UV, 1, 256, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, sr, acc, fence);   // block-uniform branch
+    else gemv_rows_staged<QTA, LA, UA, 1, 256, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, sr, acc, fence);
     MX_TRACE(tr, 3);
     MX_TRACE_BLK(p.trace_blk, 1);
-    const float v = acc[0];
-    const float pv = __shfl_xor(v, 16, 64);
-    if (sub != 0 || !valid) return;
+    const float v = acc[0];   // row sum: in lane sub == L-1 (every lane of the row for L <= 16)
+    const float pv = __shfl_xor(v, LA, 64);
+    if (sub != L - 1 || !valid) return;
     if (p.xs.dbg & 4) { if (m == 0) p.q_out[row] = v; return; }
     if ((p.xs.dbg & 8) && m > 0) return;
     if (m == 2) {
@@ -190,12 +193,20 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     QkvArgs p{};
     const ggml_tensor * ws[3] = {wq, wk, wv};
     for (int t = 0; t < 3; ++t) { p.w[t] = (const char *) ws[t]->data; p.w_row[t] = ws[t]->nb[1]; p.rows[t] = ws[t]->ne[1]; }
-    p.nblk_q = (int) mx_ceil_div(wq->ne[1], 16);
+    // geometry (g_tune[12] sweeps; opbench attn_in + decode bench on MI355X,
+    // profiles/r01/opbench_qkv_geometry.txt): Q/K 16 lanes x 2 units (two batches over
+    // K = 4096), V 32 x 2 — 6.9 us vs 8.3 for the 16 x 4 / 16 x 4 of the first version:
+    // half the per-lane dot tail
+    int cfg = g_tune[12] ? g_tune[12] - 1 : 5;
+    static const int GEO[6][4] = {{16, 4, 16, 4}, {16, 4, 64, 1}, {32, 2, 64, 1}, {32, 2, 32, 2}, {32, 1, 32, 1}, {16, 2, 32, 2}};
+    if (cfg < 0 || cfg > 5) cfg = 5;
+    const int rba = 4 * (64 / GEO[cfg][0]), rbv = 4 * (64 / GEO[cfg][2]);
+    p.nblk_q = (int) mx_ceil_div(wq->ne[1], rba);
     p.K = (int) wq->ne[0];
     p.units_a = (int) (wq->ne[0] / ((wq->type == GGML_TYPE_Q4_0 || wq->type == GGML_TYPE_Q8_0) ? 32 : 64));
     p.units_v = (int) (wv->ne[0] / ((wv->type == GGML_TYPE_Q4_0 || wv->type == GGML_TYPE_Q8_0) ? 32 : 64));
-    p.nblk_k = (int) mx_ceil_div(wk->ne[1], 16);
-    const int nblk_v = (int) mx_ceil_div(wv->ne[1], 16);
+    p.nblk_k = (int) mx_ceil_div(wk->ne[1], rba);
+    const int nblk_v = (int) mx_ceil_div(wv->ne[1], rbv);
     p.q_out = (float *) rq->data;
     p.kc = (char *) sk->data; p.kc_nb1 = sk->nb[1]; p.kidx = (const char *) kix->data; p.kidx64 = kix->type == GGML_TYPE_I64;
     p.vc = (char *) sv->data; p.vc_nb1 = sv->nb[1]; p.vidx = (const char *) vix->data; p.vidx64 = vix->type == GGML_TYPE_I64;
@@ -216,17 +227,23 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
 
     const int ta = wq->type, tv = wv->type;
     void (*kern)(QkvArgs) = nullptr;
-#define QKV(TA, TV) if (ta == TA && tv == TV) kern = k_qkv_rope_store<TA, TV, XS_NORM>;
+    // the Llama K-quant mixes get every geometry; the other type pairs the default one
+#define GEOS(TA, TV, M) if (ta == TA && tv == TV) kern = cfg == 0 ? k_qkv_rope_store<TA, TV, M, 16, 4, 16, 4> : \
+        cfg == 1 ? k_qkv_rope_store<TA, TV, M, 16, 4, 64, 1> : cfg == 2 ? k_qkv_rope_store<TA, TV, M, 32, 2, 64, 1> : \
+        cfg == 3 ? k_qkv_rope_store<TA, TV, M, 32, 2, 32, 2> : cfg == 4 ? k_qkv_rope_store<TA, TV, M, 32, 1, 32, 1> : \
+        k_qkv_rope_store<TA, TV, M, 16, 2, 32, 2>;
+#define QKV(TA, TV) if (ta == TA && tv == TV) kern = k_qkv_rope_store<TA, TV, XS_NORM, 16, 2, 32, 2>;
     QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
     QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
     QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
 #undef QKV
+    GEOS(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, XS_NORM) GEOS(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K, XS_NORM)
     if (!kern) return 0;
     if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs)) return 0;
     const int mode = gemv_mode(p.xs, p.K, 0);
     if (mode != XS_NORM) {   // the fused block normally follows attn_norm; other sources
-#define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8> : \
-        mode == XS_NORM_H2 ? k_qkv_rope_store<TA, TV, XS_NORM_H2> : k_qkv_rope_store<TA, TV, XS_F32_H2>;
+#define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8, 16, 2, 32, 2> : \
+        mode == XS_NORM_H2 ? k_qkv_rope_store<TA, TV, XS_NORM_H2, 16, 2, 32, 2> : k_qkv_rope_store<TA, TV, XS_F32_H2, 16, 2, 32, 2>;
             QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
         QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
         QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
@@ -242,6 +259,8 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     }
     p.tab = (const float2 *) S->rope_tab;
     for (int j = i; j <= last; ++j) act_cache_invalidate(c.s, g->nodes[j]);
+#undef GEOS
+    if (mode != XS_NORM && cfg != 5) return 0;   // the other sources exist in the default geometry only
     const dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
     hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K, mode), c.st, p);
     return last - i + 1;
