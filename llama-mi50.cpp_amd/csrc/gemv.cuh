@@ -339,17 +339,15 @@ __device__ __forceinline__ float w2_dot(const W2<QT> & r, int u, const LdsAct & 
     if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
         const int sb = u >> 2, g = u & 3;
         const uint32_t s0 = (uint32_t) r.hd.y, s1 = (uint32_t) r.hd.z, s2 = (uint32_t) r.hd.w;
-        auto byte = [&](int j) -> int {
-            const uint32_t v = j < 4 ? s0 : (j < 8 ? s1 : s2);
-            return (v >> (8 * (j & 3))) & 0xFF;
-        };
-        int sc[2], mn[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {   // get_scale_min_k4 (ggml-quants.c:703)
-            const int j = 2 * g + t;
-            if (j < 4) { sc[t] = byte(j) & 63; mn[t] = byte(j + 4) & 63; }
-            else { sc[t] = (byte(j + 4) & 0xF) | ((byte(j - 4) >> 6) << 4); mn[t] = (byte(j + 4) >> 4) | ((byte(j) >> 6) << 4); }
-        }
+        // get_scale_min_k4 (ggml-quants.c:703) for all eight sub-blocks at once, four 6-bit
+        // values per dword (j < 4: low 6 bits of bytes j / j+4; j >= 4: low nibble of byte
+        // j+4 with the top two bits of byte j-4 / j), then this unit's pair (2g, 2g+1) by one
+        // select and one shift: ~10 VALU instead of ~25 for per-scale byte selects
+        const uint32_t scw = g < 2 ? (s0 & 0x3F3F3F3Fu) : ((s2 & 0x0F0F0F0Fu) | ((s0 >> 2) & 0x30303030u));
+        const uint32_t mnw = g < 2 ? (s1 & 0x3F3F3F3Fu) : (((s2 >> 4) & 0x0F0F0F0Fu) | ((s1 >> 2) & 0x30303030u));
+        const uint32_t scp = scw >> (16 * (g & 1)), mnp = mnw >> (16 * (g & 1));
+        const int sc[2] = {(int) (scp & 0xFF), (int) ((scp >> 8) & 0xFF)};
+        const int mn[2] = {(int) (mnp & 0xFF), (int) ((mnp >> 8) & 0xFF)};
         const float d = h2f((uint16_t) (r.hd.x & 0xFFFF)), dmin = h2f((uint16_t) ((uint32_t) r.hd.x >> 16));
         const int wv[8] = {r.w0.x, r.w0.y, r.w0.z, r.w0.w, r.w1.x, r.w1.y, r.w1.z, r.w1.w};
         int lo[2][4], hi[2][4];

@@ -243,6 +243,7 @@ def main():
     for name in args.only or list(CASES):
         cfgs = [None]
         if args.sweep_mm and name.startswith("pp_"):
+            ctx, graphs = CASES[name](pkg, be, rng)
             for bm in (64, 128):
                 lib.ggml_backend_mi355x_set_tune(8, bm)
                 separator(pkg, be)
