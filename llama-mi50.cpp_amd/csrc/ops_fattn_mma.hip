@@ -29,6 +29,8 @@ struct FaMmaArgs {
     float scale;
 };
 
+static const bool g_fa_mma1 = getenv("GGML_MI355X_FA_MMA1") != nullptr;   // A/B: the first kernel
+
 constexpr int FM_QT = 64;    // query rows per workgroup
 constexpr int FM_KT = 64;    // keys per tile
 
@@ -213,6 +215,228 @@ __global__ __launch_bounds__(128, 2) void k_fa_mma(FaMmaArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// v2 (D = 128): the first kernel spent ~11 µs per 64-key tile (profiles/r01: 90 µs per
+// layer at pp512) on a 16-way bank-conflicted V transpose in LDS, S and P round trips
+// through LDS and un-overlapped tile loads. v2:
+//  * S^T = K·Q^T (A = K rows from LDS, B = the wave's Q fragments in registers): a lane
+//    holds 32 of the 64 scores of ITS query (lane & 31), the other 32 in lane ^ 32 —
+//    the softmax max is one cross-half shuffle, no LDS;
+//  * O^T = V^T·P^T: B = P^T straight from those registers (the MFMA k index is mapped to
+//    the keys the lane already holds; V's rows follow the same map), A = V^T read from the
+//    plain row-major V tile with ds_read_b64_tr_b16 (gfx950 transposing LDS read) — no
+//    transposed staging; O^T's columns are queries, so the rescale by alpha is lane-local;
+//  * K and V tiles in one swizzled [key][128 x f16] image each (256-B rows, chunk XOR
+//    ((row&3)<<2 | (row>>2)&3): conflict-free for both the b128 row reads and the
+//    transposed reads); the next live tile's K/V and the mask two tiles ahead are in
+//    flight while the current tile computes; tiles the mask removes are not loaded;
+//  * 4 waves = the HG query heads of a GQA group that share the K/V tile x 32 queries
+//    (HG = 4: K/V staged once for four heads).
+typedef _Float16 fhalf4 __attribute__((ext_vector_type(4)));
+typedef __fp16 fp16x4_t __attribute__((vector_size(8)));
+typedef __attribute__((address_space(3))) fp16x4_t * lds_h4_t;
+__device__ __forceinline__ fhalf4 lds_tr16(const char * a) {   // ds_read_b64_tr_b16
+    return __builtin_bit_cast(fhalf4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_h4_t) a));
+}
+
+__device__ __forceinline__ int fm2_off(int row, int ch) {     // byte offset in a 256-B-row tile
+    return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+template <int HG>
+__global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
+    constexpr int D = 128, NKS = D / 16, NDT = D / 32;
+    constexpr int QB = 32 * (4 / HG);                          // queries per workgroup
+    __shared__ __align__(16) char ks[FM_KT * 256];
+    __shared__ __align__(16) char vs[FM_KT * 256];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l32 = lane & 31, hl = lane >> 5;
+    const int Gt = p.H / p.Hkv, NGB = Gt / HG;
+    const int hk = blockIdx.y / NGB;
+    const int h = hk * Gt + (blockIdx.y % NGB) * HG + wave % HG;
+    const int qw = blockIdx.x * QB + 32 * (wave / HG);          // this wave's first query
+    const int qr = min(qw + l32, p.n_q - 1);                   // this lane's query (clamped)
+    const char * kb = p.k + (size_t) hk * p.k2;
+    const char * vb = p.v + (size_t) hk * p.v2;
+    const uint16_t * mrow = p.mask ? (const uint16_t *) (p.mask + (size_t) qr * p.m1) : nullptr;
+
+    // Q fragments, B operand of S^T: column = query l32, k = 8 dims at 16 s + 8 hl
+    fhalf8 qa[NKS];
+    {
+        const float * qp = (const float *) (p.q + (size_t) qr * p.q1 + (size_t) h * p.q2);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const float4 f0 = *(const float4 *) (qp + 16 * s + 8 * hl);
+            const float4 f1 = *(const float4 *) (qp + 16 * s + 8 * hl + 4);
+            qa[s][0] = (_Float16) f0.x; qa[s][1] = (_Float16) f0.y; qa[s][2] = (_Float16) f0.z; qa[s][3] = (_Float16) f0.w;
+            qa[s][4] = (_Float16) f1.x; qa[s][5] = (_Float16) f1.y; qa[s][6] = (_Float16) f1.z; qa[s][7] = (_Float16) f1.w;
+        }
+    }
+    // the lane's 32 keys of a tile: 32 n + 8 m + 4 hl + (0..3), n < 2, m < 4 (S^T's C layout).
+    // load_mask only issues (8-byte loads at clamped keys, unconditional: a load under a
+    // branch makes the join wait for every load in flight, the K/V prefetch included);
+    // fix_mask, one iteration later, shifts clamped groups into place and sets keys past
+    // n_kv (and a missing mask) to -inf / 0
+    const uint16_t * mp = mrow ? mrow : (const uint16_t *) p.k;
+    auto load_mask = [&](int kt, uint2 (&mk)[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int base = kt * FM_KT + 32 * (i >> 2) + 8 * (i & 3) + 4 * hl;
+            mk[i] = *(const uint2 *) (mp + min(base, p.n_kv - 4));
+        }
+    };
+    auto fix_mask = [&](int kt, uint2 (&mk)[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int base = kt * FM_KT + 32 * (i >> 2) + 8 * (i & 3) + 4 * hl;
+            const int sh = base - min(base, p.n_kv - 4);
+            uint64_t v = mrow ? ((uint64_t) mk[i].y << 32 | mk[i].x) : 0;
+            v = sh >= 4 ? 0 : v >> (16 * sh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (base + j >= p.n_kv) v = (v & ~(0xFFFFull << (16 * j))) | (0xFC00ull << (16 * j));
+            mk[i] = make_uint2((uint32_t) v, (uint32_t) (v >> 32));
+        }
+    };
+    auto any_live = [](const uint2 (&mk)[8]) {
+        int live = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            live |= ((mk[i].x & 0xFFFF) != 0xFC00) | ((mk[i].x >> 16) != 0xFC00) | ((mk[i].y & 0xFFFF) != 0xFC00) | ((mk[i].y >> 16) != 0xFC00);
+        return live;
+    };
+    // K/V tile rows, 16 B per thread per instruction: 16 threads read one 256-B row
+    // (unconditional: a load under a branch would make the loop-carried registers a
+    // scratch array; a dead tile reads one 16-B chunk for the whole workgroup instead)
+    uint4 kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3;
+#define FM2_LOAD_KV(KT, LIVE) do { \
+        const int kt_ = (KT); const bool lv_ = (LIVE); \
+        const size_t r0_ = (size_t) min(kt_ * FM_KT + (tid >> 4), p.n_kv - 1), r1_ = (size_t) min(kt_ * FM_KT + 16 + (tid >> 4), p.n_kv - 1); \
+        const size_t r2_ = (size_t) min(kt_ * FM_KT + 32 + (tid >> 4), p.n_kv - 1), r3_ = (size_t) min(kt_ * FM_KT + 48 + (tid >> 4), p.n_kv - 1); \
+        const int c_ = 16 * (tid & 15); \
+        kr0 = *(const uint4 *) (kb + (lv_ ? r0_ * p.k1 + c_ : 0)); vr0 = *(const uint4 *) (vb + (lv_ ? r0_ * p.v1 + c_ : 0)); \
+        kr1 = *(const uint4 *) (kb + (lv_ ? r1_ * p.k1 + c_ : 0)); vr1 = *(const uint4 *) (vb + (lv_ ? r1_ * p.v1 + c_ : 0)); \
+        kr2 = *(const uint4 *) (kb + (lv_ ? r2_ * p.k1 + c_ : 0)); vr2 = *(const uint4 *) (vb + (lv_ ? r2_ * p.v1 + c_ : 0)); \
+        kr3 = *(const uint4 *) (kb + (lv_ ? r3_ * p.k1 + c_ : 0)); vr3 = *(const uint4 *) (vb + (lv_ ? r3_ * p.v1 + c_ : 0)); \
+    } while (0)
+
+    ffloat16v acc_o[NDT];                                       // O^T: column = query l32
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc_o[t][e] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;                       // l_run: this half's keys only
+
+    const int n_tiles = (p.n_kv + FM_KT - 1) / FM_KT;
+    // software pipeline, one tile deep: tile kt+1's K/V rows and mask words are loaded
+    // while tile kt computes. The load destinations are consumed (mask fixed into mA,
+    // K/V stored to LDS) before they are reloaded, so no register copy waits on them.
+    uint2 mreg[8], mA[8];
+    FM2_LOAD_KV(0, true);
+    load_mask(0, mreg);
+    for (int kt = 0; kt < n_tiles; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mA[i] = mreg[i];
+        fix_mask(kt, mA);
+        {
+            const int row = tid >> 4, ch = tid & 15;
+            *(uint4 *) (ks + fm2_off(row, ch)) = kr0; *(uint4 *) (vs + fm2_off(row, ch)) = vr0;
+            *(uint4 *) (ks + fm2_off(row + 16, ch)) = kr1; *(uint4 *) (vs + fm2_off(row + 16, ch)) = vr1;
+            *(uint4 *) (ks + fm2_off(row + 32, ch)) = kr2; *(uint4 *) (vs + fm2_off(row + 32, ch)) = vr2;
+            *(uint4 *) (ks + fm2_off(row + 48, ch)) = kr3; *(uint4 *) (vs + fm2_off(row + 48, ch)) = vr3;
+        }
+        const bool live_cur = __syncthreads_or(any_live(mA));   // + the tiles are visible
+        FM2_LOAD_KV(min(kt + 1, n_tiles - 1), true);
+        load_mask(min(kt + 1, n_tiles - 1), mreg);
+        if (live_cur) {
+            // ---- S^T = K Q^T: 64 keys (2 blocks of 32) x this wave's 32 queries
+            ffloat16v acc_s[2];
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc_s[n][e] = 0.f;
+#pragma unroll
+            for (int s = 0; s < NKS; ++s)
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    const fhalf8 kf = *(const fhalf8 *) (ks + fm2_off(32 * n + l32, 2 * s + hl));
+                    acc_s[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qa[s], acc_s[n], 0, 0, 0);
+                }
+            // ---- online softmax of this lane's query over its 32 keys + the partner half's,
+            // in the log2 domain (v_exp_f32), with a lazily raised reference max: O and l are
+            // rescaled only when a query's max grows by more than 2^8 (P <= 256 stays exact
+            // enough in f16), i.e. on the first tiles, not on every tile
+            constexpr float LOG2E = 1.4426950408889634f;
+            const float sl = p.scale * LOG2E;
+            float mt = -INFINITY;
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const uint2 mv = mA[4 * n + (e >> 2)];
+                    const uint32_t w = (e & 2) ? mv.y : mv.x;
+                    const float mval = h2f((uint16_t) ((e & 1) ? (w >> 16) : (w & 0xFFFF)));
+                    acc_s[n][e] = acc_s[n][e] * sl + mval * LOG2E;
+                    mt = fmaxf(mt, acc_s[n][e]);
+                }
+            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+            const bool raise = mt > m_run + 8.0f;               // false while mt = -inf
+            if (__any(raise)) {                                 // wave-uniform
+                const float m_new = raise ? mt : m_run;
+                const float alpha = raise ? __builtin_amdgcn_exp2f(m_run - m_new) : 1.f;   // m_run = -inf: 0
+                l_run *= alpha;
+                m_run = m_new;
+#pragma unroll
+                for (int t = 0; t < NDT; ++t)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc_o[t][e] *= alpha;
+            }
+            fhalf8 pb[4];                                       // P^T fragments, k-step s
+            float lt = 0.f;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float pv = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(acc_s[s >> 1][8 * (s & 1) + j] - m_run);
+                    lt += pv;
+                    pb[s][j] = (_Float16) pv;
+                }
+            l_run += lt;
+            // ---- O^T += V^T P^T; A = V^T by transposing reads: the 16-lane group g reads
+            // keys r0 + (0..3) [+ 8] x dims 32 t + 16 (g & 1) + (0..15); lane 4q + pp of the
+            // group addresses row r0 + q, dims +4 pp .. +4 pp + 3
+            const int g = lane >> 4, iq = (lane >> 2) & 3, ip = lane & 3;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int r0 = 32 * (s >> 1) + 16 * (s & 1) + 4 * (g >> 1) + iq;
+#pragma unroll
+                for (int t = 0; t < NDT; ++t) {
+                    const int c0 = 4 * t + 2 * (g & 1) + (ip >> 1);
+                    const fhalf4 lo = lds_tr16(vs + fm2_off(r0, c0) + 8 * (ip & 1));
+                    const fhalf4 hi = lds_tr16(vs + fm2_off(r0 + 8, c0) + 8 * (ip & 1));
+                    const fhalf8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    acc_o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pb[s], acc_o[t], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();                                        // K/V tiles are rewritten next
+    }
+    // ---- normalise and store: lane = query l32, rows d = 32 t + 8 g + 4 hl + (0..3)
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = l_tot == 0.f ? 0.f : 1.0f / l_tot;
+    if (qw + l32 < p.n_q) {
+        float * out = (float *) (p.dst + (size_t) h * p.d1 + (size_t) (qw + l32) * p.d2);
+#pragma unroll
+        for (int t = 0; t < NDT; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                *(float4 *) (out + 32 * t + 8 * g + 4 * hl) = make_float4(acc_o[t][4 * g] * inv, acc_o[t][4 * g + 1] * inv,
+                                                                         acc_o[t][4 * g + 2] * inv, acc_o[t][4 * g + 3] * inv);
+    }
+#undef FM2_LOAD_KV
+}
+
 bool fa_mma_ok(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * k = dst->src[1];
@@ -244,6 +468,14 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
     p.dst = (char *) dst->data; p.d1 = dst->nb[1]; p.d2 = dst->nb[2];
     p.n_q = (int) q->ne[1]; p.n_kv = (int) k->ne[1]; p.H = (int) q->ne[2]; p.Hkv = (int) k->ne[2];
     p.scale = mx_op_param<float>(dst, 0);
+    if (k->ne[0] == 128 && k->ne[1] >= 4 && !g_fa_mma1 && (dst->nb[1] % 16) == 0 && ((uintptr_t) dst->data % 16) == 0) {
+        const int Gt = p.H / p.Hkv, HG = Gt % 4 == 0 ? 4 : (Gt % 2 == 0 ? 2 : 1);
+        const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32 * (4 / HG)), (unsigned) (p.Hkv * (Gt / HG)));
+        if (HG == 4) k_fa_mma2<4><<<g2, 256, 0, c.st>>>(p);
+        else if (HG == 2) k_fa_mma2<2><<<g2, 256, 0, c.st>>>(p);
+        else k_fa_mma2<1><<<g2, 256, 0, c.st>>>(p);
+        return;
+    }
     dim3 grid((unsigned) mx_ceil_div(p.n_q, FM_QT), (unsigned) p.H);
     if (k->ne[0] == 64) k_fa_mma<64><<<grid, 128, 0, c.st>>>(p);
     else k_fa_mma<128><<<grid, 128, 0, c.st>>>(p);

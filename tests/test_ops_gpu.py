@@ -176,7 +176,11 @@ def test_fused_gate_up_swiglu(pkg, backend, orc, tname):
                                                # decode kernel v2 (ops_fattn_dec.hip): one split (direct
                                                # store), ragged last split, GQA 8, D 64 with 2 query rows
                                                (1, 64, 8, 8, 128), (1, 100, 32, 4, 128), (2, 65, 16, 2, 64),
-                                               (4, 1500, 32, 8, 128)])
+                                               (4, 1500, 32, 8, 128),
+                                               # prefill kernel v2 (k_fa_mma2, D 128): 4 / 2 / 1 heads
+                                               # per workgroup, GQA 8 (two head groups), ragged tiles
+                                               (512, 512, 32, 8, 128), (200, 450, 6, 3, 128), (77, 77, 16, 2, 128),
+                                               (33, 1000, 4, 4, 128)])
 def test_flash_attn(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
     rng = np.random.default_rng(n_q * 1000 + n_kv)
     q = rng.standard_normal((H, n_q, D)).astype(np.float32)

@@ -165,19 +165,22 @@ def case_ffn_block(pkg, be, rng, tname="q4_K", tdown="q4_K", K=4096, F=14336):
     return ctx, graphs
 
 
-def case_fa(pkg, be, rng, n_kv, H=32, Hkv=8, D=128):
+def case_fa(pkg, be, rng, n_kv, H=32, Hkv=8, D=128, n_q=1):
     ctx = pkg.Context()
-    q = ctx.new_tensor("f32", D, 1, H)
+    q = ctx.new_tensor("f32", D, n_q, H)
     k = ctx.new_tensor("f16", D, n_kv, Hkv)
     v = ctx.new_tensor("f16", D, n_kv, Hkv)
-    m = ctx.new_tensor("f16", n_kv, 1)
+    m = ctx.new_tensor("f16", n_kv, n_q)
     o = ctx.flash_attn_ext(q, k, v, m, 1.0 / np.sqrt(D))
     g = ctx.build(o)
     ctx.alloc(be)
-    q.set(rng.standard_normal((H, D)).astype(np.float32))
+    q.set(rng.standard_normal((H, n_q, D)).astype(np.float32))
     k.set(rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16))
     v.set(rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16))
-    m.set(np.zeros(n_kv, np.float16).view(np.uint16))
+    mask = np.zeros((n_q, n_kv), np.float32)
+    for i in range(n_q):                      # causal, the prompt at the end of the cache
+        mask[i, n_kv - n_q + i + 1:] = -np.inf
+    m.set(mask.astype(np.float16).view(np.uint16))
     return ctx, [g]
 
 
@@ -213,6 +216,8 @@ CASES = {
     "fa_256": lambda p, b, r: case_fa(p, b, r, 256),
     "fa_1024": lambda p, b, r: case_fa(p, b, r, 1024),
     "fa_4096": lambda p, b, r: case_fa(p, b, r, 4096),
+    "fa_pp512": lambda p, b, r: case_fa(p, b, r, 512, n_q=512),
+    "fa_pp2048": lambda p, b, r: case_fa(p, b, r, 2048, n_q=512),
     "rms_mul": lambda p, b, r: case_rms(p, b, r),
 }
 
