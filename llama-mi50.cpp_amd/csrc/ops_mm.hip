@@ -30,6 +30,9 @@ struct MmqArgs {
     const _Float16 * x; int64_t kp;          // activations f16 [cols][kp]
     float * dst; size_t d_col, d_c2, d_c3;   // in floats
     int64_t M, N, K, ne12, r2, r3;
+    int dbg;                                 // timing experiments (g_tune[13], k_mmq3): 1 weight loads
+                                             // from one L2-resident block, 2 no MFMAs, 4 activation
+                                             // loads from one 256-B row, 8 no dequantisation, 16 two K steps
 };
 
 // ---- f32 → f16 activation rows, zero padded to kp (8 values per thread) ------
@@ -493,6 +496,152 @@ __global__ __launch_bounds__(256, 2) void k_mmq2(MmqArgs p) {
     }
 }
 
+// 8 waves: waves 0-3 and 4-7 each cover the whole 128-token x BM-row tile over one half
+// of every K step (kh), so each SIMD holds two waves that hide each other's LDS-read /
+// MFMA / dequantisation latencies. With four waves (one per SIMD) a K step cost ~2400
+// cycles against 512 of MFMA work, and removing the MFMAs and the HBM weight stream
+// (g_tune[13] = 3) still left ~85 % of the time (profiles/r01/opbench_mmq_dbg.txt).
+// The two halves' accumulators are summed through LDS once, at the end.
+template <int QT, int BM>
+__global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
+    constexpr int NT = 512;
+    constexpr int NU = BM * 4;                  // weight units per K step
+    constexpr int UPT = (NU + NT - 1) / NT;     // per thread (BM 64: waves 4-7 load duplicates, store none)
+    constexpr int WM = BM / 2;                  // weight rows per wave
+    constexpr int TM = WM / 32;                 // 32-row MFMA tiles per wave (1 or 2)
+    constexpr int NA = MM_BT * MM_BK / 8 / NT;  // activation 16-byte chunks per thread per K step
+    static_assert(2 * 4 * TM * 16 * 64 * 4 <= (MM_BT + BM) * MM_BK * 2, "accumulator exchange fits the tiles");
+    __shared__ uint4 lds[(MM_BT + BM) * MM_BK / 8];
+    uint4 * lds_a = lds;
+    uint4 * lds_b = lds + MM_BT * MM_BK / 8;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = wave >> 2, wq = wave & 3;    // K half of the step; place in the 2 x 2 wave grid
+    const int wm = wq >> 1, wn = wq & 1;        // wave: 64 tokens (wm) x WM weight rows (wn)
+    const int64_t tok0 = (int64_t) blockIdx.x * MM_BT;
+    const int64_t row0 = (int64_t) blockIdx.y * BM;
+    const int64_t ch = blockIdx.z;
+    const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
+    const char * wbase = p.w + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
+    const _Float16 * xbase = p.x + ch * p.N * p.kp;
+    const int64_t nk = (p.dbg & 16) ? 2 : p.K / MM_BK;
+
+    float16v acc[2][TM];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    // two register stages (A, B): step k+2's activation rows and raw weight blocks are
+    // loaded while step k computes and step k+1 is already in flight (the activation tile
+    // comes from L2 and its latency, not HBM or the MFMAs, bounded the one-stage loop:
+    // g_tune[13] experiments, profiles/r01/opbench_mmq_dbg.txt). Loads are unconditional
+    // (clamped to the last step) so the stages stay registers.
+    uint4 raA[NA], raB[NA];
+    RawW<QT> rwA[UPT], rwB[UPT];
+    auto load = [&](uint4 (&ra)[NA], RawW<QT> (&rw)[UPT], int64_t kt) {
+        const int64_t k0 = min(kt, nk - 1) * MM_BK;
+#pragma unroll
+        for (int it = 0; it < NA; ++it) {
+            const int unit = tid + NT * it;
+            const int t = unit >> 4, chn = unit & 15;
+            const int64_t tok = min(tok0 + t, p.N - 1);
+            ra[it] = *(const uint4 *) (xbase + ((p.dbg & 4) ? 8 * chn : tok * p.kp + k0 + 8 * chn));
+        }
+#pragma unroll
+        for (int it = 0; it < UPT; ++it) {
+            const int unit = (tid + NT * it) % NU;
+            raw_load<QT>(p, wbase, (p.dbg & 1) ? row0 : row0 + (unit >> 2), (p.dbg & 1) ? 0 : k0, unit & 3, rw[it]);
+        }
+    };
+    auto store = [&](const uint4 (&ra)[NA], const RawW<QT> (&rw)[UPT], int64_t k0) {
+#pragma unroll
+        for (int it = 0; it < NA; ++it) {
+            const int unit = tid + NT * it;
+            const int t = unit >> 4, chn = unit & 15;
+            lds_a[swz(t, chn)] = tok0 + t < p.N ? ra[it] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int it = 0; it < UPT; ++it) {
+            const int unit = tid + NT * it;
+            if (unit < NU && !(p.dbg & 8))                    // wave-uniform
+                raw_store<QT>(rw[it], (int) k0, row0 + (unit >> 2) < p.M, unit >> 2, unit & 3, lds_b);
+        }
+    };
+
+    const int r = lane & 31, hsel = lane >> 5;
+    auto mfma_step = [&]() {
+#pragma unroll
+        for (int kq = 0; kq < MM_BK / 2; kq += 16) {
+            if (p.dbg & 2) break;
+            const int chn = (kh * (MM_BK / 2) + kq) / 8 + hsel;
+            half8 a[2], b[TM];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint4 va = lds_a[swz(wm * 64 + i * 32 + r, chn)];
+                a[i] = *(const half8 *) &va;
+            }
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                const uint4 vb = lds_b[swz(wn * WM + j * 32 + r, chn)];
+                b[j] = *(const half8 *) &vb;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < TM; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    load(raA, rwA, 0);
+    load(raB, rwB, 1);
+    store(raA, rwA, 0);
+    __syncthreads();
+    // nk is even (K % 256 == 0): straight-line pairs, no exits — with early exits the
+    // waitcnt insertion fell back to vmcnt(0) at the loop head, draining the prefetch.
+    // The last pair stages a clamped copy of the last step that nothing reads.
+    for (int64_t kt = 0; kt < nk; kt += 2) {
+        // LDS: step kt; B: step kt+1 in flight; A: free -> step kt+2
+        load(raA, rwA, kt + 2);
+        mfma_step();
+        __syncthreads();
+        store(raB, rwB, (kt + 1) * MM_BK);
+        __syncthreads();
+        load(raB, rwB, kt + 3);
+        mfma_step();
+        __syncthreads();
+        store(raA, rwA, min(kt + 2, nk - 1) * MM_BK);
+        __syncthreads();
+    }
+    // K halves: waves 4-7 hand their accumulators to waves 0-3 (the loop ended on a barrier)
+    float * red = (float *) lds;
+    if (kh == 1) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) red[(((wq * 2 + i) * TM + j) * 16 + e) * 64 + lane] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (kh == 1) return;
+    float * dbase = p.dst + i12 * p.d_c2 + i13 * p.d_c3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            const int64_t wrow = row0 + wn * WM + j * 32 + (lane & 31);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const float v = acc[i][j][e] + red[(((wq * 2 + i) * TM + j) * 16 + e) * 64 + lane];
+                const int64_t tok = tok0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+                if (tok < p.N && wrow < p.M) dbase[tok * p.d_col + wrow] = v;
+            }
+        }
+    }
+}
+
 static bool g_mmq_v1 = getenv("GGML_MI355X_MMQ_V1") != nullptr;
 
 bool mmq_type_ok(int t) {
@@ -539,12 +688,23 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
     p.dst = (float *) dst->data; p.d_col = dst->nb[1] / 4; p.d_c2 = dst->nb[2] / 4; p.d_c3 = dst->nb[3] / 4;
     p.M = w->ne[1]; p.N = x->ne[1]; p.K = w->ne[0]; p.ne12 = x->ne[2];
     p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
+    p.dbg = g_tune[13];
     const bool kq = w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
     if (kq && !g_mmq_v1 && p.K % 256 == 0) {
         const int64_t tiles128 = mx_ceil_div(p.N, MM_BT) * mx_ceil_div(p.M, 128) * (x->ne[2] * x->ne[3]);
         int bm = tiles128 < 512 ? 64 : 128;
         if (g_tune[8]) bm = g_tune[8];   // sweeps
         dim3 g2((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, bm), (unsigned) (x->ne[2] * x->ne[3]));
+        // one round of 64-row tiles on the CUs: the 8-wave kernel (two waves per SIMD, K
+        // step split between the wave halves) — pp512 q/k/v/o 51 -> 44 us, down 203 -> 189;
+        // larger grids keep the 4-wave kernel, two of whose workgroups share a CU
+        // (gate/up 131 vs 163 us, profiles/r01/opbench_mmq_dbg.txt)
+        const bool w8 = g_tune[5] == 1 || (g_tune[5] == 0 && bm == 64 && (int64_t) g2.x * g2.y * g2.z <= 256);
+        if (w8 && bm == 64) {
+#define MQ3(T) case T: k_mmq3<T, 64><<<g2, 512, 0, c.st>>>(p); return;
+            switch (w->type) { MQ3(GGML_TYPE_Q4_K) MQ3(GGML_TYPE_Q5_K) MQ3(GGML_TYPE_Q6_K) default: break; }
+#undef MQ3
+        }
 #define MQ2(T) case T: if (bm == 64) k_mmq2<T, 64><<<g2, 256, 0, c.st>>>(p); else k_mmq2<T, 128><<<g2, 256, 0, c.st>>>(p); return;
         switch (w->type) { MQ2(GGML_TYPE_Q4_K) MQ2(GGML_TYPE_Q5_K) MQ2(GGML_TYPE_Q6_K) default: break; }
 #undef MQ2

@@ -51,6 +51,32 @@ def test_mul_mat_quant(pkg, backend, orc, tname, N):
     assert nmse(y, ref_exact) < 5e-4
 
 
+@pytest.mark.parametrize("tname", ["q4_K", "q6_K", "q5_K"])
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_mul_mat_quant_prefill_kernels(pkg, backend, orc, tname, kernel):
+    """both K-quant prefill GEMMs (ops_mm.hip): 8-wave k_mmq3 (g_tune[5] = 1) and 4-wave
+    k_mmq2 (g_tune[5] = 2), ragged token and row tiles, K over 8 steps"""
+    lib = pkg._lib.load()
+    lib.ggml_backend_mi355x_set_tune(5, kernel)
+    try:
+        tid = NAMES[tname]
+        rng = np.random.default_rng(7 + kernel)
+        K, M, N = 1024, 200, 150
+        w, rb = rand_quant(tid, M, K, rng)
+        x = rng.standard_normal((N, K)).astype(np.float32)
+
+        def build(ctx):
+            tw = ctx.new_tensor(tid, K, M)
+            tx = ctx.new_tensor("f32", K, N)
+            return [ctx.mul_mat(tw, tx)], [(tw, w), (tx, x)]
+
+        y = run(pkg, backend, build)[0].reshape(N, M)
+        assert np.all(np.isfinite(y))
+        assert nmse(y, orc.mul_mat(tid, w, rb, x, exact=True)) < 5e-4
+    finally:
+        lib.ggml_backend_mi355x_set_tune(5, 0)
+
+
 @pytest.mark.parametrize("tname", ["q4_K", "q6_K", "q5_K", "q4_0", "q8_0", "q4_1", "q5_0", "q5_1"])
 def test_get_rows_dequant_bit_exact(pkg, backend, orc, tname):
     tid = NAMES[tname]
