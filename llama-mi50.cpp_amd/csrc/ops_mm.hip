@@ -57,6 +57,17 @@ __global__ void k_act_f16(const char * __restrict__ x, int64_t K, int64_t ne11, 
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 16 + (chunk ^ (row & 15)); }  // in 16-byte units
 
+template <int CPR>   // CPR 16-byte chunks per row (power of two)
+__device__ __forceinline__ int swzn(int row, int chunk) { return row * CPR + (chunk ^ (row & (CPR - 1))); }
+
+template <int CPR>
+__device__ __forceinline__ void st_h8n(uint4 * lds, int row, int chunk, const float (&v)[8]) {
+    half8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (_Float16) v[i];
+    lds[swzn<CPR>(row, chunk)] = *(uint4 *) &h;
+}
+
 __device__ __forceinline__ void st_h8(uint4 * lds, int row, int chunk, const float (&v)[8]) {
     half8 h;
 #pragma unroll
@@ -323,23 +334,21 @@ __device__ __forceinline__ void raw_load(const MmqArgs & p, const char * wbase, 
     }
 }
 
-template <int QT>
-__device__ __forceinline__ void raw_store(const RawW<QT> & r, int k0, bool valid, int rl, int c, uint4 * lds) {
+template <int QT, int CPR = 16>
+__device__ __forceinline__ void raw_store(const RawW<QT> & r, int k0, bool valid, int rl, int c, uint4 * lds, int choff = 0) {
     if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
         const int hf = (k0 >> 7) & 1;
         const int g = 2 * hf + (c >> 1), h = c & 1;
-        // get_scale_min_k4 on the 12 scale bytes held in hd.y..hd.w (register form)
-        auto byte = [&](int j) -> int {
-            const uint32_t v = j < 4 ? (uint32_t) r.hd.y : (j < 8 ? (uint32_t) r.hd.z : (uint32_t) r.hd.w);
-            return (v >> (8 * (j & 3))) & 0xFF;
-        };
-        auto smk = [&](int j, int & sc, int & mn) {
-            if (j < 4) { sc = byte(j) & 63; mn = byte(j + 4) & 63; }
-            else { sc = (byte(j + 4) & 0xF) | ((byte(j - 4) >> 6) << 4); mn = (byte(j + 4) >> 4) | ((byte(j) >> 6) << 4); }
-        };
-        int s0, m0, s1, m1;
-        smk(2 * g, s0, m0);
-        smk(2 * g + 1, s1, m1);
+        // get_scale_min_k4 (ggml-quants.c:703) for all eight sub-blocks at once, four 6-bit
+        // values per dword, then this unit's pair (2g, 2g+1) by one select and one shift
+        // (as the decode dot, gemv.cuh); value selects only — a runtime-indexed byte pick
+        // out of the struct made the raw-weight stages an LDS-promoted alloca
+        const uint32_t q0 = (uint32_t) r.hd.y, q1 = (uint32_t) r.hd.z, q2 = (uint32_t) r.hd.w;
+        const uint32_t scw = g < 2 ? (q0 & 0x3F3F3F3Fu) : ((q2 & 0x0F0F0F0Fu) | ((q0 >> 2) & 0x30303030u));
+        const uint32_t mnw = g < 2 ? (q1 & 0x3F3F3F3Fu) : (((q2 >> 4) & 0x0F0F0F0Fu) | ((q1 >> 2) & 0x30303030u));
+        const uint32_t scp = scw >> (16 * (g & 1)), mnp = mnw >> (16 * (g & 1));
+        const int s0 = (int) (scp & 0xFF), s1 = (int) ((scp >> 8) & 0xFF);
+        const int m0 = (int) (mnp & 0xFF), m1 = (int) ((mnp >> 8) & 0xFF);
         const float d = h2f((uint16_t) (r.hd.x & 0xFFFF)), dmin = h2f((uint16_t) ((uint32_t) r.hd.x >> 16));
         const float d0 = valid ? d * s0 : 0.f, mm0 = valid ? dmin * m0 : 0.f;
         const float d1 = valid ? d * s1 : 0.f, mm1 = valid ? dmin * m1 : 0.f;
@@ -362,16 +371,16 @@ __device__ __forceinline__ void raw_store(const RawW<QT> & r, int k0, bool valid
         float t[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) t[i] = lo[i];
-        st_h8(lds, rl, kl / 8, t);
+        st_h8n<CPR>(lds, rl, choff + kl / 8, t);
 #pragma unroll
         for (int i = 0; i < 8; ++i) t[i] = lo[8 + i];
-        st_h8(lds, rl, kl / 8 + 1, t);
+        st_h8n<CPR>(lds, rl, choff + kl / 8 + 1, t);
 #pragma unroll
         for (int i = 0; i < 8; ++i) t[i] = hi[i];
-        st_h8(lds, rl, (kl + 32) / 8, t);
+        st_h8n<CPR>(lds, rl, choff + (kl + 32) / 8, t);
 #pragma unroll
         for (int i = 0; i < 8; ++i) t[i] = hi[8 + i];
-        st_h8(lds, rl, (kl + 32) / 8 + 1, t);
+        st_h8n<CPR>(lds, rl, choff + (kl + 32) / 8 + 1, t);
     } else {
         const float d = valid ? h2f(r.d) : 0.f;
         const uint8_t * la = (const uint8_t *) &r.la, * lb = (const uint8_t *) &r.lb, * hb = (const uint8_t *) &r.qh;
@@ -389,7 +398,7 @@ __device__ __forceinline__ void raw_store(const RawW<QT> & r, int k0, bool valid
             const float sc = d * (float) scp[2 * qq];
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[qq][i] *= sc;
-            st_h8(lds, rl, (32 * qq + 8 * c) / 8, v[qq]);
+            st_h8n<CPR>(lds, rl, choff + (32 * qq + 8 * c) / 8, v[qq]);
         }
     }
 }
@@ -496,24 +505,29 @@ __global__ __launch_bounds__(256, 2) void k_mmq2(MmqArgs p) {
     }
 }
 
-// 8 waves: waves 0-3 and 4-7 each cover the whole 128-token x BM-row tile over one half
-// of every K step (kh), so each SIMD holds two waves that hide each other's LDS-read /
-// MFMA / dequantisation latencies. With four waves (one per SIMD) a K step cost ~2400
-// cycles against 512 of MFMA work, and removing the MFMAs and the HBM weight stream
-// (g_tune[13] = 3) still left ~85 % of the time (profiles/r01/opbench_mmq_dbg.txt).
-// The two halves' accumulators are summed through LDS once, at the end.
+// 8 waves, K step 256 (a whole super-block per row): waves 0-3 and 4-7 cover the same
+// 128-token x 64-row tile over the two 128-wide halves of every K step (kh), so each SIMD
+// holds two waves that hide each other's LDS-read / MFMA / dequantisation latencies, and
+// every thread stages exactly one 32-weight unit (half kh of the super-block). With four
+// waves (one per SIMD) and 128-wide steps, removing the MFMAs, the HBM weight stream and
+// the activation loads (g_tune[13]) still left ~75 % of the time: the per-step skeleton
+// (staging, dequantisation, barriers) set the pace, so the step is as wide as LDS allows
+// (96 KB). Two register stages: step k+2 loads while k computes and k+1 is in flight.
+// The halves' accumulators are summed through LDS once, at the end.
+constexpr int MM3_BK = 256;
+constexpr int MM3_CPR = MM3_BK / 8;             // 16-byte chunks per LDS row
+
 template <int QT, int BM>
 __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
     constexpr int NT = 512;
-    constexpr int NU = BM * 4;                  // weight units per K step
-    constexpr int UPT = (NU + NT - 1) / NT;     // per thread (BM 64: waves 4-7 load duplicates, store none)
+    static_assert(BM * 8 == NT, "one weight unit per thread");
     constexpr int WM = BM / 2;                  // weight rows per wave
-    constexpr int TM = WM / 32;                 // 32-row MFMA tiles per wave (1 or 2)
-    constexpr int NA = MM_BT * MM_BK / 8 / NT;  // activation 16-byte chunks per thread per K step
-    static_assert(2 * 4 * TM * 16 * 64 * 4 <= (MM_BT + BM) * MM_BK * 2, "accumulator exchange fits the tiles");
-    __shared__ uint4 lds[(MM_BT + BM) * MM_BK / 8];
+    constexpr int TM = WM / 32;                 // 32-row MFMA tiles per wave
+    constexpr int NA = MM_BT * MM3_BK / 8 / NT; // activation 16-byte chunks per thread per K step
+    static_assert(2 * 4 * TM * 16 * 64 * 4 <= (MM_BT + BM) * MM3_BK * 2, "accumulator exchange fits the tiles");
+    __shared__ uint4 lds[(MM_BT + BM) * MM3_BK / 8];
     uint4 * lds_a = lds;
-    uint4 * lds_b = lds + MM_BT * MM_BK / 8;
+    uint4 * lds_b = lds + MM_BT * MM3_BK / 8;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kh = wave >> 2, wq = wave & 3;    // K half of the step; place in the 2 x 2 wave grid
     const int wm = wq >> 1, wn = wq & 1;        // wave: 64 tokens (wm) x WM weight rows (wn)
@@ -523,7 +537,9 @@ __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
     const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
     const char * wbase = p.w + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
     const _Float16 * xbase = p.x + ch * p.N * p.kp;
-    const int64_t nk = (p.dbg & 16) ? 2 : p.K / MM_BK;
+    const int64_t nk = (p.dbg & 16) ? 2 : p.K / MM3_BK;
+    // this thread's weight unit: half kh (wave-uniform) of row ur's super-block, chunk uc
+    const int ur = (tid & 255) >> 2, uc = tid & 3;
 
     float16v acc[2][TM];
 #pragma unroll
@@ -533,58 +549,45 @@ __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-    // two register stages (A, B): step k+2's activation rows and raw weight blocks are
-    // loaded while step k computes and step k+1 is already in flight (the activation tile
-    // comes from L2 and its latency, not HBM or the MFMAs, bounded the one-stage loop:
-    // g_tune[13] experiments, profiles/r01/opbench_mmq_dbg.txt). Loads are unconditional
-    // (clamped to the last step) so the stages stay registers.
     uint4 raA[NA], raB[NA];
-    RawW<QT> rwA[UPT], rwB[UPT];
-    auto load = [&](uint4 (&ra)[NA], RawW<QT> (&rw)[UPT], int64_t kt) {
-        const int64_t k0 = min(kt, nk - 1) * MM_BK;
+    RawW<QT> rwA[1], rwB[1];
+    auto load = [&](uint4 (&ra)[NA], RawW<QT> (&rw)[1], int64_t kt) {   // unconditional, clamped
+        const int64_t k0 = min(kt, nk - 1) * MM3_BK;
 #pragma unroll
         for (int it = 0; it < NA; ++it) {
             const int unit = tid + NT * it;
-            const int t = unit >> 4, chn = unit & 15;
+            const int t = unit / MM3_CPR, chn = unit % MM3_CPR;
             const int64_t tok = min(tok0 + t, p.N - 1);
             ra[it] = *(const uint4 *) (xbase + ((p.dbg & 4) ? 8 * chn : tok * p.kp + k0 + 8 * chn));
         }
-#pragma unroll
-        for (int it = 0; it < UPT; ++it) {
-            const int unit = (tid + NT * it) % NU;
-            raw_load<QT>(p, wbase, (p.dbg & 1) ? row0 : row0 + (unit >> 2), (p.dbg & 1) ? 0 : k0, unit & 3, rw[it]);
-        }
+        raw_load<QT>(p, wbase, (p.dbg & 1) ? row0 : row0 + ur, (p.dbg & 1) ? 0 : k0 + 128 * kh, uc, rw[0]);
     };
-    auto store = [&](const uint4 (&ra)[NA], const RawW<QT> (&rw)[UPT], int64_t k0) {
+    auto store = [&](const uint4 (&ra)[NA], const RawW<QT> (&rw)[1], int64_t kt) {
+        const int64_t k0 = min(kt, nk - 1) * MM3_BK;
 #pragma unroll
         for (int it = 0; it < NA; ++it) {
             const int unit = tid + NT * it;
-            const int t = unit >> 4, chn = unit & 15;
-            lds_a[swz(t, chn)] = tok0 + t < p.N ? ra[it] : make_uint4(0, 0, 0, 0);
+            const int t = unit / MM3_CPR, chn = unit % MM3_CPR;
+            lds_a[swzn<MM3_CPR>(t, chn)] = tok0 + t < p.N ? ra[it] : make_uint4(0, 0, 0, 0);
         }
-#pragma unroll
-        for (int it = 0; it < UPT; ++it) {
-            const int unit = tid + NT * it;
-            if (unit < NU && !(p.dbg & 8))                    // wave-uniform
-                raw_store<QT>(rw[it], (int) k0, row0 + (unit >> 2) < p.M, unit >> 2, unit & 3, lds_b);
-        }
+        if (!(p.dbg & 8)) raw_store<QT, MM3_CPR>(rw[0], (int) (k0 + 128 * kh), row0 + ur < p.M, ur, uc, lds_b, 16 * kh);
     };
 
     const int r = lane & 31, hsel = lane >> 5;
     auto mfma_step = [&]() {
 #pragma unroll
-        for (int kq = 0; kq < MM_BK / 2; kq += 16) {
+        for (int kq = 0; kq < MM3_BK / 2; kq += 16) {
             if (p.dbg & 2) break;
-            const int chn = (kh * (MM_BK / 2) + kq) / 8 + hsel;
+            const int chn = (kh * (MM3_BK / 2) + kq) / 8 + hsel;
             half8 a[2], b[TM];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const uint4 va = lds_a[swz(wm * 64 + i * 32 + r, chn)];
+                const uint4 va = lds_a[swzn<MM3_CPR>(wm * 64 + i * 32 + r, chn)];
                 a[i] = *(const half8 *) &va;
             }
 #pragma unroll
             for (int j = 0; j < TM; ++j) {
-                const uint4 vb = lds_b[swz(wn * WM + j * 32 + r, chn)];
+                const uint4 vb = lds_b[swzn<MM3_CPR>(wn * WM + j * 32 + r, chn)];
                 b[j] = *(const half8 *) &vb;
             }
 #pragma unroll
@@ -598,20 +601,19 @@ __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
     load(raB, rwB, 1);
     store(raA, rwA, 0);
     __syncthreads();
-    // nk is even (K % 256 == 0): straight-line pairs, no exits — with early exits the
-    // waitcnt insertion fell back to vmcnt(0) at the loop head, draining the prefetch.
-    // The last pair stages a clamped copy of the last step that nothing reads.
+    // straight-line pairs (early exits made the waitcnt pass drain the prefetch at the
+    // loop head); an odd last step skips only its MFMAs
     for (int64_t kt = 0; kt < nk; kt += 2) {
         // LDS: step kt; B: step kt+1 in flight; A: free -> step kt+2
         load(raA, rwA, kt + 2);
         mfma_step();
         __syncthreads();
-        store(raB, rwB, (kt + 1) * MM_BK);
+        store(raB, rwB, kt + 1);
         __syncthreads();
         load(raB, rwB, kt + 3);
-        mfma_step();
+        if (kt + 1 < nk) mfma_step();                         // workgroup-uniform
         __syncthreads();
-        store(raA, rwA, min(kt + 2, nk - 1) * MM_BK);
+        store(raA, rwA, kt + 2);
         __syncthreads();
     }
     // K halves: waves 4-7 hand their accumulators to waves 0-3 (the loop ended on a barrier)
