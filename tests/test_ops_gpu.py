@@ -136,19 +136,22 @@ def test_rms_norm_fused_mul(pkg, backend, orc, ne0, nrows):
 
 
 @pytest.mark.parametrize("mode", [0, 2])
-def test_rope(pkg, backend, orc, mode):
+@pytest.mark.parametrize("ndims,heads", [(128, 8), (64, 8), (128, 1)])
+def test_rope(pkg, backend, orc, mode, ndims, heads):
+    """heads > 1: per-token table kernel (k_rope2), partial rotation with ndims < head dim;
+    heads = 1: per-row kernel"""
     rng = np.random.default_rng(11)
-    hd, heads, ntok = 128, 8, 5
+    hd, ntok = 128, 5
     x = rng.standard_normal((ntok, heads, hd)).astype(np.float32)
     pos = np.array([0, 1, 7, 300, 4095], np.int32)
 
     def build(ctx):
         tx = ctx.new_tensor("f32", hd, heads, ntok)
         tp = ctx.new_tensor("i32", ntok)
-        return [ctx.rope_ext(tx, tp, None, hd, mode, 8192, 500000.0)], [(tx, x), (tp, pos)]
+        return [ctx.rope_ext(tx, tp, None, ndims, mode, 8192, 500000.0)], [(tx, x), (tp, pos)]
 
     y = run(pkg, backend, build)[0].reshape(ntok, heads, hd)
-    ref = orc.rope(x, pos, hd, mode, 8192, 500000.0)
+    ref = orc.rope(x, pos, ndims, mode, 8192, 500000.0)
     assert nmse(y, ref) < 1e-7
 
 
