@@ -154,6 +154,8 @@ bool flash_attn_supported(const ggml_tensor * dst);
 // fused decode helpers (exec.cpp decides, kernels live in ops_mmvq.hip / ops_misc.hip)
 // y_gate/up = W·x ; out = act(gate) * up   (ggml-cuda.cu:2145-2181 semantics)
 bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * up_mm, ggml_tensor * glu);
+// the same node triple for a prefill ubatch on MFMA (k_mmq3g, ops_mm.hip)
+bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * up_mm, ggml_tensor * glu);
 // out = W·x + residual (MUL_MAT followed by ADD)
 bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * residual, ggml_tensor * add);
 // RMS_NORM → MUL(w) that also emits the quantised activation of its output

@@ -219,7 +219,7 @@ static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     else return false;
     if (uses[a] != 1 || uses[b] != 1 || ((a->flags | b->flags) & GGML_TENSOR_FLAG_OUTPUT)) return false;
     act_cache_invalidate(c.s, glu);
-    return mmvq_fused_glu(c, gate, up, glu);
+    return mmvq_fused_glu(c, gate, up, glu) || mmq_fused_glu(c, gate, up, glu);
 }
 
 static void run_node(OpCtx & c, ggml_tensor * n) {

@@ -27,6 +27,7 @@ constexpr int MM_BK = 128;   // K per step
 
 struct MmqArgs {
     const char * w; size_t w_row, w_c2, w_c3;
+    const char * w2;                         // k_mmq3g: the up matrix (same layout as w)
     const _Float16 * x; int64_t kp;          // activations f16 [cols][kp]
     float * dst; size_t d_col, d_c2, d_c3;   // in floats
     int64_t M, N, K, ne12, r2, r3;
@@ -644,6 +645,133 @@ __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
     }
 }
 
+// FFN gate/up/SwiGLU of a prefill ubatch in one pass (MUL_MAT(gate), MUL_MAT(up),
+// GLU(SWIGLU) — the decode form is gemv2 EPI 1): the k_mmq3 tile with two weight
+// matrices. Waves 0-3 multiply the shared 128-token activation tile by the gate rows,
+// waves 4-7 by the up rows, each over the whole 256-wide K step; the up half hands its
+// accumulators over through LDS and the gate half writes silu(g)·u. The activation tile
+// is staged once for both products, gate and up are never written, and the separate GLU
+// pass (a 88 MB read-write at pp512) disappears.
+template <int QT>
+__global__ __launch_bounds__(512, 2) void k_mmq3g(MmqArgs p) {
+    constexpr int NT = 512, BM = 64;
+    constexpr int WM = BM / 2, TM = WM / 32;
+    constexpr int NA = MM_BT * MM3_BK / 8 / NT;
+    constexpr int LB = BM * MM3_BK / 8;          // uint4 per weight tile
+    static_assert(2 * 4 * TM * 16 * 64 * 4 <= (MM_BT + 2 * BM) * MM3_BK * 2, "accumulator exchange fits the tiles");
+    __shared__ uint4 lds[(MM_BT + 2 * BM) * MM3_BK / 8];
+    uint4 * lds_a = lds;
+    uint4 * lds_b = lds + MM_BT * MM3_BK / 8;    // [gate | up]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int mh = wave >> 2, wq = wave & 3;     // matrix (0 gate, 1 up); place in the 2 x 2 wave grid
+    const int wm = wq >> 1, wn = wq & 1;
+    const int64_t tok0 = (int64_t) blockIdx.x * MM_BT;
+    const int64_t row0 = (int64_t) blockIdx.y * BM;
+    const _Float16 * xbase = p.x;
+    const int64_t nk = p.K / MM3_BK;
+    // this thread's two weight units: half hh of row ur's super-block, chunk uc, of gate and of up
+    const int hh = tid >> 8, ur = (tid & 255) >> 2, uc = tid & 3;
+
+    float16v acc[2][TM];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    uint4 raA[NA], raB[NA];
+    RawW<QT> rwA[2], rwB[2];
+    auto load = [&](uint4 (&ra)[NA], RawW<QT> (&rw)[2], int64_t kt) {   // unconditional, clamped
+        const int64_t k0 = min(kt, nk - 1) * MM3_BK;
+#pragma unroll
+        for (int it = 0; it < NA; ++it) {
+            const int unit = tid + NT * it;
+            const int t = unit / MM3_CPR, chn = unit % MM3_CPR;
+            const int64_t tok = min(tok0 + t, p.N - 1);
+            ra[it] = *(const uint4 *) (xbase + tok * p.kp + k0 + 8 * chn);
+        }
+        raw_load<QT>(p, p.w, row0 + ur, k0 + 128 * hh, uc, rw[0]);
+        raw_load<QT>(p, p.w2, row0 + ur, k0 + 128 * hh, uc, rw[1]);
+    };
+    auto store = [&](const uint4 (&ra)[NA], const RawW<QT> (&rw)[2], int64_t kt) {
+        const int64_t k0 = min(kt, nk - 1) * MM3_BK;
+#pragma unroll
+        for (int it = 0; it < NA; ++it) {
+            const int unit = tid + NT * it;
+            const int t = unit / MM3_CPR, chn = unit % MM3_CPR;
+            lds_a[swzn<MM3_CPR>(t, chn)] = tok0 + t < p.N ? ra[it] : make_uint4(0, 0, 0, 0);
+        }
+        raw_store<QT, MM3_CPR>(rw[0], (int) (k0 + 128 * hh), row0 + ur < p.M, ur, uc, lds_b, 16 * hh);
+        raw_store<QT, MM3_CPR>(rw[1], (int) (k0 + 128 * hh), row0 + ur < p.M, ur, uc, lds_b + LB, 16 * hh);
+    };
+
+    const int r = lane & 31, hsel = lane >> 5;
+    const uint4 * lbm = lds_b + mh * LB;
+    auto mfma_step = [&]() {
+#pragma unroll
+        for (int kk = 0; kk < MM3_BK; kk += 16) {
+            const int chn = kk / 8 + hsel;
+            half8 a[2], b[TM];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint4 va = lds_a[swzn<MM3_CPR>(wm * 64 + i * 32 + r, chn)];
+                a[i] = *(const half8 *) &va;
+            }
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                const uint4 vb = lbm[swzn<MM3_CPR>(wn * WM + j * 32 + r, chn)];
+                b[j] = *(const half8 *) &vb;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < TM; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    load(raA, rwA, 0);
+    load(raB, rwB, 1);
+    store(raA, rwA, 0);
+    __syncthreads();
+    for (int64_t kt = 0; kt < nk; kt += 2) {
+        load(raA, rwA, kt + 2);
+        mfma_step();
+        __syncthreads();
+        store(raB, rwB, kt + 1);
+        __syncthreads();
+        load(raB, rwB, kt + 3);
+        if (kt + 1 < nk) mfma_step();                          // workgroup-uniform
+        __syncthreads();
+        store(raA, rwA, kt + 2);
+        __syncthreads();
+    }
+    float * red = (float *) lds;
+    if (mh == 1) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) red[(((wq * 2 + i) * TM + j) * 16 + e) * 64 + lane] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (mh == 1) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+            const int64_t wrow = row0 + wn * WM + j * 32 + (lane & 31);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const float g = acc[i][j][e], u = red[(((wq * 2 + i) * TM + j) * 16 + e) * 64 + lane];
+                const int64_t tok = tok0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+                if (tok < p.N && wrow < p.M) p.dst[tok * p.d_col + wrow] = (g / (1.0f + expf(-g))) * u;
+            }
+        }
+    }
+}
+
 static bool g_mmq_v1 = getenv("GGML_MI355X_MMQ_V1") != nullptr;
 
 bool mmq_type_ok(int t) {
@@ -664,10 +792,9 @@ size_t mmq_scratch(const ggml_tensor * dst) {
     return ncols * mmq_kp(dst) * 2 + 256;
 }
 
-void mmq_run(OpCtx & c, ggml_tensor * dst) {
-    const ggml_tensor * w = dst->src[0];
-    const ggml_tensor * x = dst->src[1];
-    const int64_t kp = mmq_kp(dst);
+// f32 activation -> f16 rows padded to kp, cached by (tensor, K, ncols) so GEMMs that
+// share their input (q/k/v, gate/up) convert it once
+static _Float16 * mmq_act(OpCtx & c, const ggml_tensor * x, int64_t kp) {
     const int64_t ncols = x->ne[1] * x->ne[2] * x->ne[3];
     const size_t abytes = (size_t) ncols * kp * 2;
     Stream * s = c.s;
@@ -684,6 +811,14 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
         if (cacheable) { s->f16_src = x->data; memcpy(s->f16_key, key, sizeof key); }
         else s->f16_src = nullptr;
     }
+    return xa;
+}
+
+void mmq_run(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    const int64_t kp = mmq_kp(dst);
+    _Float16 * xa = mmq_act(c, x, kp);
     MmqArgs p{};
     p.w = (const char *) w->data; p.w_row = w->nb[1]; p.w_c2 = w->nb[2]; p.w_c3 = w->nb[3];
     p.x = xa; p.kp = kp;
@@ -720,6 +855,37 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
 #undef MQ
         default: MX_ABORT("mmq type %d", (int) w->type);
     }
+}
+
+static bool mmq_ok(const ggml_tensor * dst);
+static const bool g_mmq_glu_off = getenv("GGML_MI355X_NO_MMQ_GLU") != nullptr;
+
+bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu) {
+    const ggml_tensor * wg = gate->src[0], * wu = up->src[0];
+    const ggml_tensor * x = gate->src[1];
+    if (g_mmq_glu_off || g_mmq_v1 || up->src[1] != x || wg->type != wu->type) return false;
+    if (wg->type != GGML_TYPE_Q4_K && wg->type != GGML_TYPE_Q5_K && wg->type != GGML_TYPE_Q6_K) return false;
+    if (mx_op_param<int32_t>(glu, 0) != GGML_GLU_OP_SWIGLU || mx_op_param<int32_t>(glu, 1) != 0) return false;
+    if (x->type != GGML_TYPE_F32 || x->ne[1] <= 8 || x->ne[2] != 1 || x->ne[3] != 1) return false;
+    for (int i = 0; i < 4; ++i) if (wg->ne[i] != wu->ne[i] || wg->nb[i] != wu->nb[i]) return false;
+    if (wg->ne[2] != 1 || wg->ne[3] != 1 || wg->ne[0] % 256 || x->ne[0] != wg->ne[0]) return false;
+    if (!mmq_ok(gate) || !mmq_ok(up)) return false;
+    if (glu->type != GGML_TYPE_F32 || glu->nb[0] != 4 || glu->ne[0] != wg->ne[1] || glu->ne[1] != x->ne[1]) return false;
+    deferred_guard_read(c, x);
+    deferred_guard_write(c, glu);
+    const int64_t kp = mmq_kp(gate);
+    MmqArgs p{};
+    p.w = (const char *) wg->data; p.w2 = (const char *) wu->data; p.w_row = wg->nb[1];
+    p.x = mmq_act(c, x, kp); p.kp = kp;
+    p.dst = (float *) glu->data; p.d_col = glu->nb[1] / 4;
+    p.M = wg->ne[1]; p.N = x->ne[1]; p.K = wg->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1;
+    const dim3 g((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, 64), 1);
+    switch (wg->type) {
+        case GGML_TYPE_Q4_K: k_mmq3g<GGML_TYPE_Q4_K><<<g, 512, 0, c.st>>>(p); break;
+        case GGML_TYPE_Q5_K: k_mmq3g<GGML_TYPE_Q5_K><<<g, 512, 0, c.st>>>(p); break;
+        default:             k_mmq3g<GGML_TYPE_Q6_K><<<g, 512, 0, c.st>>>(p); break;
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------

@@ -173,27 +173,29 @@ def test_soft_max_masked(pkg, backend, orc, ne00, ne01, heads):
     assert nmse(y, ref) < 1e-6
 
 
-@pytest.mark.parametrize("tname", ["q4_K", "q6_K"])
-def test_fused_gate_up_swiglu(pkg, backend, orc, tname):
+@pytest.mark.parametrize("tname", ["q4_K", "q6_K", "q5_K"])
+@pytest.mark.parametrize("N", [1, 150])
+def test_fused_gate_up_swiglu(pkg, backend, orc, tname, N):
+    """N = 1: decode GEMV (gemv2 EPI 1); N = 150: prefill k_mmq3g (ragged token and row tiles)"""
     tid = NAMES[tname]
     rng = np.random.default_rng(21)
-    K, M = 1024, 512
+    K, M = 1024, (512 if N == 1 else 200)
     wg, rb = rand_quant(tid, M, K, rng)
     wu, _ = rand_quant(tid, M, K, rng)
-    x = rng.standard_normal((1, K)).astype(np.float32)
+    x = rng.standard_normal((N, K)).astype(np.float32)
     before = backend.stats()["nodes_fused"]
 
     def build(ctx):
         tg = ctx.new_tensor(tid, K, M)
         tu = ctx.new_tensor(tid, K, M)
-        tx = ctx.new_tensor("f32", K, 1)
+        tx = ctx.new_tensor("f32", K, N)
         up = ctx.mul_mat(tu, tx)
         gate = ctx.mul_mat(tg, tx)
         return [ctx.swiglu_split(gate, up)], [(tg, wg), (tu, wu), (tx, x)]
 
-    y = run(pkg, backend, build)[0].reshape(M)
-    g = orc.mul_mat(tid, wg, rb, x, exact=True)[0]
-    u = orc.mul_mat(tid, wu, rb, x, exact=True)[0]
+    y = run(pkg, backend, build)[0].reshape(N, M)
+    g = orc.mul_mat(tid, wg, rb, x, exact=True)
+    u = orc.mul_mat(tid, wu, rb, x, exact=True)
     ref = orc.swiglu(g, u)
     assert nmse(y, ref) < 5e-4
     assert backend.stats()["nodes_fused"] >= before + 2, "gate/up/GLU fusion did not fire"
