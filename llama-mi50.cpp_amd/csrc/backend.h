@@ -86,10 +86,13 @@ struct Stream {
     Scratch scratch;
     Scratch act;                       // ring of quantised activations (act_cache)
     ActCacheEntry act_cache[4];
-    // f16 copy of the last prefill GEMM activation (q/k/v and gate/up share one)
+    // f16 copies of prefill GEMM activations (q/k/v and gate/up share one), two slots of
+    // f16.cap bytes each: a kernel can read one while writing the next GEMM's input to the
+    // other (fused SwiGLU -> down projection); f16_last = the slot used most recently
     Scratch f16;
-    const void * f16_src = nullptr;
-    int64_t f16_key[4] = {0, 0, 0, 0};       // K, ncols, nb1, kp
+    const void * f16_src[2] = {nullptr, nullptr};
+    int64_t f16_key[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};   // K, ncols, nb1, kp
+    int f16_last = 0;
     int act_next = 0;
     size_t act_slot = 0;               // bytes per ring slot
     GraphCache gcache;
@@ -156,6 +159,9 @@ bool flash_attn_supported(const ggml_tensor * dst);
 bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * up_mm, ggml_tensor * glu);
 // the same node triple for a prefill ubatch on MFMA (k_mmq3g, ops_mm.hip)
 bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * up_mm, ggml_tensor * glu);
+bool mmq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, ggml_tensor * add);
+// f16 act-cache slot for a producer's f32 output rows (ops_mm.hip); null if it does not fit
+_Float16 * mmq_act_claim(OpCtx & c, const void * data, int64_t K, int64_t ncols, size_t row_bytes);
 // out = W·x + residual (MUL_MAT followed by ADD)
 bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * residual, ggml_tensor * add);
 // RMS_NORM → MUL(w) that also emits the quantised activation of its output

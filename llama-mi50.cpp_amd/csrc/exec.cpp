@@ -197,9 +197,9 @@ static bool try_fuse_mm_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     if (add->op != GGML_OP_ADD) return false;
     const ggml_tensor * res = add->src[0] == mm ? add->src[1] : (add->src[1] == mm ? add->src[0] : nullptr);
     if (!res || res == mm || uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return false;
-    if (!mmvq_small_batch_ok(mm)) return false;
     act_cache_invalidate(c.s, add);
-    return mmvq_fused_add(c, mm, res, add);
+    if (mmvq_small_batch_ok(mm)) return mmvq_fused_add(c, mm, res, add);
+    return mmq_fused_add(c, mm, res, add);
 }
 
 // MUL_MAT(gate) , MUL_MAT(up) , GLU(gate, up) with one activation column:
@@ -315,9 +315,9 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     if (f16need > s->f16.cap) {
         HIP_CHECK(hipStreamSynchronize(s->stream));
         if (s->f16.base) HIP_CHECK(hipFree(s->f16.base));
-        HIP_CHECK(hipMalloc((void **) &s->f16.base, f16need));
+        HIP_CHECK(hipMalloc((void **) &s->f16.base, 2 * f16need));
         s->f16.cap = f16need;
-        s->f16_src = nullptr;
+        s->f16_src[0] = s->f16_src[1] = nullptr;
         s->gcache.key.clear();
     }
     if (need > s->scratch.cap) {

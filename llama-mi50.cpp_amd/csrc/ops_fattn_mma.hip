@@ -25,6 +25,7 @@ struct FaMmaArgs {
     const char * v; size_t v1, v2;
     const char * mask; size_t m1;         // f16 [n_kv, n_q] or null
     char * dst; size_t d1, d2;            // f32 [D, H, n_q]
+    _Float16 * h;                         // k_fa_mma2: also f16 [n_q][H * D] (act cache) or null
     int n_q, n_kv, H, Hkv;
     float scale;
 };
@@ -433,6 +434,16 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
             for (int g = 0; g < 4; ++g)
                 *(float4 *) (out + 32 * t + 8 * g + 4 * hl) = make_float4(acc_o[t][4 * g] * inv, acc_o[t][4 * g + 1] * inv,
                                                                          acc_o[t][4 * g + 2] * inv, acc_o[t][4 * g + 3] * inv);
+        if (p.h) {      // the output projection's f16 input row (act cache)
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            _Float16 * ho = p.h + (size_t) (qw + l32) * p.H * D + (size_t) h * D;
+#pragma unroll
+            for (int t = 0; t < NDT; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    *(h4 *) (ho + 32 * t + 8 * g + 4 * hl) = h4{(_Float16) (acc_o[t][4 * g] * inv), (_Float16) (acc_o[t][4 * g + 1] * inv),
+                                                               (_Float16) (acc_o[t][4 * g + 2] * inv), (_Float16) (acc_o[t][4 * g + 3] * inv)};
+        }
     }
 #undef FM2_LOAD_KV
 }
@@ -470,6 +481,9 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
     p.scale = mx_op_param<float>(dst, 0);
     if (k->ne[0] == 128 && k->ne[1] >= 4 && !g_fa_mma1 && (dst->nb[1] % 16) == 0 && ((uintptr_t) dst->data % 16) == 0) {
         const int Gt = p.H / p.Hkv, HG = Gt % 4 == 0 ? 4 : (Gt % 2 == 0 ? 2 : 1);
+        // contiguous [D, H, n_q] output: the output projection reads it as [H*D, n_q] rows
+        if (dst->nb[1] == 4 * (size_t) k->ne[0] && dst->nb[2] == (size_t) 4 * k->ne[0] * p.H && dst->ne[3] == 1)
+            p.h = mmq_act_claim(c, dst->data, k->ne[0] * p.H, p.n_q, dst->nb[2]);
         const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32 * (4 / HG)), (unsigned) (p.Hkv * (Gt / HG)));
         if (HG == 4) k_fa_mma2<4><<<g2, 256, 0, c.st>>>(p);
         else if (HG == 2) k_fa_mma2<2><<<g2, 256, 0, c.st>>>(p);

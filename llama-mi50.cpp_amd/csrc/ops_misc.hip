@@ -490,7 +490,7 @@ __global__ void k_rms_norm(const char * __restrict__ x, const char * __restrict_
 // norm against ~3 µs of traffic).
 template <bool MUL, int VPT>
 __global__ __launch_bounds__(256) void k_rms_norm_v4(const char * __restrict__ x, const char * __restrict__ w, char * __restrict__ y,
-                                                     T4 gx, T4 gw, T4 gy, float eps) {
+                                                     T4 gx, T4 gw, T4 gy, float eps, _Float16 * __restrict__ h) {
     __shared__ float lds[16];
     const int64_t r = blockIdx.x;
     const int64_t i1 = r % gx.ne[1], i2 = (r / gx.ne[1]) % gx.ne[2], i3 = r / (gx.ne[1] * gx.ne[2]);
@@ -515,6 +515,10 @@ __global__ __launch_bounds__(256) void k_rms_norm_v4(const char * __restrict__ x
         float4 o = make_float4(v[j].x * scale, v[j].y * scale, v[j].z * scale, v[j].w * scale);
         if constexpr (MUL) { const float4 wv = pw[i]; o.x *= wv.x; o.y *= wv.y; o.z *= wv.z; o.w *= wv.w; }
         py[i] = o;
+        if (h) {   // the f16 row a following prefill GEMM reads (act cache, contiguous rows)
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            *(h4 *) (h + r * gx.ne[0] + 4 * i) = h4{(_Float16) o.x, (_Float16) o.y, (_Float16) o.z, (_Float16) o.w};
+        }
     }
 }
 
@@ -529,7 +533,8 @@ void op_rms_norm(OpCtx & c, ggml_tensor * norm, const ggml_tensor * mul, ggml_te
         const int vpt = (int) mx_ceil_div(x->ne[0] / 4, 256);
         const T4 gw = mul ? geo(mul) : geo(x);
         const char * wp = mul ? (const char *) mul->data : nullptr;
-#define RN(M, V) k_rms_norm_v4<M, V><<<(unsigned) nr, 256, 0, c.st>>>((const char *) x->data, wp, (char *) out->data, geo(x), gw, geo(out), eps)
+        _Float16 * h = mx_is_contiguous(out) && out->ne[2] == 1 && out->ne[3] == 1 ? mmq_act_claim(c, out->data, out->ne[0], out->ne[1], out->nb[1]) : nullptr;
+#define RN(M, V) k_rms_norm_v4<M, V><<<(unsigned) nr, 256, 0, c.st>>>((const char *) x->data, wp, (char *) out->data, geo(x), gw, geo(out), eps, h)
         if (mul) { if (vpt <= 2) RN(true, 2); else if (vpt <= 4) RN(true, 4); else RN(true, 8); }
         else     { if (vpt <= 2) RN(false, 2); else if (vpt <= 4) RN(false, 4); else RN(false, 8); }
 #undef RN

@@ -28,6 +28,8 @@ constexpr int MM_BK = 128;   // K per step
 struct MmqArgs {
     const char * w; size_t w_row, w_c2, w_c3;
     const char * w2;                         // k_mmq3g: the up matrix (same layout as w)
+    _Float16 * h; int64_t h_col;             // k_mmq3g: also the f16 copy of the output (act cache)
+    const float * res; size_t r_col;         // k_mmq2/k_mmq3: + residual (MUL_MAT -> ADD), in floats
     const _Float16 * x; int64_t kp;          // activations f16 [cols][kp]
     float * dst; size_t d_col, d_c2, d_c3;   // in floats
     int64_t M, N, K, ne12, r2, r3;
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(256, 2) void k_mmq2(MmqArgs p) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int64_t tok = tok0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
-                if (tok < p.N && wrow < p.M) dbase[tok * p.d_col + wrow] = acc[i][j][e];
+                if (tok < p.N && wrow < p.M) dbase[tok * p.d_col + wrow] = acc[i][j][e] + (p.res ? p.res[tok * p.r_col + wrow] : 0.f);
             }
         }
     }
@@ -639,7 +641,7 @@ __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
             for (int e = 0; e < 16; ++e) {
                 const float v = acc[i][j][e] + red[(((wq * 2 + i) * TM + j) * 16 + e) * 64 + lane];
                 const int64_t tok = tok0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
-                if (tok < p.N && wrow < p.M) dbase[tok * p.d_col + wrow] = v;
+                if (tok < p.N && wrow < p.M) dbase[tok * p.d_col + wrow] = v + (p.res ? p.res[tok * p.r_col + wrow] : 0.f);
             }
         }
     }
@@ -766,13 +768,18 @@ __global__ __launch_bounds__(512, 2) void k_mmq3g(MmqArgs p) {
             for (int e = 0; e < 16; ++e) {
                 const float g = acc[i][j][e], u = red[(((wq * 2 + i) * TM + j) * 16 + e) * 64 + lane];
                 const int64_t tok = tok0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
-                if (tok < p.N && wrow < p.M) p.dst[tok * p.d_col + wrow] = (g / (1.0f + expf(-g))) * u;
+                const float v = (g / (1.0f + expf(-g))) * u;
+                if (tok < p.N && wrow < p.M) {
+                    p.dst[tok * p.d_col + wrow] = v;
+                    if (p.h) p.h[tok * p.h_col + wrow] = (_Float16) v;
+                }
             }
         }
     }
 }
 
 static bool g_mmq_v1 = getenv("GGML_MI355X_MMQ_V1") != nullptr;
+static const bool g_act_claim_off = getenv("GGML_MI355X_NO_ACT_CLAIM") != nullptr;   // A/B
 
 bool mmq_type_ok(int t) {
     switch (t) {
@@ -792,6 +799,21 @@ size_t mmq_scratch(const ggml_tensor * dst) {
     return ncols * mmq_kp(dst) * 2 + 256;
 }
 
+// A producer of a prefill GEMM's input (RMS norm, attention, fused SwiGLU) writes the f16
+// copy itself: it claims the cache slot for its f32 output rows (data, K, ncols, row
+// stride) and the GEMM's mmq_act finds it — no separate conversion pass. Rows of K %
+// 128 == 0 only (kp == K, no padding to write); null when the slot does not fit.
+_Float16 * mmq_act_claim(OpCtx & c, const void * data, int64_t K, int64_t ncols, size_t row_bytes) {
+    Stream * s = c.s;
+    if (g_act_claim_off || K % MM_BK || ncols <= 8 || !s->f16.base || (size_t) K * ncols * 2 > s->f16.cap) return nullptr;
+    const int64_t key[4] = {K, ncols, (int64_t) row_bytes, K};
+    const int k = 1 - s->f16_last;             // not the slot the running kernel may be reading
+    s->f16_src[k] = data;
+    memcpy(s->f16_key[k], key, sizeof key);
+    s->f16_last = k;
+    return (_Float16 *) s->f16.base + (size_t) k * (s->f16.cap / 2);
+}
+
 // f32 activation -> f16 rows padded to kp, cached by (tensor, K, ncols) so GEMMs that
 // share their input (q/k/v, gate/up) convert it once
 static _Float16 * mmq_act(OpCtx & c, const ggml_tensor * x, int64_t kp) {
@@ -801,20 +823,24 @@ static _Float16 * mmq_act(OpCtx & c, const ggml_tensor * x, int64_t kp) {
     _Float16 * xa;
     const int64_t key[4] = {x->ne[0], ncols, (int64_t) x->nb[1], kp};
     const bool cacheable = s->f16.base && abytes <= s->f16.cap && mx_is_contiguous(x);
-    if (cacheable && s->f16_src == x->data && !memcmp(s->f16_key, key, sizeof key)) {
-        xa = (_Float16 *) s->f16.base;      // same activation as the previous GEMM (q/k/v, gate/up)
-    } else {
-        xa = cacheable ? (_Float16 *) s->f16.base : (_Float16 *) c.scratch->take(abytes);
-        dim3 grid((unsigned) mx_ceil_div(kp, 8 * 256), (unsigned) ncols);
-        k_act_f16<<<grid, 256, 0, c.st>>>((const char *) x->data, x->ne[0], x->ne[1], x->ne[2],
-                                          x->nb[0], x->nb[1], x->nb[2], x->nb[3], kp, xa);
-        if (cacheable) { s->f16_src = x->data; memcpy(s->f16_key, key, sizeof key); }
-        else s->f16_src = nullptr;
-    }
+    auto slot = [&](int k) { return (_Float16 *) s->f16.base + (size_t) k * (s->f16.cap / 2); };
+    for (int k = 0; k < 2 && cacheable; ++k)
+        if (s->f16_src[k] == x->data && !memcmp(s->f16_key[k], key, sizeof key)) {
+            s->f16_last = k;                // same activation as an earlier GEMM / its producer
+            return slot(k);
+        }
+    const int k = 1 - s->f16_last;
+    xa = cacheable ? slot(k) : (_Float16 *) c.scratch->take(abytes);
+    dim3 grid((unsigned) mx_ceil_div(kp, 8 * 256), (unsigned) ncols);
+    k_act_f16<<<grid, 256, 0, c.st>>>((const char *) x->data, x->ne[0], x->ne[1], x->ne[2],
+                                      x->nb[0], x->nb[1], x->nb[2], x->nb[3], kp, xa);
+    if (cacheable) { s->f16_src[k] = x->data; memcpy(s->f16_key[k], key, sizeof key); s->f16_last = k; }
     return xa;
 }
 
-void mmq_run(OpCtx & c, ggml_tensor * dst) {
+// out (default dst) receives the product, + res when given (K-quant MFMA kernels only:
+// the caller checks mmq_kq_ok)
+static void mmq_run_ex(OpCtx & c, ggml_tensor * dst, ggml_tensor * out, const ggml_tensor * res) {
     const ggml_tensor * w = dst->src[0];
     const ggml_tensor * x = dst->src[1];
     const int64_t kp = mmq_kp(dst);
@@ -822,7 +848,8 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
     MmqArgs p{};
     p.w = (const char *) w->data; p.w_row = w->nb[1]; p.w_c2 = w->nb[2]; p.w_c3 = w->nb[3];
     p.x = xa; p.kp = kp;
-    p.dst = (float *) dst->data; p.d_col = dst->nb[1] / 4; p.d_c2 = dst->nb[2] / 4; p.d_c3 = dst->nb[3] / 4;
+    p.dst = (float *) out->data; p.d_col = out->nb[1] / 4; p.d_c2 = out->nb[2] / 4; p.d_c3 = out->nb[3] / 4;
+    if (res) { p.res = (const float *) res->data; p.r_col = res->nb[1] / 4; }
     p.M = w->ne[1]; p.N = x->ne[1]; p.K = w->ne[0]; p.ne12 = x->ne[2];
     p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
     p.dbg = g_tune[13];
@@ -846,6 +873,7 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
         switch (w->type) { MQ2(GGML_TYPE_Q4_K) MQ2(GGML_TYPE_Q5_K) MQ2(GGML_TYPE_Q6_K) default: break; }
 #undef MQ2
     }
+    MX_ASSERT(!res && out == dst);
     dim3 grid((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, MM_BW), (unsigned) (x->ne[2] * x->ne[3]));
     switch (w->type) {
 #define MQ(T) case T: k_mmq<T><<<grid, 256, 0, c.st>>>(p); break;
@@ -857,8 +885,28 @@ void mmq_run(OpCtx & c, ggml_tensor * dst) {
     }
 }
 
+void mmq_run(OpCtx & c, ggml_tensor * dst) { mmq_run_ex(c, dst, dst, nullptr); }
+
 static bool mmq_ok(const ggml_tensor * dst);
+// A/B: GGML_MI355X_NO_MMQ_GLU=1 turns off the prefill GEMM fusions (gate/up/SwiGLU, + residual)
 static const bool g_mmq_glu_off = getenv("GGML_MI355X_NO_MMQ_GLU") != nullptr;
+
+// MUL_MAT -> ADD(mm, residual) of a prefill ubatch: the residual is added in the GEMM
+// epilogue (attention output and FFN down projections: no product round trip, no ADD pass)
+bool mmq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, ggml_tensor * add) {
+    const ggml_tensor * w = mm->src[0], * x = mm->src[1];
+    const bool kq = w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
+    if (!kq || g_mmq_v1 || g_mmq_glu_off || w->ne[0] % 256 || x->ne[1] <= 8 || !mmq_ok(mm)) return false;
+    if (x->ne[2] != 1 || x->ne[3] != 1 || w->ne[2] != 1 || w->ne[3] != 1) return false;
+    if (res->type != GGML_TYPE_F32 || add->type != GGML_TYPE_F32 || !mx_are_same_shape(res, mm) || !mx_are_same_shape(add, mm)) return false;
+    if (res->nb[0] != 4 || add->nb[0] != 4 || res->nb[1] % 4 || add->nb[1] % 4) return false;
+    deferred_guard_read(c, x);
+    deferred_guard_read(c, res);
+    deferred_guard_write(c, add);
+    mmq_run_ex(c, const_cast<ggml_tensor *>(mm), add, res);
+    return true;
+}
+
 
 bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu) {
     const ggml_tensor * wg = gate->src[0], * wu = up->src[0];
@@ -879,6 +927,10 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, 
     p.x = mmq_act(c, x, kp); p.kp = kp;
     p.dst = (float *) glu->data; p.d_col = glu->nb[1] / 4;
     p.M = wg->ne[1]; p.N = x->ne[1]; p.K = wg->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1;
+    // the down projection reads this output: write its f16 copy too (claimed after the
+    // input conversion above, which used the same slot)
+    p.h = mmq_act_claim(c, glu->data, glu->ne[0], glu->ne[1], glu->nb[1]);
+    p.h_col = glu->ne[0];
     const dim3 g((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, 64), 1);
     switch (wg->type) {
         case GGML_TYPE_Q4_K: k_mmq3g<GGML_TYPE_Q4_K><<<g, 512, 0, c.st>>>(p); break;

@@ -102,16 +102,17 @@ static size_t slot_bytes_raw(int64_t ne0, int64_t ncols) {
 void act_cache_reset(Stream * s) {
     for (auto & e : s->act_cache) e = ActCacheEntry{};
     s->act_next = 0;
-    s->f16_src = nullptr;
+    s->f16_src[0] = s->f16_src[1] = nullptr;
 }
 
 void act_cache_invalidate(Stream * s, const ggml_tensor * w) {
     const char * lo = (const char *) w->data;
     const char * hi = lo + mx_nbytes(w);
-    if (s->f16_src) {
-        const char * a = (const char *) s->f16_src;
-        const char * b = a + (size_t) s->f16_key[1] * (size_t) s->f16_key[2];
-        if (a < hi && lo < b) s->f16_src = nullptr;
+    for (int k = 0; k < 2; ++k) {
+        if (!s->f16_src[k]) continue;
+        const char * a = (const char *) s->f16_src[k];
+        const char * b = a + (size_t) s->f16_key[k][1] * (size_t) s->f16_key[k][2];
+        if (a < hi && lo < b) s->f16_src[k] = nullptr;
     }
     for (auto & e : s->act_cache) {
         if (!e.data) continue;

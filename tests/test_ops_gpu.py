@@ -173,6 +173,30 @@ def test_soft_max_masked(pkg, backend, orc, ne00, ne01, heads):
     assert nmse(y, ref) < 1e-6
 
 
+@pytest.mark.parametrize("tname", ["q4_K", "q6_K"])
+@pytest.mark.parametrize("N", [1, 150])
+def test_fused_mul_mat_add(pkg, backend, orc, tname, N):
+    """MUL_MAT -> ADD(residual): decode GEMV epilogue (N = 1), prefill GEMM epilogue (N = 150)"""
+    tid = NAMES[tname]
+    rng = np.random.default_rng(31)
+    K, M = 1024, 200
+    w, rb = rand_quant(tid, M, K, rng)
+    x = rng.standard_normal((N, K)).astype(np.float32)
+    r = rng.standard_normal((N, M)).astype(np.float32)
+    before = backend.stats()["nodes_fused"]
+
+    def build(ctx):
+        tw = ctx.new_tensor(tid, K, M)
+        tx = ctx.new_tensor("f32", K, N)
+        tr = ctx.new_tensor("f32", M, N)
+        return [ctx.add(ctx.mul_mat(tw, tx), tr)], [(tw, w), (tx, x), (tr, r)]
+
+    y = run(pkg, backend, build)[0].reshape(N, M)
+    ref = orc.mul_mat(tid, w, rb, x, exact=True) + r
+    assert nmse(y, ref) < 5e-4
+    assert backend.stats()["nodes_fused"] >= before + 1, "MUL_MAT -> ADD fusion did not fire"
+
+
 @pytest.mark.parametrize("tname", ["q4_K", "q6_K", "q5_K"])
 @pytest.mark.parametrize("N", [1, 150])
 def test_fused_gate_up_swiglu(pkg, backend, orc, tname, N):
