@@ -160,6 +160,8 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * 
 // the same node triple for a prefill ubatch on MFMA (k_mmq3g, ops_mm.hip)
 bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * up_mm, ggml_tensor * glu);
 bool mmq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, ggml_tensor * add);
+// 2-3 prefill GEMMs sharing src1 (q/k/v) in one launch (k_mmq3m); false if not eligible (nothing run)
+bool mmq_group_run(OpCtx & c, ggml_tensor * const * mms, int n);
 // f16 act-cache slot for a producer's f32 output rows (ops_mm.hip); null if it does not fit
 _Float16 * mmq_act_claim(OpCtx & c, const void * data, int64_t K, int64_t ncols, size_t row_bytes);
 // out = W·x + residual (MUL_MAT followed by ADD)

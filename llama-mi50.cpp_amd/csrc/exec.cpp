@@ -252,6 +252,41 @@ static void run_node(OpCtx & c, ggml_tensor * n) {
 
 static bool g_sync_debug = getenv("GGML_MI355X_SYNC_DEBUG") != nullptr;
 
+// Prefill q/k/v: the MUL_MATs that share this one's src1 within the next few nodes run
+// in one launch here (mmq_group_run). The later members move ahead of the nodes between
+// (q's RoPE in libllama's order), so those must not touch their outputs — the allocator
+// may place a later member's output over a tensor that dies in between — nor write x or
+// the weights.
+static bool try_group_mm(OpCtx & c, ggml_cgraph * g, int i, std::unordered_map<const ggml_tensor *, int> & done) {
+    ggml_tensor * n0 = g->nodes[i];
+    const ggml_tensor * x = n0->src[1];
+    if (!x || x->ne[1] <= 8 || g_no_qkv) return false;
+    ggml_tensor * mm[3] = {n0};
+    int pos[3] = {i}, nm = 1;
+    std::vector<int> between;
+    for (int j = i + 1; j < g->n_nodes && j < i + 24 && nm < 3; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (is_view_op(n->op) || mx_is_empty(n)) continue;
+        if (n->op == GGML_OP_MUL_MAT && n->src[1] == x) { mm[nm] = n; pos[nm++] = j; continue; }
+        between.push_back(j);
+        if (between.size() > 6) break;
+    }
+    if (nm < 2) return false;
+    for (int k = 1; k < nm; ++k)
+        for (int j : between) {
+            if (j > pos[k]) continue;
+            const ggml_tensor * b = g->nodes[j];
+            if (t_overlaps(b, mm[k]) || t_overlaps(b, x) || t_overlaps(b, mm[k]->src[0])) return false;
+            for (int s = 0; s < GGML_MAX_SRC; ++s) if (b->src[s] && t_overlaps(b->src[s], mm[k])) return false;
+        }
+    for (int k = 0; k < nm; ++k) { deferred_guard_node(c, mm[k]); act_cache_invalidate(c.s, mm[k]); }
+    if (!mmq_group_run(c, mm, nm)) return false;
+    for (int k = 1; k < nm; ++k) done[mm[k]] = 1;
+    c.s->n_fused += nm - 1;
+    c.s->n_nodes_run += nm;
+    return true;
+}
+
 static void run_nodes(Stream * s, ggml_cgraph * g) {
     OpCtx c{s, s->stream, &s->scratch};
     static thread_local UseMap uses;
@@ -264,9 +299,12 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
     act_cache_reset(s);
     s->deferred.clear();
     s->rope_valid = false;
+    static thread_local std::unordered_map<const ggml_tensor *, int> done;   // run ahead by a group
+    done.clear();
     for (int i = 0; i < g->n_nodes; ++i) {
         ggml_tensor * n = g->nodes[i];
         if (is_view_op(n->op) || mx_is_empty(n)) continue;
+        if (!done.empty() && done.count(n)) continue;
         s->scratch.reset();
         if (s->use_fusion) {
             if (n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }
@@ -276,6 +314,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
                 if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; continue; }
             }
             if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
+            if (n->op == GGML_OP_MUL_MAT && try_group_mm(c, g, i, done)) continue;
             if (n->op == GGML_OP_MUL_MAT && try_fuse_mm_add(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
         }
         deferred_guard_node(c, n);

@@ -520,22 +520,21 @@ __global__ __launch_bounds__(256, 2) void k_mmq2(MmqArgs p) {
 constexpr int MM3_BK = 256;
 constexpr int MM3_CPR = MM3_BK / 8;             // 16-byte chunks per LDS row
 
+// one 128-token x BM-row output tile (blocks x: tokens, z: batch; the rows are row0..)
 template <int QT, int BM>
-__global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
+__device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, uint4 * lds) {
     constexpr int NT = 512;
     static_assert(BM * 8 == NT, "one weight unit per thread");
     constexpr int WM = BM / 2;                  // weight rows per wave
     constexpr int TM = WM / 32;                 // 32-row MFMA tiles per wave
     constexpr int NA = MM_BT * MM3_BK / 8 / NT; // activation 16-byte chunks per thread per K step
     static_assert(2 * 4 * TM * 16 * 64 * 4 <= (MM_BT + BM) * MM3_BK * 2, "accumulator exchange fits the tiles");
-    __shared__ uint4 lds[(MM_BT + BM) * MM3_BK / 8];
     uint4 * lds_a = lds;
     uint4 * lds_b = lds + MM_BT * MM3_BK / 8;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kh = wave >> 2, wq = wave & 3;    // K half of the step; place in the 2 x 2 wave grid
     const int wm = wq >> 1, wn = wq & 1;        // wave: 64 tokens (wm) x WM weight rows (wn)
     const int64_t tok0 = (int64_t) blockIdx.x * MM_BT;
-    const int64_t row0 = (int64_t) blockIdx.y * BM;
     const int64_t ch = blockIdx.z;
     const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
     const char * wbase = p.w + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
@@ -645,6 +644,40 @@ __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
             }
         }
     }
+}
+
+template <int QT, int BM>
+__global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
+    __shared__ uint4 lds[(MM_BT + BM) * MM3_BK / 8];
+    mmq3_tile<QT, BM>(p, (int64_t) blockIdx.y * BM, lds);
+}
+
+// Up to three GEMMs that share the activation (the q/k/v projections of a prefill
+// ubatch) in one launch: blockIdx.y runs over the row tiles of all of them, so the
+// small k/v grids (64 workgroups each at pp512) fill the CUs beside q's. Segments of
+// type QTB (Q4_K_M's Q6_K attn_v) take the second instantiation of the tile.
+constexpr int MQ3M_MAX = 3;
+struct MmqSegs {
+    const char * w[MQ3M_MAX]; size_t w_row[MQ3M_MAX];
+    float * dst[MQ3M_MAX]; size_t d_col[MQ3M_MAX];
+    int64_t M[MQ3M_MAX];
+    int tb0[MQ3M_MAX + 1];                     // first row tile of each segment (prefix sums)
+    int isb[MQ3M_MAX];                         // segment of type QTB
+    int n;
+};
+
+template <int QTA, int QTB>
+__global__ __launch_bounds__(512, 2) void k_mmq3m(MmqArgs p, MmqSegs sg) {
+    __shared__ uint4 lds[(MM_BT + 64) * MM3_BK / 8];
+    const int by = (int) blockIdx.y;
+    int seg = 0;
+#pragma unroll
+    for (int k = 1; k < MQ3M_MAX; ++k) if (k < sg.n && by >= sg.tb0[k]) seg = k;
+    MmqArgs q = p;
+    q.w = sg.w[seg]; q.w_row = sg.w_row[seg]; q.dst = sg.dst[seg]; q.d_col = sg.d_col[seg]; q.M = sg.M[seg];
+    const int64_t row0 = (int64_t) (by - sg.tb0[seg]) * 64;
+    if (sg.isb[seg]) mmq3_tile<QTB, 64>(q, row0, lds);
+    else mmq3_tile<QTA, 64>(q, row0, lds);
 }
 
 // FFN gate/up/SwiGLU of a prefill ubatch in one pass (MUL_MAT(gate), MUL_MAT(up),
@@ -938,6 +971,48 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, 
         default:             k_mmq3g<GGML_TYPE_Q6_K><<<g, 512, 0, c.st>>>(p); break;
     }
     return true;
+}
+
+// q/k/v of a prefill ubatch in one launch (k_mmq3m): members share src1, K-quant weights
+// of at most two types (the first member's, and one other), K % 256 == 0
+static bool kq_type(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
+
+bool mmq_group_run(OpCtx & c, ggml_tensor * const * mms, int n) {
+    if (n < 2 || n > MQ3M_MAX || g_mmq_v1 || g_mmq_glu_off || g_tune[5] == 2) return false;
+    const ggml_tensor * x = mms[0]->src[1];
+    const int ta = mms[0]->src[0]->type;
+    int tb = ta;
+    for (int k = 0; k < n; ++k) {
+        const ggml_tensor * m = mms[k], * w = m->src[0];
+        if (m->src[1] != x || !kq_type(w->type) || !mmq_ok(m)) return false;
+        if (w->ne[0] != x->ne[0] || w->ne[0] % 256 || w->ne[2] != 1 || w->ne[3] != 1) return false;
+        if (m->type != GGML_TYPE_F32 || m->nb[0] != 4 || m->ne[2] != 1 || m->ne[3] != 1) return false;
+        if (w->type != ta) { if (tb != ta && tb != w->type) return false; tb = w->type; }
+    }
+    if (x->type != GGML_TYPE_F32 || x->ne[1] <= 8 || x->ne[2] != 1 || x->ne[3] != 1) return false;
+    const bool combo = (ta == GGML_TYPE_Q6_K || tb == GGML_TYPE_Q6_K || ta == tb) && !(ta == GGML_TYPE_Q5_K && tb == GGML_TYPE_Q4_K) &&
+                       !(ta == GGML_TYPE_Q4_K && tb == GGML_TYPE_Q5_K);
+    if (!combo || (ta == GGML_TYPE_Q6_K && tb == GGML_TYPE_Q5_K)) return false;
+    const int64_t kp = mmq_kp(mms[0]);
+    MmqArgs p{};
+    p.x = mmq_act(c, x, kp); p.kp = kp;
+    p.N = x->ne[1]; p.K = x->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = g_tune[13];
+    MmqSegs sg{};
+    sg.n = n;
+    sg.tb0[0] = 0;
+    for (int k = 0; k < n; ++k) {
+        const ggml_tensor * m = mms[k], * w = m->src[0];
+        sg.w[k] = (const char *) w->data; sg.w_row[k] = w->nb[1];
+        sg.dst[k] = (float *) m->data; sg.d_col[k] = m->nb[1] / 4; sg.M[k] = w->ne[1];
+        sg.isb[k] = w->type != ta;
+        sg.tb0[k + 1] = sg.tb0[k] + (int) mx_ceil_div(w->ne[1], 64);
+    }
+    const dim3 g((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) sg.tb0[n], 1);
+#define M3M(A, B) if (ta == A && tb == B) { k_mmq3m<A, B><<<g, 512, 0, c.st>>>(p, sg); return true; }
+    M3M(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) M3M(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) M3M(GGML_TYPE_Q6_K, GGML_TYPE_Q4_K)
+    M3M(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) M3M(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) M3M(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K)
+#undef M3M
+    return false;
 }
 
 // ---------------------------------------------------------------------------

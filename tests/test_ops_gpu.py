@@ -173,6 +173,29 @@ def test_soft_max_masked(pkg, backend, orc, ne00, ne01, heads):
     assert nmse(y, ref) < 1e-6
 
 
+@pytest.mark.parametrize("types", [("q4_K", "q4_K", "q6_K"), ("q6_K", "q4_K"), ("q5_K", "q5_K", "q5_K")])
+def test_grouped_prefill_mul_mats(pkg, backend, orc, types):
+    """prefill GEMMs sharing src1 (q/k/v) in one k_mmq3m launch, mixed weight types"""
+    rng = np.random.default_rng(41)
+    K, N = 1024, 150
+    Ms = [256, 128, 200][:len(types)]
+    ws = [rand_quant(NAMES[t], M, K, rng) for t, M in zip(types, Ms)]
+    x = rng.standard_normal((N, K)).astype(np.float32)
+    before = backend.stats()["nodes_fused"]
+
+    def build(ctx):
+        tx = ctx.new_tensor("f32", K, N)
+        tws = [ctx.new_tensor(NAMES[t], K, M) for t, M in zip(types, Ms)]
+        outs = [ctx.mul_mat(tw, tx) for tw in tws]
+        return outs, [(tx, x)] + [(tw, w) for tw, (w, _) in zip(tws, ws)]
+
+    ys = run(pkg, backend, build)
+    for y, t, M, (w, rb) in zip(ys, types, Ms, ws):
+        ref = orc.mul_mat(NAMES[t], w, rb, x, exact=True)
+        assert nmse(y.reshape(N, M), ref) < 5e-4
+    assert backend.stats()["nodes_fused"] >= before + len(types) - 1, "grouped GEMM did not fire"
+
+
 @pytest.mark.parametrize("tname", ["q4_K", "q6_K"])
 @pytest.mark.parametrize("N", [1, 150])
 def test_fused_mul_mat_add(pkg, backend, orc, tname, N):
