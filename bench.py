@@ -34,6 +34,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "llama-bench tg128 + pp512 tok/s, Llama-3-8B Q4_K_M, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+MFMA_F16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no sparsity)
+# prefill matmul FLOPs per token (2 x weight-matrix parameters of all layers; the causal
+# attention adds ~1 % at pp512 and is left out): Llama-3-8B 2 * 218,103,808 * 32
+PP_FLOPS_PER_TOKEN = {"llama3_8b": 2 * 218103808 * 32}
 
 
 def dist_setup(n_gpus):
@@ -380,6 +384,11 @@ def main():
                        "model_shape": args.model, "recipe": recipe, "tg": args.tg, "pp": args.pp,
                        "flash_attn": not args.no_fa, "parallelism": par},
             "pp512_tok_s": round(pp_tok_s, 1) if pp_tok_s else None,
+            "pp_roofline": ({"bound": "mfma", "achieved": round(pp_tok_s * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world, 1),
+                             "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
+                             "frac": round(pp_tok_s * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world / MFMA_F16_PEAK_TFS, 4),
+                             "flops_per_token": PP_FLOPS_PER_TOKEN[args.model]}
+                            if pp_tok_s and args.model in PP_FLOPS_PER_TOKEN else None),
             "decode_bytes_per_token": decode_bytes,
             "decode_roofline": {"achieved_GBs": round(per_gpu_bytes_s / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
                                 "frac": round(per_gpu_bytes_s / 1e9 / HBM_PEAK_GBS, 4)},
