@@ -520,9 +520,19 @@ __global__ __launch_bounds__(256, 2) void k_mmq2(MmqArgs p) {
 constexpr int MM3_BK = 256;
 constexpr int MM3_CPR = MM3_BK / 8;             // 16-byte chunks per LDS row
 
+// XCD-aware tile order (workgroup i runs on XCD i % 8): the tiles of one XCD are a
+// contiguous run of (token block fastest, row block) tiles, so the token blocks that
+// share a weight tile read it through one L2. On when p.dbg & 32 (A/B) or g_xcd_tiles.
+__device__ __forceinline__ void mmq_tile_xy(const MmqArgs & p, int & bx, int & by) {
+    const int gx = (int) gridDim.x, n = gx * (int) gridDim.y;
+    int id = (int) blockIdx.x + gx * (int) blockIdx.y;
+    if ((p.dbg & 32) && n % 8 == 0) id = (id % 8) * (n / 8) + id / 8;
+    bx = id % gx; by = id / gx;
+}
+
 // one 128-token x BM-row output tile (blocks x: tokens, z: batch; the rows are row0..)
 template <int QT, int BM>
-__device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, uint4 * lds) {
+__device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, int64_t tok0, uint4 * lds) {
     constexpr int NT = 512;
     static_assert(BM * 8 == NT, "one weight unit per thread");
     constexpr int WM = BM / 2;                  // weight rows per wave
@@ -534,7 +544,6 @@ __device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, uint4
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kh = wave >> 2, wq = wave & 3;    // K half of the step; place in the 2 x 2 wave grid
     const int wm = wq >> 1, wn = wq & 1;        // wave: 64 tokens (wm) x WM weight rows (wn)
-    const int64_t tok0 = (int64_t) blockIdx.x * MM_BT;
     const int64_t ch = blockIdx.z;
     const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
     const char * wbase = p.w + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
@@ -649,7 +658,9 @@ __device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, uint4
 template <int QT, int BM>
 __global__ __launch_bounds__(512, 2) void k_mmq3(MmqArgs p) {
     __shared__ uint4 lds[(MM_BT + BM) * MM3_BK / 8];
-    mmq3_tile<QT, BM>(p, (int64_t) blockIdx.y * BM, lds);
+    int bx, by;
+    mmq_tile_xy(p, bx, by);
+    mmq3_tile<QT, BM>(p, (int64_t) by * BM, (int64_t) bx * MM_BT, lds);
 }
 
 // Up to three GEMMs that share the activation (the q/k/v projections of a prefill
@@ -669,15 +680,16 @@ struct MmqSegs {
 template <int QTA, int QTB>
 __global__ __launch_bounds__(512, 2) void k_mmq3m(MmqArgs p, MmqSegs sg) {
     __shared__ uint4 lds[(MM_BT + 64) * MM3_BK / 8];
-    const int by = (int) blockIdx.y;
+    int bx, by;
+    mmq_tile_xy(p, bx, by);
     int seg = 0;
 #pragma unroll
     for (int k = 1; k < MQ3M_MAX; ++k) if (k < sg.n && by >= sg.tb0[k]) seg = k;
     MmqArgs q = p;
     q.w = sg.w[seg]; q.w_row = sg.w_row[seg]; q.dst = sg.dst[seg]; q.d_col = sg.d_col[seg]; q.M = sg.M[seg];
     const int64_t row0 = (int64_t) (by - sg.tb0[seg]) * 64;
-    if (sg.isb[seg]) mmq3_tile<QTB, 64>(q, row0, lds);
-    else mmq3_tile<QTA, 64>(q, row0, lds);
+    if (sg.isb[seg]) mmq3_tile<QTB, 64>(q, row0, (int64_t) bx * MM_BT, lds);
+    else mmq3_tile<QTA, 64>(q, row0, (int64_t) bx * MM_BT, lds);
 }
 
 // FFN gate/up/SwiGLU of a prefill ubatch in one pass (MUL_MAT(gate), MUL_MAT(up),
@@ -700,8 +712,10 @@ __global__ __launch_bounds__(512, 2) void k_mmq3g(MmqArgs p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int mh = wave >> 2, wq = wave & 3;     // matrix (0 gate, 1 up); place in the 2 x 2 wave grid
     const int wm = wq >> 1, wn = wq & 1;
-    const int64_t tok0 = (int64_t) blockIdx.x * MM_BT;
-    const int64_t row0 = (int64_t) blockIdx.y * BM;
+    int bx, by;
+    mmq_tile_xy(p, bx, by);
+    const int64_t tok0 = (int64_t) bx * MM_BT;
+    const int64_t row0 = (int64_t) by * BM;
     const _Float16 * xbase = p.x;
     const int64_t nk = p.K / MM3_BK;
     // this thread's two weight units: half hh of row ur's super-block, chunk uc, of gate and of up
@@ -959,7 +973,7 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, 
     p.w = (const char *) wg->data; p.w2 = (const char *) wu->data; p.w_row = wg->nb[1];
     p.x = mmq_act(c, x, kp); p.kp = kp;
     p.dst = (float *) glu->data; p.d_col = glu->nb[1] / 4;
-    p.M = wg->ne[1]; p.N = x->ne[1]; p.K = wg->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1;
+    p.M = wg->ne[1]; p.N = x->ne[1]; p.K = wg->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = g_tune[13];
     // the down projection reads this output: write its f16 copy too (claimed after the
     // input conversion above, which used the same slot)
     p.h = mmq_act_claim(c, glu->data, glu->ne[0], glu->ne[1], glu->nb[1]);
