@@ -417,7 +417,7 @@ void ggml_backend_mi355x_stats(ggml_backend_t b, uint64_t out[4]) {
 namespace mx {
 double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * const * w2, int nw,
                  const ggml_tensor * x, ggml_tensor * dst, int iters);
-extern int g_tune[16];
+extern int g_tune[32];
 }
 
 extern "C" double ggml_backend_mi355x_time_mmvq(ggml_backend_t b, const ggml_tensor * const * w, const ggml_tensor * const * w2,
@@ -467,5 +467,5 @@ extern "C" int ggml_backend_mi355x_trace_read(unsigned long long * out, int n) {
 }
 
 extern "C" void ggml_backend_mi355x_set_tune(int idx, int value) {
-    if (idx >= 0 && idx < 16) mx::g_tune[idx] = value;
+    if (idx >= 0 && idx < 32) mx::g_tune[idx] = value;
 }

@@ -53,7 +53,7 @@ __host__ __device__ inline float * gemv_lds_red(char * smem, int64_t K) { return
 // MI355X (tools/opbench.py ffn_block / q_q4k, profiles/r01): grids of one block per CU
 // (the 4096-row projections) are latency-bound and win with registers; grids of several
 // waves' worth per SIMD (SwiGLU, lm_head) win with the occupancy LDS staging buys.
-extern int g_tune[16];
+extern int g_tune[32];
 inline int gemv_mode(const XStage & xs, int64_t K, int64_t n_waves = 0, int nt = 256) {
     if (xs.q8) return XS_Q8;
     bool lds = n_waves >= 2048;

@@ -26,7 +26,7 @@ struct XStage {
                                     // before the prologue (g_tune[14] = 1; A/B)
 };
 
-extern int g_tune[16];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)
+extern int g_tune[32];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)
 extern bool g_gemv2;        // v2 GEMV enabled (GGML_MI355X_GEMV_V1 turns it off)
 
 bool gemv2_type_ok(int t);

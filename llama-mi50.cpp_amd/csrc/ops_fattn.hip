@@ -17,7 +17,7 @@
 
 namespace mx {
 
-extern int g_tune[16];
+extern int g_tune[32];
 
 constexpr int FA_TILE = 256;
 constexpr int FA_MAXG = 8;

@@ -21,7 +21,7 @@
 //    replay) combines them — no second kernel, no second launch gap.
 #include "backend.h"
 
-namespace mx { extern int g_tune[16]; }
+namespace mx { extern int g_tune[32]; }
 
 namespace mx {
 

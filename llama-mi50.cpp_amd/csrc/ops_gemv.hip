@@ -7,7 +7,7 @@
 
 namespace mx {
 
-int g_tune[16] = {0};
+int g_tune[32] = {0};
 bool g_gemv2 = getenv("GGML_MI355X_GEMV_V1") == nullptr;
 
 struct G2Args {
@@ -110,6 +110,13 @@ static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
         }
     }
     constexpr bool FULL = QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q6_K;   // full tuning grid
+    if constexpr (FULL && EPI == 0) {
+        // g_tune[16]: waves per workgroup of the plain 16 x 4 geometry (lm_head): 8 or 16
+        // halve / quarter the workgroups that each stage (and normalise) the activation —
+        // measured slower (lm_head 82.6 / 92.9 / 123.3 us for 4 / 8 / 16 waves), kept for sweeps
+        if (g_tune[16] == 8 && lpr == 16 && upl == 4) return launch_cfg<QT, 16, 4, EPI, 8>(st, p);
+        if (g_tune[16] == 16 && lpr == 16 && upl == 4) return launch_cfg<QT, 16, 4, EPI, 16>(st, p);
+    }
     if constexpr (FULL) {
 #define CFG(L, U) if (lpr == L && upl == U) return launch_cfg<QT, L, U, EPI>(st, p);
         CFG(16, 2) CFG(16, 4) CFG(32, 2) CFG(32, 4) CFG(64, 2) CFG(64, 4)
