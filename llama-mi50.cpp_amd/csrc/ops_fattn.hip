@@ -17,6 +17,10 @@
 
 namespace mx {
 
+// e^x as v_exp_f32(x · log2 e): the libm expf's range reduction sat on the softmax's
+// critical path (decode FA v2: 6.95 -> 5.56 us at 256 keys with the same change)
+__device__ __forceinline__ float fa_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
 extern int g_tune[32];
 
 constexpr int FA_TILE = 256;
@@ -142,13 +146,13 @@ __global__ __launch_bounds__(256) void k_fattn(FaArgs p) {
             const float mnew = fmaxf(mold, mx);
             float sum = 0.f;
             for (int i = lane; i < FA_TILE; i += 64) {
-                const float e = mnew == -INFINITY ? 0.f : expf(sc[g][i] - mnew);
+                const float e = mnew == -INFINITY ? 0.f : fa_exp(sc[g][i] - mnew);
                 sc[g][i] = e;
                 sum += e;
             }
             sum = wave_sum(sum);
             if (lane == 0) {
-                const float a = mold == -INFINITY ? 0.f : expf(mold - mnew);
+                const float a = mold == -INFINITY ? 0.f : fa_exp(mold - mnew);
                 alpha[g] = a;
                 lrun[g] = lrun[g] * a + sum;
                 mrun[g] = mnew;
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
             s = x + m;
         }
         const float mx = wave_max(s);
-        const float e = mx == -INFINITY ? 0.f : expf(s - mx);
+        const float e = mx == -INFINITY ? 0.f : fa_exp(s - mx);
         const float l = wave_sum(e);
         pw[wave][g][lane] = e;
         if (lane == 0) { wm[wave][g] = mx; wl[wave][g] = l; }
@@ -367,11 +371,11 @@ __global__ __launch_bounds__(256) void k_fattn_dec(FaArgs p, FaOut fo) {
         float L = 0.f, O = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            const float f = wm[w][g] == -INFINITY ? 0.f : expf(wm[w][g] - M);
+            const float f = wm[w][g] == -INFINITY ? 0.f : fa_exp(wm[w][g] - M);
             L += wl[w][g] * f;
             O += wo[w][g][d] * f;
         }
-        if (sk != -INFINITY) L += expf(sk - M);
+        if (sk != -INFINITY) L += fa_exp(sk - M);
         if (fo.direct) {
             float * out = (float *) (fo.dst + h * fo.nb1 + iq1 * fo.nb2 + iq3 * fo.nb3);
             out[d] = L == 0.f ? 0.f : O / L;
@@ -418,10 +422,10 @@ __global__ __launch_bounds__(64) void k_fattn_combine(const float * __restrict__
     float l_l = 0.f;
     for (int s = lane; s < nsplit; s += 64) {
         const float ms = mp[(size_t) s * nrows + r];
-        if (ms != -INFINITY) l_l += lp[(size_t) s * nrows + r] * expf(ms - M);
+        if (ms != -INFINITY) l_l += lp[(size_t) s * nrows + r] * fa_exp(ms - M);
     }
     float L = wave_sum(l_l);
-    if (has_sink) L += expf(sk - M);
+    if (has_sink) L += fa_exp(sk - M);
     const float inv = L == 0.f ? 0.f : 1.0f / L;
     float o[DPT];
 #pragma unroll
@@ -440,7 +444,7 @@ __global__ __launch_bounds__(64) void k_fattn_combine(const float * __restrict__
         for (int s = 0; s < PRE; ++s) {
             if (s0 + s >= nsplit) break;
             const float ms = mp[(size_t) (s0 + s) * nrows + r];
-            const float w = ms == -INFINITY ? 0.f : expf(ms - M);
+            const float w = ms == -INFINITY ? 0.f : fa_exp(ms - M);
 #pragma unroll
             for (int i = 0; i < DPT; ++i) o[i] += w * ov[s][i];
         }

@@ -123,7 +123,8 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
                 acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[h][2], acc, false);
                 acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[h][3], acc, false);
                 acc = dpp_sum_group<LPK>(acc);
-                s[h][t] = mk[t] == -INFINITY ? -INFINITY : acc * p.scale + mk[t];
+                // log2 domain (v_exp_f32 below): s = (q·k·scale + mask) · log2(e)
+                s[h][t] = mk[t] == -INFINITY ? -INFINITY : (acc * p.scale + mk[t]) * 1.4426950408889634f;
             }
         }
         // online softmax (the wave's keys of this chunk: xor over the key rows kq)
@@ -135,10 +136,10 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
 #pragma unroll
             for (int off = LPK; off < 64; off <<= 1) mc = fmaxf(mc, __shfl_xor(mc, off, 64));
             const float Mn = fmaxf(M[h], mc);
-            const float a = M[h] == -INFINITY ? 0.f : expf(M[h] - Mn);
+            const float a = M[h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(M[h] - Mn);
             float pr[FD_NI], lc = 0.f;
 #pragma unroll
-            for (int t = 0; t < FD_NI; ++t) { pr[t] = Mn == -INFINITY ? 0.f : expf(s[h][t] - Mn); lc += pr[t]; }
+            for (int t = 0; t < FD_NI; ++t) { pr[t] = Mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[h][t] - Mn); lc += pr[t]; }
 #pragma unroll
             for (int off = LPK; off < 64; off <<= 1) lc += __shfl_xor(lc, off, 64);
             L[h] = L[h] * a + lc;
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         float Lw = 0.f, O = 0.f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
-            const float f = wm[w][h] == -INFINITY ? 0.f : expf(wm[w][h] - Mw);
+            const float f = wm[w][h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(wm[w][h] - Mw);
             Lw += wl[w][h] * f;
             O += wo[w][h][d] * f;
         }
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         float Mx = -INFINITY, Ls = 0.f;
         for (int sp = 0; sp < p.nsplit; ++sp) Mx = fmaxf(Mx, sM[tid][sp]);
         for (int sp = 0; sp < p.nsplit; ++sp) {
-            const float f = sM[tid][sp] == -INFINITY ? 0.f : expf(sM[tid][sp] - Mx);
+            const float f = sM[tid][sp] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sM[tid][sp] - Mx);
             Ls += sF[tid][sp] * f;
             sM[tid][sp] = f;                 // now the weight of split sp
         }
