@@ -52,7 +52,9 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
                                               [&] { if constexpr (EPI == 2) asm volatile("" : "+v"(res)); });
     MX_TRACE(tr, 3);
     float v = acc[0];
-    if constexpr (EPI == 1) v = (v / (1.0f + expf(-v))) * acc[1];
+    // silu by v_exp_f32 / v_rcp_f32: libm expf and the IEEE division sat on every
+    // workgroup's tail
+    if constexpr (EPI == 1) v = v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f)) * acc[1];
     if constexpr (EPI == 2) v += res;
     if (sub == LPR - 1 && valid) p.dst[row] = v;
     MX_TRACE(tr, 4);
