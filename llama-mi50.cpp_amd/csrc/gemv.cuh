@@ -73,21 +73,24 @@ __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
 }
 
 // quantise 16 values held by this thread; the partner thread (tid ^ 1) holds the other
-// half of the 32-block. Bit-identical to k_quantize_act (amax/127, roundf(x/d)).
+// half of the 32-block (k_quantize_act semantics up to the rounding noted below).
 __device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) {
     float amax = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
     amax = fmaxf(amax, dpp_f<0xB1>(-INFINITY, amax));   // partner lane tid ^ 1
     const float dd = amax / 127.0f;
-    const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
+    // 127 · v_rcp_f32(amax) and round-to-nearest-even (v_rndne_f32): the IEEE division and
+    // the round-half-away sequence of roundf sat on the prologue's critical path (they
+    // differ from amax/127, roundf only in the last ulp of id / at exact .5 ties)
+    const float id = amax == 0.0f ? 0.0f : 127.0f * __builtin_amdgcn_rcpf(amax);
     int sum = 0, pk[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         int w = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int qi = (int) roundf(v[4 * j + k] * id);
+            const int qi = (int) __builtin_rintf(v[4 * j + k] * id);
             sum += qi;
             w |= (qi & 0xFF) << (8 * k);
         }
@@ -207,7 +210,7 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
             ss = 0.f;
 #pragma unroll
             for (int wv = 0; wv < NT / 64; ++wv) ss += red[wv];
-            scale = 1.0f / sqrtf(ss / (float) K + xs.eps);
+            scale = __builtin_amdgcn_rsqf(ss / (float) K + xs.eps);
         }
         for (int hg = t; hg < nhg; hg += NT) {   // nhg is even: partner lanes stay paired
             float v2[16];
@@ -236,7 +239,7 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
         ss = 0.f;
 #pragma unroll
         for (int wv = 0; wv < NT / 64; ++wv) ss += red[wv];
-        const float scale = 1.0f / sqrtf(ss / (float) K + xs.eps);
+        const float scale = __builtin_amdgcn_rsqf(ss / (float) K + xs.eps);
 #pragma unroll
         for (int h = 0; h < HPT; ++h) {
             const int hg = t + NT * h;
