@@ -64,6 +64,13 @@ int ggml_backend_mi355x_trace_read(unsigned long long * out, int n);
 /* Debug: {start, end} s_memrealtime (100 MHz) of every workgroup of the last GEMV launch
  * recorded while tune index 6 == 2, at out[2*block]. Read-and-clear; returns n or -1. */
 int ggml_backend_mi355x_trace_blocks_read(unsigned long long * out, int n);
+/* Kernel-choice log: while on, every launch site of the hot-path kernels appends one line
+ * naming the kernel and the geometry it picked (e.g. "gemv2 qt=12 lpr=16 upl=2 epi=1 w=8
+ * mode=4 ..."), so tests can assert which instantiation ran at a shape. on != 0 clears and
+ * starts it, 0 stops it. */
+void ggml_backend_mi355x_klog(int on);
+/* Copies the log (NUL-terminated, at most n - 1 bytes); returns its full length. */
+size_t ggml_backend_mi355x_klog_read(char * out, size_t n);
 #ifdef __cplusplus
 }
 #endif

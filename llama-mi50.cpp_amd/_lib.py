@@ -74,6 +74,8 @@ def load():
     _sig(lib, "ggml_backend_mi355x_set_tune", None, I, I)
     _sig(lib, "ggml_backend_mi355x_trace_read", I, P, I)
     _sig(lib, "ggml_backend_mi355x_trace_blocks_read", I, P, I)
+    _sig(lib, "ggml_backend_mi355x_klog", None, I)
+    _sig(lib, "ggml_backend_mi355x_klog_read", ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t)
     # graph builder
     _sig(lib, "mxg_init", P)
     _sig(lib, "mxg_free", None, P)

@@ -153,10 +153,18 @@ static const ggml_backend_buffer_type_i kHostBuftIface = {
 Stream * stream_of(ggml_backend_t b) { return (Stream *) b->context; }
 
 static const char * be_name(ggml_backend_t b) { return stream_of(b)->name.c_str(); }
+void klog_dump(const char * path);
 static void be_free(ggml_backend_t b) {
     Stream * s = stream_of(b);
     hipSetDevice(s->device);
     hipStreamSynchronize(s->stream);
+    // GGML_MI355X_STATS=1: executor counters of this backend on stderr when libllama frees
+    // it (drop-in runs: shows the fusions fired on the reference's own node order)
+    if (getenv("GGML_MI355X_STATS"))
+        fprintf(stderr, "[mi355x] stats {\"backend\": \"%s\", \"graph_compute\": %llu, \"graph_replay\": %llu, "
+                "\"nodes_run\": %llu, \"nodes_fused\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
+                (unsigned long long) s->n_graph_replay, (unsigned long long) s->n_nodes_run, (unsigned long long) s->n_fused);
+    if (const char * kp = getenv("GGML_MI355X_KLOG")) klog_dump(kp);
     if (s->gcache.exec) hipGraphExecDestroy(s->gcache.exec);
     if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
     if (s->scratch.base) hipFree(s->scratch.base);
@@ -334,6 +342,7 @@ static void * rg_proc(ggml_backend_reg_t, const char * name) {
 
 static const ggml_backend_reg_i kRegIface = { rg_name, rg_count, rg_get, rg_proc };
 
+void klog_env_init();
 static void init_registry() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) { (void) hipGetLastError(); n = 0; }
@@ -354,6 +363,7 @@ static void init_registry() {
         d->host_buft = ggml_backend_buffer_type{kHostBuftIface, &d->dev, d.get()};
         g_devices.push_back(std::move(d));
     }
+    klog_env_init();
     g_reg.api_version = GGML_BACKEND_API_VERSION;
     g_reg.iface = kRegIface;
     g_reg.context = nullptr;
@@ -464,6 +474,47 @@ extern "C" int ggml_backend_mi355x_trace_read(unsigned long long * out, int n) {
     HIP_CHECK(hipMemcpy(out, mx::g_trace_dev, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     HIP_CHECK(hipMemset(mx::g_trace_dev, 0, 16 * 128 * sizeof(unsigned long long)));   // read-and-clear
     return n;
+}
+
+namespace mx {
+int g_klog = 0;
+static std::mutex g_klog_mu;
+static std::string g_klog_buf;
+void klog_add(const char * fmt, ...) {
+    char line[256];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(line, sizeof(line), fmt, ap);
+    va_end(ap);
+    std::lock_guard<std::mutex> lk(g_klog_mu);
+    if (g_klog_buf.size() < (1u << 22)) { g_klog_buf += line; g_klog_buf += '\n'; }
+}
+
+// GGML_MI355X_KLOG=<path>: record from registry init, written to <path> when a backend
+// is freed (appended: one block per backend)
+void klog_dump(const char * path) {
+    std::lock_guard<std::mutex> lk(g_klog_mu);
+    if (FILE * f = fopen(path, "a")) { fwrite(g_klog_buf.data(), 1, g_klog_buf.size(), f); fclose(f); }
+    g_klog_buf.clear();
+}
+void klog_env_init() { if (getenv("GGML_MI355X_KLOG")) g_klog = 1; }
+}
+
+// on != 0: start recording kernel choices (clears the log); 0: stop
+extern "C" void ggml_backend_mi355x_klog(int on) {
+    std::lock_guard<std::mutex> lk(mx::g_klog_mu);
+    mx::g_klog_buf.clear();
+    mx::g_klog = on;
+}
+// copies the log (NUL-terminated, truncated to n - 1 bytes); returns its full length
+extern "C" size_t ggml_backend_mi355x_klog_read(char * out, size_t n) {
+    std::lock_guard<std::mutex> lk(mx::g_klog_mu);
+    if (out && n) {
+        const size_t k = std::min(n - 1, mx::g_klog_buf.size());
+        memcpy(out, mx::g_klog_buf.data(), k);
+        out[k] = 0;
+    }
+    return mx::g_klog_buf.size();
 }
 
 extern "C" void ggml_backend_mi355x_set_tune(int idx, int value) {

@@ -123,7 +123,13 @@ namespace mx {
 unsigned long long * mx_trace_slot(int slot);
 // host: per-workgroup {start, end} s_memrealtime pairs of the last traced launch (tune 6 == 2)
 unsigned long long * mx_trace_blocks();
+// host: kernel-choice log (ggml_backend_mi355x_klog / _klog_read). Launch sites record
+// the kernel and geometry they picked, so tests can assert which instantiation ran at a
+// given shape. Off unless enabled; appended only while launching (eager or capture).
+extern int g_klog;
+void klog_add(const char * fmt, ...) __attribute__((format(printf, 1, 2)));
 }
+#define MX_KLOG(...) do { if (mx::g_klog) mx::klog_add(__VA_ARGS__); } while (0)
 #if defined(__HIPCC__)
 
 // Cross-lane reductions on DPP (gfx9 data-parallel primitives: quad_perm, half/row

@@ -619,13 +619,14 @@ void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
         int G = blocks_full >= 128 ? Gt : 1;
         if (g_tune[7]) G = std::min(g_tune[7], Gt);
         const dim3 gridd((unsigned) (q->ne[1] * k->ne[2] * (Gt / G) * q->ne[3]), (unsigned) nsplit);
+        MX_KLOG("fattn_dec D=%d G=%d nsplit=%d n_kv=%d", D, G, (int) nsplit, (int) k->ne[1]);
 #define DEC(DD, GG) if (D == DD && G == GG) k_fattn_dec<DD, GG><<<gridd, 256, 0, c.st>>>(b, fo); else
 #define DECG(DD) DEC(DD, 1) DEC(DD, 2) DEC(DD, 4) DEC(DD, 8)
         DECG(64) DECG(128) DECG(256) MX_ABORT("fattn dec D=%d G=%d", D, G);
 #undef DECG
 #undef DEC
         if (nsplit == 1) return;
-    } else if (k->type == GGML_TYPE_F16) fa_launch<uint16_t, uint16_t>(c, D, grid, b);
+    } else if (k->type == GGML_TYPE_F16) { MX_KLOG("fattn_tile D=%d f16", D); fa_launch<uint16_t, uint16_t>(c, D, grid, b); }
     else fa_launch<float, float>(c, D, grid, b);
     // decode: also emit the q8 activation of the output for the O-projection GEMV
     ActQ * q8 = nullptr;

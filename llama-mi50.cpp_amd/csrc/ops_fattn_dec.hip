@@ -305,6 +305,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     a.part = (float *) c.scratch->take(fa_dec2_scratch(dst));
     a.cnt = c.s->fa_cnt;
     const dim3 grid((unsigned) (a.Hkv * (Gt / f.G) * a.n_q * q->ne[3]), (unsigned) a.nsplit);
+MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv);
 #define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { k_fattn_dec2<DD, GG, NWW><<<grid, 64 * NWW, 0, c.st>>>(a); return; }
     FD(128, 1, 16) FD(64, 1, 16)
     FD(128, 4, 4) FD(128, 1, 4) FD(128, 2, 4) FD(128, 8, 4) FD(64, 1, 4) FD(64, 2, 4) FD(64, 4, 4) FD(64, 8, 4)

@@ -485,12 +485,14 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
         if (dst->nb[1] == 4 * (size_t) k->ne[0] && dst->nb[2] == (size_t) 4 * k->ne[0] * p.H && dst->ne[3] == 1)
             p.h = mmq_act_claim(c, dst->data, k->ne[0] * p.H, p.n_q, dst->nb[2]);
         const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32 * (4 / HG)), (unsigned) (p.Hkv * (Gt / HG)));
+        MX_KLOG("fa_mma2 HG=%d n_q=%d n_kv=%d H=%d Hkv=%d", HG, p.n_q, p.n_kv, p.H, p.Hkv);
         if (HG == 4) k_fa_mma2<4><<<g2, 256, 0, c.st>>>(p);
         else if (HG == 2) k_fa_mma2<2><<<g2, 256, 0, c.st>>>(p);
         else k_fa_mma2<1><<<g2, 256, 0, c.st>>>(p);
         return;
     }
     dim3 grid((unsigned) mx_ceil_div(p.n_q, FM_QT), (unsigned) p.H);
+    MX_KLOG("fa_mma D=%d n_q=%d n_kv=%d", (int) k->ne[0], p.n_q, p.n_kv);
     if (k->ne[0] == 64) k_fa_mma<64><<<grid, 128, 0, c.st>>>(p);
     else k_fa_mma<128><<<grid, 128, 0, c.st>>>(p);
 }

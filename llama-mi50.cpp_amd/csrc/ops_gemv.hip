@@ -87,6 +87,7 @@ static void launch_cfg(hipStream_t st, const G2Args & p, bool regs = false) {
     // regs: register staging of x even on a large grid (the q8-emitting SwiGLU)
     const int mode = gemv_mode(p.xs, p.K, regs && g_tune[9] == 0 ? 0 : (int64_t) grid * W, 64 * W);
     const size_t lds = gemv_lds_bytes(p.K, mode);
+    MX_KLOG("gemv2 qt=%d lpr=%d upl=%d epi=%d w=%d mode=%d K=%d M=%d q8o=%d", QT, LPR, UPL, EPI, W, mode, p.K, p.nrows, p.q8o != nullptr);
     switch (mode) {
         case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8><<<grid, 64 * W, lds, st>>>(p); break;
         case XS_NORM_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_LDS><<<grid, 64 * W, lds, st>>>(p); break;

@@ -911,6 +911,8 @@ static void mmq_run_ex(OpCtx & c, ggml_tensor * dst, ggml_tensor * out, const gg
         // larger grids keep the 4-wave kernel, two of whose workgroups share a CU
         // (gate/up 131 vs 163 us, profiles/r01/opbench_mmq_dbg.txt)
         const bool w8 = g_tune[5] == 1 || (g_tune[5] == 0 && bm == 64 && (int64_t) g2.x * g2.y * g2.z <= 256);
+        MX_KLOG("mmq%d qt=%d bm=%d M=%lld N=%lld K=%lld res=%d", w8 && bm == 64 ? 3 : 2, (int) w->type, bm,
+                (long long) p.M, (long long) p.N, (long long) p.K, res != nullptr);
         if (w8 && bm == 64) {
 #define MQ3(T) case T: k_mmq3<T, 64><<<g2, 512, 0, c.st>>>(p); return;
             switch (w->type) { MQ3(GGML_TYPE_Q4_K) MQ3(GGML_TYPE_Q5_K) MQ3(GGML_TYPE_Q6_K) default: break; }
@@ -922,6 +924,7 @@ static void mmq_run_ex(OpCtx & c, ggml_tensor * dst, ggml_tensor * out, const gg
     }
     MX_ASSERT(!res && out == dst);
     dim3 grid((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, MM_BW), (unsigned) (x->ne[2] * x->ne[3]));
+    MX_KLOG("mmq1 qt=%d M=%lld N=%lld K=%lld", (int) w->type, (long long) p.M, (long long) p.N, (long long) p.K);
     switch (w->type) {
 #define MQ(T) case T: k_mmq<T><<<grid, 256, 0, c.st>>>(p); break;
         MQ(GGML_TYPE_Q4_0) MQ(GGML_TYPE_Q4_1) MQ(GGML_TYPE_Q5_0) MQ(GGML_TYPE_Q5_1) MQ(GGML_TYPE_Q8_0)
@@ -979,6 +982,7 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, 
     p.h = mmq_act_claim(c, glu->data, glu->ne[0], glu->ne[1], glu->nb[1]);
     p.h_col = glu->ne[0];
     const dim3 g((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) mx_ceil_div(p.M, 64), 1);
+    MX_KLOG("mmq3g qt=%d M=%lld N=%lld K=%lld", (int) wg->type, (long long) p.M, (long long) p.N, (long long) p.K);
     switch (wg->type) {
         case GGML_TYPE_Q4_K: k_mmq3g<GGML_TYPE_Q4_K><<<g, 512, 0, c.st>>>(p); break;
         case GGML_TYPE_Q5_K: k_mmq3g<GGML_TYPE_Q5_K><<<g, 512, 0, c.st>>>(p); break;
@@ -1022,6 +1026,7 @@ bool mmq_group_run(OpCtx & c, ggml_tensor * const * mms, int n) {
         sg.tb0[k + 1] = sg.tb0[k] + (int) mx_ceil_div(w->ne[1], 64);
     }
     const dim3 g((unsigned) mx_ceil_div(p.N, MM_BT), (unsigned) sg.tb0[n], 1);
+    MX_KLOG("mmq3m n=%d qta=%d qtb=%d N=%lld K=%lld", n, ta, tb, (long long) p.N, (long long) p.K);
 #define M3M(A, B) if (ta == A && tb == B) { k_mmq3m<A, B><<<g, 512, 0, c.st>>>(p, sg); return true; }
     M3M(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) M3M(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) M3M(GGML_TYPE_Q6_K, GGML_TYPE_Q4_K)
     M3M(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) M3M(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) M3M(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K)

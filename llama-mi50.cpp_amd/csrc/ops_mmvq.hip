@@ -242,6 +242,7 @@ static void launch_lpr(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch
     constexpr int RPB = 4 * (64 / LPR);
     dim3 grid((unsigned) mx_ceil_div(p.nrows, RPB), (unsigned) nch);
     const int64_t per_lane = mx_ceil_div(p.units, LPR);
+    MX_KLOG("mmvq1 qt=%d nc=%d lpr=%d epi=%d M=%d", QT, NC, LPR, EPI, (int) p.nrows);
     if constexpr (NC == 1) {
         if (per_lane >= 5) k_mmvq<QT, NC, LPR, 8, EPI><<<grid, 256, 0, c.st>>>(p, a);
         else if (per_lane >= 3) k_mmvq<QT, NC, LPR, 4, EPI><<<grid, 256, 0, c.st>>>(p, a);

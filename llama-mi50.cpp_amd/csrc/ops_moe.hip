@@ -90,6 +90,7 @@ size_t mul_mat_id_scratch(const ggml_tensor * dst) {
 
 template <int QT>
 static void moe_launch_q(OpCtx & c, const MoeArgs & p, const ActQ & a, int64_t items) {
+    MX_KLOG("moe_mmvq qt=%d K=%d M=%d items=%lld", QT, (int) p.K, (int) p.M, (long long) items);
     if (p.K <= 2048) k_moe_mmvq<QT, 16><<<dim3((unsigned) mx_ceil_div(p.M, 16), (unsigned) items), 256, 0, c.st>>>(p, a);
     else if (p.K <= 8192) k_moe_mmvq<QT, 32><<<dim3((unsigned) mx_ceil_div(p.M, 8), (unsigned) items), 256, 0, c.st>>>(p, a);
     else k_moe_mmvq<QT, 64><<<dim3((unsigned) mx_ceil_div(p.M, 4), (unsigned) items), 256, 0, c.st>>>(p, a);
@@ -120,6 +121,7 @@ void op_mul_mat_id(OpCtx & c, ggml_tensor * dst) {
         return;
     }
     dim3 grid((unsigned) mx_ceil_div(p.M, 4), (unsigned) items);
+    MX_KLOG("moe_generic type=%d K=%d M=%d items=%lld", (int) as->type, (int) p.K, (int) p.M, (long long) items);
     const char * pb = (const char *) b->data;
     switch (as->type) {
 #define MG(T) case T: k_moe_generic<T><<<grid, 256, 0, c.st>>>(p, pb, b->nb[1], b->nb[2]); break;

@@ -262,6 +262,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
 #undef GEOS
     if (mode != XS_NORM && cfg != 5) return 0;   // the other sources exist in the default geometry only
     const dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
+    MX_KLOG("qkv qta=%d qtv=%d mode=%d cfg=%d K=%d", ta, tv, mode, cfg, p.K);
     hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K, mode), c.st, p);
     return last - i + 1;
 }

@@ -37,6 +37,17 @@ class Backend:
     def synchronize(self):
         self.lib.mxg_synchronize(self.ptr)
 
+    def klog(self, on=True):
+        """start (clear) / stop the kernel-choice log (ggml_backend_mi355x_klog)"""
+        self.lib.ggml_backend_mi355x_klog(1 if on else 0)
+
+    def klog_read(self):
+        """the kernel-choice lines recorded since klog(True)"""
+        n = self.lib.ggml_backend_mi355x_klog_read(None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        self.lib.ggml_backend_mi355x_klog_read(buf, n + 1)
+        return buf.value.decode().splitlines()
+
     def free(self):
         if self.ptr:
             self.lib.mxg_backend_free(self.ptr)

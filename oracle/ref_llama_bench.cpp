@@ -5,7 +5,11 @@
 //                tools/llama-bench/llama-bench.cpp:1962-2010 (random tokens, decode,
 //                synchronise per token), printed as one JSON line;
 //   logits mode: --logits <tokens.i32> <out.f32> writes the logits of every position
-//                (end-to-end parity of the MI355X runner vs the reference CPU backend).
+//                (end-to-end parity of the MI355X runner vs the reference CPU backend);
+//                --last N writes only the last N positions' logits (long prompts, e.g.
+//                pp2048 as 4 ubatches with -b 2048 -ub 512);
+//   -r R       : bench mode repeats pp / tg R times and reports the mean and the
+//                per-repetition rates, llama-bench's avg_ts / samples_ts.
 // -ngl > 0 with GGML_BACKEND_PATH=libggml-mi355x.so runs the reference libllama on the
 // MI355X backend unmodified (the drop-in check).
 #include "llama.h"
@@ -19,13 +23,40 @@
 #include <string>
 #include <vector>
 
+// --dump <file>: the scheduler's eval callback (llama_context_params::cb_eval, as
+// tools/eval-callback uses it) records every f32 node of the graph: name, op, shape, sum,
+// sum of squares and the first values — diffing a -ngl 0 and a -ngl 99 dump finds the
+// first node where the MI355X backend departs from the reference CPU backend.
+static FILE * g_dump = nullptr;
+static std::string g_dump_dir;   // --dump-dir: also the raw f32 values, one file per node
+static int g_dump_idx = 0;
+static bool dump_cb(ggml_tensor * t, bool ask, void *) {
+    if (ask) return t->type == GGML_TYPE_F32;
+    if (!g_dump || t->type != GGML_TYPE_F32 || !ggml_is_contiguous(t)) return true;
+    std::vector<float> v(ggml_nelements(t));
+    ggml_backend_tensor_get(t, v.data(), 0, ggml_nbytes(t));
+    double s = 0, s2 = 0;
+    for (float x : v) { s += x; s2 += (double) x * x; }
+    fprintf(g_dump, "%s %s %lld %lld %lld %lld %.9g %.9g", t->name, ggml_op_desc(t), (long long) t->ne[0],
+            (long long) t->ne[1], (long long) t->ne[2], (long long) t->ne[3], s, s2);
+    for (size_t i = 0; i < v.size() && i < 4; ++i) fprintf(g_dump, " %.7g", v[i]);
+    fprintf(g_dump, "\n");
+    if (!g_dump_dir.empty()) {
+        char fn[512];
+        snprintf(fn, sizeof(fn), "%s/%03d.f32", g_dump_dir.c_str(), g_dump_idx++);
+        if (FILE * f = fopen(fn, "wb")) { fwrite(v.data(), 4, v.size(), f); fclose(f); }
+    }
+    return true;
+}
+
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 int main(int argc, char ** argv) {
     std::string model, tok_in, logits_out;
-    int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0, incremental = 0;
+    int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0, incremental = 0, last = 0, n_batch = 0, n_ubatch = 0, reps = 1;
+    int ctk = -1;   // K/V cache type (ggml_type id), -1: default f16
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() { return std::string(argv[++i]); };
@@ -38,6 +69,13 @@ int main(int argc, char ** argv) {
         else if (a == "-c") n_ctx = std::stoi(next());
         else if (a == "--logits") { tok_in = next(); logits_out = next(); }
         else if (a == "--incremental") incremental = 1;   // logits mode: one token per llama_decode
+        else if (a == "--last") last = std::stoi(next());
+        else if (a == "-b") n_batch = std::stoi(next());
+        else if (a == "-ub") n_ubatch = std::stoi(next());
+        else if (a == "-r") reps = std::max(1, std::stoi(next()));
+        else if (a == "-ctk") ctk = std::stoi(next());
+        else if (a == "--dump") g_dump = fopen(next().c_str(), "w");
+        else if (a == "--dump-dir") g_dump_dir = next();
     }
     llama_log_set([](ggml_log_level, const char *, void *) {}, nullptr);
     llama_backend_init();
@@ -60,12 +98,14 @@ int main(int argc, char ** argv) {
     }
     llama_context_params cp = llama_context_default_params();
     cp.n_ctx = n_ctx > 0 ? n_ctx : std::max(512, (int) (pp + tg + toks.size() + 64));
-    cp.n_batch = std::max<int>({pp, (int) toks.size(), 1});
-    cp.n_ubatch = std::min<int>(512, cp.n_batch);
+    cp.n_batch = n_batch > 0 ? n_batch : std::max<int>({pp, (int) toks.size(), 1});
+    cp.n_ubatch = n_ubatch > 0 ? n_ubatch : std::min<int>(512, cp.n_batch);
+    if (ctk >= 0) { cp.type_k = (ggml_type) ctk; cp.type_v = (ggml_type) ctk; }
     cp.n_threads = threads;
     cp.n_threads_batch = threads;
     cp.flash_attn_type = fa ? LLAMA_FLASH_ATTN_TYPE_ENABLED : LLAMA_FLASH_ATTN_TYPE_DISABLED;
     cp.no_perf = true;
+    if (g_dump) { cp.cb_eval = dump_cb; cp.cb_eval_user_data = nullptr; }
     llama_context * ctx = llama_init_from_model(m, cp);
     if (!ctx) { fprintf(stderr, "context failed\n"); return 1; }
 
@@ -81,41 +121,67 @@ int main(int argc, char ** argv) {
         printf("{\"n_tokens\": %zu, \"n_vocab\": %d, \"incremental\": 1}\n", toks.size(), n_vocab);
     } else if (!toks.empty()) {
         llama_batch b = llama_batch_init((int) toks.size(), 0, 1);
+        const size_t first = last > 0 && (size_t) last < toks.size() ? toks.size() - last : 0;
         for (size_t i = 0; i < toks.size(); ++i) {
-            b.token[i] = toks[i]; b.pos[i] = (llama_pos) i; b.n_seq_id[i] = 1; b.seq_id[i][0] = 0; b.logits[i] = 1;
+            b.token[i] = toks[i]; b.pos[i] = (llama_pos) i; b.n_seq_id[i] = 1; b.seq_id[i][0] = 0; b.logits[i] = i >= first;
         }
         b.n_tokens = (int) toks.size();
         if (llama_decode(ctx, b) != 0) { fprintf(stderr, "decode failed\n"); return 1; }
         llama_synchronize(ctx);
         FILE * f = fopen(logits_out.c_str(), "wb");
-        for (size_t i = 0; i < toks.size(); ++i) fwrite(llama_get_logits_ith(ctx, (int) i), sizeof(float), n_vocab, f);
+        for (size_t i = first; i < toks.size(); ++i) fwrite(llama_get_logits_ith(ctx, (int) i), sizeof(float), n_vocab, f);
         fclose(f);
         llama_batch_free(b);
-        printf("{\"n_tokens\": %zu, \"n_vocab\": %d}\n", toks.size(), n_vocab);
+        printf("{\"n_tokens\": %zu, \"n_out\": %zu, \"n_vocab\": %d}\n", toks.size(), toks.size() - first, n_vocab);
     } else {
+        // llama-bench.cpp:1962-2010: a warmup run of each test, then R timed repetitions,
+        // each on a cleared KV cache; pp in n_batch-sized llama_decode calls
         std::srand(0);
-        std::vector<llama_token> p(pp);
-        for (auto & t : p) t = std::rand() % n_vocab;
-        double pp_s = 0;
-        if (pp > 0) {
-            const double t0 = now_s();
-            llama_decode(ctx, llama_batch_get_one(p.data(), pp));
+        auto run_pp = [&](int n) {
+            std::vector<llama_token> p(n);
+            for (auto & t : p) t = std::rand() % n_vocab;
+            for (int i = 0; i < n; i += cp.n_batch) {
+                const int nb = std::min<int>(cp.n_batch, n - i);
+                llama_decode(ctx, llama_batch_get_one(p.data() + i, nb));
+            }
             llama_synchronize(ctx);
-            pp_s = now_s() - t0;
+        };
+        auto run_tg = [&](int n) {
+            llama_token t = std::rand() % n_vocab;
+            for (int i = 0; i < n; ++i) {
+                llama_decode(ctx, llama_batch_get_one(&t, 1));
+                llama_synchronize(ctx);
+                t = std::rand() % n_vocab;
+            }
+        };
+        std::vector<double> pp_ts, tg_ts;
+        for (int r = -1; r < reps; ++r) {   // r = -1: warmup
+            if (pp > 0) {
+                llama_memory_clear(llama_get_memory(ctx), false);
+                const double t0 = now_s();
+                run_pp(pp);
+                if (r >= 0) pp_ts.push_back(pp / (now_s() - t0));
+            }
+            if (tg > 0) {
+                llama_memory_clear(llama_get_memory(ctx), false);
+                const double t1 = now_s();
+                run_tg(r < 0 ? 1 : tg);
+                if (r >= 0) tg_ts.push_back(tg / (now_s() - t1));
+            }
         }
-        llama_memory_clear(llama_get_memory(ctx), false);
-        const double t1 = now_s();
-        llama_token t = std::rand() % n_vocab;
-        for (int i = 0; i < tg; ++i) {
-            llama_decode(ctx, llama_batch_get_one(&t, 1));
-            llama_synchronize(ctx);
-            t = std::rand() % n_vocab;
-        }
-        const double tg_s = now_s() - t1;
-        printf("{\"pp\": %d, \"tg\": %d, \"threads\": %d, \"pp_tok_s\": %.3f, \"tg_tok_s\": %.3f}\n",
-               pp, tg, threads, pp > 0 ? pp / pp_s : 0.0, tg > 0 ? tg / tg_s : 0.0);
+        auto mean = [](const std::vector<double> & v) { double s = 0; for (double x : v) s += x; return v.empty() ? 0.0 : s / v.size(); };
+        auto list = [](const std::vector<double> & v) {
+            std::string s = "[";
+            for (size_t i = 0; i < v.size(); ++i) { char b[32]; snprintf(b, sizeof(b), "%s%.3f", i ? ", " : "", v[i]); s += b; }
+            return s + "]";
+        };
+        printf("{\"pp\": %d, \"tg\": %d, \"threads\": %d, \"reps\": %d, \"n_batch\": %d, \"n_ubatch\": %d, \"fa\": %d, "
+               "\"pp_tok_s\": %.3f, \"tg_tok_s\": %.3f, \"pp_samples\": %s, \"tg_samples\": %s}\n",
+               pp, tg, threads, reps, (int) cp.n_batch, (int) cp.n_ubatch, fa, mean(pp_ts), mean(tg_ts),
+               list(pp_ts).c_str(), list(tg_ts).c_str());
     }
     llama_free(ctx);
     llama_model_free(m);
+    if (g_dump) fclose(g_dump);
     return 0;
 }

@@ -18,7 +18,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} ;;
-    refops) OUT=$OUT/refops step refops 1200 bash scripts/gpu_ref_ops.sh ;;
+    refops) step refops 1200 env OUT=$OUT/refops bash scripts/gpu_ref_ops.sh ;;
     opbench) step opbench 900 bash scripts/opbench.sh ${OPBENCH_ARGS:-} ;;
     bench) step bench 900 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

@@ -354,3 +354,38 @@ def test_norm_absorbed_by_gemv(pkg, backend, orc, extra_use):
         assert nmse(res[2].reshape(1, K), 2.0 * xn) < 1e-10
     else:
         assert backend.stats()["nodes_fused"] >= before + 2, "norm was not deferred"
+
+
+@pytest.mark.parametrize("tname", ["q4_K", "q6_K", "q5_K", "q4_0", "q8_0"])
+@pytest.mark.parametrize("norm", [False, True])
+def test_gemv_lds_dma_staging_forced(pkg, backend, orc, tname, norm):
+    """the LDS-DMA activation prologue (XS_F32_LDS / XS_NORM_LDS: counted vmcnt wait + raw
+    s_barrier, gemv.cuh stage_finish) normally runs only on grids of >= 2048 waves;
+    g_tune[9] = 1 forces it at a small shape, K over several weight batches"""
+    lib = pkg._lib.load()
+    tid = NAMES[tname]
+    rng = np.random.default_rng(61)
+    K, M = 2048, 320
+    w, rb = rand_quant(tid, M, K, rng)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    nw = rng.uniform(0.5, 1.5, K).astype(np.float32)
+
+    def build(ctx):
+        tw = ctx.new_tensor(tid, K, M)
+        tx = ctx.new_tensor("f32", K, 1)
+        tn = ctx.new_tensor("f32", K)
+        src = ctx.mul(ctx.rms_norm(tx, 1e-5), tn) if norm else tx
+        return [ctx.mul_mat(tw, src)], [(tw, w), (tx, x), (tn, nw)]
+
+    lib.ggml_backend_mi355x_set_tune(9, 1)
+    backend.klog(True)
+    try:
+        y = run(pkg, backend, build)[0].reshape(1, M)
+        log = backend.klog_read()
+    finally:
+        backend.klog(False)
+        lib.ggml_backend_mi355x_set_tune(9, 0)
+    xin = orc.rms_norm(x, 1e-5) * nw if norm else x
+    assert nmse(y, orc.mul_mat(tid, w, rb, xin, exact=True)) < 5e-4
+    mode = 4 if norm else 3
+    assert any(ln.startswith("gemv2 ") and f" mode={mode} " in ln for ln in log), log

@@ -26,6 +26,17 @@ SHAPES = {
                  rope_base=10000.0),
     "small": dict(n_vocab=4096, n_embd=1024, n_layer=4, n_head=8, n_head_kv=2, n_ff=2816, n_ctx=2048,
                   rope_base=500000.0),
+    # two-layer models at the full widths of the bench configs: every decode / prefill
+    # kernel instantiation the Llama-3-8B / Mixtral benches time, in a GGUF the reference
+    # CPU backend runs in seconds (Q4_K_M over 2 layers: layer 0 Q4_K, layer 1 Q6_K v/down)
+    "llama3_8b_2l": dict(n_vocab=128256, n_embd=4096, n_layer=2, n_head=32, n_head_kv=8, n_ff=14336,
+                         n_ctx=8192, rope_base=500000.0),
+    "llama3_70b": dict(n_vocab=128256, n_embd=8192, n_layer=80, n_head=64, n_head_kv=8, n_ff=28672,
+                       n_ctx=8192, rope_base=500000.0),
+    "mixtral_8x7b": dict(n_vocab=32000, n_embd=4096, n_layer=32, n_head=32, n_head_kv=8, n_ff=14336,
+                         n_ctx=32768, rope_base=1e6, n_expert=8, n_expert_used=2),
+    "mixtral_2l": dict(n_vocab=32000, n_embd=4096, n_layer=2, n_head=32, n_head_kv=8, n_ff=14336,
+                       n_ctx=32768, rope_base=1e6, n_expert=8, n_expert_used=2),
     "tiny_moe": dict(n_vocab=1024, n_embd=256, n_layer=2, n_head=4, n_head_kv=2, n_ff=512, n_ctx=1024,
                      rope_base=10000.0, n_expert=4, n_expert_used=2),
 }
@@ -47,6 +58,12 @@ def tensor_plan(s, recipe):
     plan = []
 
     def main_t(i, kind):
+        # 8-expert models: attn_k / attn_v Q8_0 (llama-quant.cpp:311-321); 70B: attn_v
+        # Q4_K -> Q5_K (:305-310)
+        if n_exp == 8 and kind in ("k", "v") and recipe in ("q4_k_m", "q5_k_m"):
+            return "q8_0"
+        if kind == "v" and recipe == "q4_k_m" and E == 8192 and L == 80 and not use_more_bits(i, L):
+            return "q5_K"
         if recipe == "q4_k_m":
             return "q6_K" if kind in ("v", "down") and use_more_bits(i, L) else "q4_K"
         if recipe == "q5_k_m":
