@@ -172,6 +172,7 @@ static void be_free(ggml_backend_t b) {
     if (s->f16.base) hipFree(s->f16.base);
     if (s->rope_tab) hipFree(s->rope_tab);
     if (s->fa_cnt) hipFree(s->fa_cnt);
+    if (s->cpy_ev) hipEventDestroy(s->cpy_ev);
     hipStreamDestroy(s->stream);
     delete s;  // the ggml_backend struct lives inside Stream
 }
@@ -201,12 +202,11 @@ static bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const ggml_te
         HIP_CHECK(hipMemcpyPeerAsync(dst->data, ds->device, src->data, ss->device, n, ss->stream));
     }
     if (ss != ds) {
-        hipEvent_t ev;
-        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_CHECK(hipEventRecord(ev, ss->stream));
+        // the source stream's persistent event (re-recording it is legal once the wait
+        // below has been enqueued: the waiter captured the earlier record)
+        HIP_CHECK(hipEventRecord(ss->cpy_ev, ss->stream));
         HIP_CHECK(hipSetDevice(ds->device));
-        HIP_CHECK(hipStreamWaitEvent(ds->stream, ev, 0));
-        HIP_CHECK(hipEventDestroy(ev));  // destruction is deferred until the event completes
+        HIP_CHECK(hipStreamWaitEvent(ds->stream, ss->cpy_ev, 0));
     }
     return true;
 }
@@ -247,6 +247,7 @@ static ggml_backend_t make_backend(Device * d) {
     s->device = d->id;
     s->name = d->name;
     HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&s->cpy_ev, hipEventDisableTiming));
     HIP_CHECK(hipMalloc((void **) &s->rope_tab, MX_ROPE_TAB * sizeof(float2)));   // never inside a capture
     HIP_CHECK(hipMalloc((void **) &s->fa_cnt, MX_FA_CNT * sizeof(unsigned int)));
     HIP_CHECK(hipMemset(s->fa_cnt, 0, MX_FA_CNT * sizeof(unsigned int)));
@@ -362,6 +363,20 @@ static void init_registry() {
         d->buft = ggml_backend_buffer_type{kBuftIface, &d->dev, d.get()};
         d->host_buft = ggml_backend_buffer_type{kHostBuftIface, &d->dev, d.get()};
         g_devices.push_back(std::move(d));
+    }
+    // peer access between every pair of devices (reference: ggml_cuda_set_peer_access,
+    // ggml-cuda.cu:1374): the layer split's hipMemcpyPeerAsync then goes device to device
+    // over xGMI instead of staging through host memory. GGML_MI355X_NO_PEER=1 skips it.
+    if (n > 1 && !getenv("GGML_MI355X_NO_PEER")) {
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                int ok = 0;
+                if (i == j || hipDeviceCanAccessPeer(&ok, i, j) != hipSuccess || !ok) continue;
+                hipSetDevice(i);
+                const hipError_t e = hipDeviceEnablePeerAccess(j, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void) hipGetLastError();
+            }
+        hipSetDevice(0);
     }
     klog_env_init();
     g_reg.api_version = GGML_BACKEND_API_VERSION;

@@ -83,6 +83,7 @@ struct Stream {
     int device = 0;
     std::vector<DeferredNorm> deferred;
     hipStream_t stream = nullptr;
+    hipEvent_t cpy_ev = nullptr;       // cpy_tensor_async ordering event (one per stream, reused)
     Scratch scratch;
     Scratch act;                       // ring of quantised activations (act_cache)
     ActCacheEntry act_cache[4];

@@ -255,4 +255,18 @@ __device__ __forceinline__ uint16_t f2bf(float f) {  // round-to-nearest-even, N
 
 __device__ __forceinline__ int dot4_i8(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 
+// The one q8 activation quantiser of the backend (every producer of a q8 activation uses
+// it: GEMV prologues, the SwiGLU q8 emission, the fused RMS-norm q8 copy, the standalone
+// quantiser, the decode-attention combine), so an activation quantises identically whatever
+// path produced it. Semantics of quantize_q8_1 (ggml-cuda/quantize.cu:5-48): per 32 values
+// d = amax/127, q = round(x/d). The reciprocal is 127 * v_rcp_f32(amax) and the rounding
+// v_rndne_f32 (half to even): one instruction each instead of an IEEE division and roundf's
+// half-away sequence; results differ from roundf(x * (1/d)) only at exact .5 ties and in
+// the last ulp of 1/d.
+struct Q8Scale { float d, id; };
+__device__ __forceinline__ Q8Scale q8_scale(float amax) {
+    return Q8Scale{amax / 127.0f, amax == 0.0f ? 0.0f : 127.0f * __builtin_amdgcn_rcpf(amax)};
+}
+__device__ __forceinline__ int q8_round(float x, float id) { return (int) __builtin_rintf(x * id); }
+
 #endif  // __HIPCC__

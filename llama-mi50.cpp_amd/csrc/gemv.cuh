@@ -79,18 +79,15 @@ __device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) 
 #pragma unroll
     for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
     amax = fmaxf(amax, dpp_f<0xB1>(-INFINITY, amax));   // partner lane tid ^ 1
-    const float dd = amax / 127.0f;
-    // 127 · v_rcp_f32(amax) and round-to-nearest-even (v_rndne_f32): the IEEE division and
-    // the round-half-away sequence of roundf sat on the prologue's critical path (they
-    // differ from amax/127, roundf only in the last ulp of id / at exact .5 ties)
-    const float id = amax == 0.0f ? 0.0f : 127.0f * __builtin_amdgcn_rcpf(amax);
+    const Q8Scale qs = q8_scale(amax);   // common.h: the backend's one q8 quantiser
+    const float dd = qs.d, id = qs.id;
     int sum = 0, pk[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         int w = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int qi = (int) __builtin_rintf(v[4 * j + k] * id);
+            const int qi = q8_round(v[4 * j + k], id);
             sum += qi;
             w |= (qi & 0xFF) << (8 * k);
         }

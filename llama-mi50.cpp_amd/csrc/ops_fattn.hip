@@ -461,9 +461,9 @@ __global__ __launch_bounds__(64) void k_fattn_combine(const float * __restrict__
             float amax = d < D ? fabsf(v) : 0.f;
 #pragma unroll
             for (int off = 16; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 32));
-            const float dd = amax / 127.0f;
-            const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
-            const int qi = (int) roundf(v * id);
+            const Q8Scale qsc = q8_scale(amax);
+            const float dd = qsc.d;
+            const int qi = q8_round(v, qsc.id);
             int sum = qi;
 #pragma unroll
             for (int off = 16; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 32);

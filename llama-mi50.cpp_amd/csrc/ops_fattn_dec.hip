@@ -206,9 +206,13 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     __builtin_amdgcn_s_waitcnt(0);           // this thread's partial stores have completed
     __syncthreads();                         // ... and every thread's
     unsigned int * cnt = p.cnt + (iq3 * p.n_q + iq1) * slots + hslot;
-    if (tid == 0) s_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) (p.nsplit - 1);
+    // acq_rel at agent scope: the release orders this workgroup's partial stores before the
+    // count, the acquire makes every other split's partials visible to the last arrival
+    // (the memory model's guarantee, not only the write-through stores' hardware behaviour)
+    if (tid == 0) s_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) (p.nsplit - 1);
     __syncthreads();
     if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every thread of the merging workgroup
     const float * pb = p.part + (size_t) ((iq3 * p.n_q + iq1) * slots + hslot) * p.nsplit * PW;
     auto ld = [](const float * a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     // (max, sum) of every split in one parallel round trip, then per-split weights

@@ -68,9 +68,9 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
             if (wave < RPB / 32 && lane < 32) {
                 const float x = orow[32 * wave + lane];
                 const float amax = lane_bcast(dpp_max_group<32>(fabsf(x)), 31);
-                const float dd = amax / 127.0f;
-                const float id = amax == 0.0f ? 0.0f : 127.0f * __builtin_amdgcn_rcpf(amax);   // as q8_half
-                const int qi = (int) __builtin_rintf(x * id);
+                const Q8Scale qs = q8_scale(amax);
+                const float dd = qs.d;
+                const int qi = q8_round(x, qs.id);
                 const int sum = __builtin_amdgcn_readlane(dpp_sum_group_i<32>(qi), 31);
                 const int qb = blk * (RPB / 32) + wave;
                 p.q8o[qb * 32 + lane] = (int8_t) qi;

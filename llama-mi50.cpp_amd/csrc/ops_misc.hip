@@ -598,15 +598,15 @@ __global__ void k_rms_norm_q8(const char * __restrict__ x, const char * __restri
         float amax = 0.f;
 #pragma unroll
         for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
-        const float dd = amax / 127.0f;
-        const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
+        const Q8Scale qsc = q8_scale(amax);
+        const float dd = qsc.d, id = qsc.id;
         int sum = 0, packed[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             int wq = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int qi = (int) roundf(v[4 * j + k] * id);
+                const int qi = q8_round(v[4 * j + k], id);
                 sum += qi;
                 wq |= (qi & 0xFF) << (8 * k);
             }

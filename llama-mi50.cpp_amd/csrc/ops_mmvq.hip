@@ -39,8 +39,8 @@ __global__ void k_quantize_act(const char * __restrict__ x, int64_t K, int64_t n
     float amax = 0.f;
 #pragma unroll
     for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
-    const float dd = amax / 127.0f;
-    const float id = amax == 0.0f ? 0.0f : 1.0f / dd;
+    const Q8Scale qsc = q8_scale(amax);
+    const float dd = qsc.d, id = qsc.id;
     int sum = 0;
     int packed[8];
 #pragma unroll
@@ -48,7 +48,7 @@ __global__ void k_quantize_act(const char * __restrict__ x, int64_t K, int64_t n
         int w = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int qi = (int) roundf(v[4 * j + k] * id);
+            const int qi = q8_round(v[4 * j + k], id);
             sum += qi;
             w |= (qi & 0xFF) << (8 * k);
         }

@@ -59,6 +59,11 @@ def test_graph_replay_deterministic(pkg, backend, tiny):
 
 
 def test_unfused_executor_matches(pkg, tiny):
+    """fusion off and graphs off: the same logits up to float reduction order. Every q8
+    activation is made by the one quantiser (common.h q8_scale / q8_round), so the fused
+    paths (prologue quantisation, SwiGLU q8 emission) and the unfused ones (standalone
+    quantiser, fused RMS-norm q8 copy) round identically; what remains is the RMS sum's
+    order (per-workgroup prologue vs one norm kernel) and the FA split order."""
     rng = np.random.default_rng(4)
     toks = rng.integers(0, TINY["n_vocab"], 6).astype(np.int32)
     s = pkg.Session(tiny, n_ctx=256)
