@@ -11,13 +11,16 @@ logits copy-back. value = generated tokens / wall time. pp512 (one 512-token pre
 test_prompt :1962) is reported beside it.
 
 Multi-GPU (torchrun, one process per GPU, --mode pipeline, the default for N > 1): the
-layer split of SURVEY §8e. Rank r owns layers [r*L/N, (r+1)*L/N) of ONE model; the
-hidden state of each token goes to rank r+1 by RCCL point-to-point send/recv over xGMI.
-N sequences are decoded at once (one per pipeline slot), so every GPU is busy and the
-per-GPU work (128 tokens x L layers) is the same at every N ("weak"); value = all
-sequences' generated tokens / max wall time over ranks. --mode replicas runs a whole
-model per GPU instead. --model picks the BASELINE.json config (llama3_8b, llama3_70b,
-mixtral_8x7b, tinyllama).
+layer split of SURVEY §8e, as llama-bench -sm layer measures it. Rank r owns layers
+[r*L/N, (r+1)*L/N) of ONE model; the hidden state of each token goes to rank r+1 by RCCL
+point-to-point send/recv over xGMI. The headline value is ONE sequence (llama-bench tg128:
+every token passes all N stages in turn), so the total work is fixed as N grows
+("strong") and the curve is expected flat to declining: layer split buys capacity, not
+decode speed. `pipelined_tok_s` reports N sequences in flight (one per
+pipeline slot, every GPU busy) beside it. --mode replicas runs a whole model per GPU.
+--model picks the BASELINE.json config (llama3_8b, llama3_70b, mixtral_8x7b, tinyllama).
+Single GPU: `dropin` runs the reference's own libllama on this backend
+(GGML_BACKEND_PATH, -ngl 99) on the same GGUF shape — the drop-in throughput.
 """
 import argparse
 import ctypes
@@ -133,28 +136,89 @@ def roofline_glu(pkg, be, model, iters=256):
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(us, 2)}
 
 
+REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref-llama-bench")
+LIB = os.path.join(ROOT, "llama-mi50.cpp_amd", "lib", "libggml-mi355x.so")
+
+
+def bench_gguf(model="llama3_8b", recipe="q4_k_m"):
+    """the synthetic GGUF of the bench shape (tools/gguf_synth.py), written once per box"""
+    gguf = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mx_bench_{model}_{recipe}.gguf")
+    if not os.path.exists(gguf):
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gguf_synth.py"), "--shape", model,
+                        "--recipe", recipe, "--out", gguf + ".part"], check=True, timeout=900,
+                       stdout=subprocess.DEVNULL)
+        os.replace(gguf + ".part", gguf)
+    return gguf
+
+
+def host_threads():
+    """CPU threads this process may use: the affinity mask, capped by the cgroup CPU quota
+    (a GPU box shows the whole machine's CPUs but grants a share of them)"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return int(os.environ.get("MX_CPU_THREADS", n))
+
+
 def cpu_baseline(args):
     """Reference CPU backend (oracle/_ref, built from /root/reference sources) on the same
-    workload shape, bounded sample. Returns None when the reference build is absent."""
-    exe = os.path.join(ROOT, "oracle", "_ref", "ref-llama-bench")
-    if not os.path.exists(exe) or args.no_cpu_baseline:
+    GGUF, bounded sample, every CPU thread this process is granted (-t nproc).
+    Returns None when the reference build is absent."""
+    if not os.path.exists(REF_BENCH) or args.no_cpu_baseline:
         return None
-    threads = int(os.environ.get("MX_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    gguf = os.path.join(os.environ.get("TMPDIR", "/tmp"), "mx_bench_llama3_8b_q4km.gguf")
+    threads = host_threads()
     try:
-        if not os.path.exists(gguf):
-            subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gguf_synth.py"), "--shape", "llama3_8b",
-                            "--recipe", "q4_k_m", "--out", gguf], check=True, timeout=900)
-        r = subprocess.run([exe, "-m", gguf, "-t", str(threads), "-p", str(args.cpu_pp), "-n", str(args.cpu_tg)],
-                           capture_output=True, text=True, timeout=900)
+        gguf = bench_gguf()
+        r = subprocess.run([REF_BENCH, "-m", gguf, "-t", str(threads), "-p", str(args.cpu_pp), "-n", str(args.cpu_tg),
+                            "-r", "1"], capture_output=True, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         res = json.loads(line)
         return {"value": res["tg_tok_s"], "unit": "tok/s", "cores": threads, "kind": "reference",
                 "pp_tok_s": res.get("pp_tok_s"),
-                "sample": f"reference CPU backend (libllama+ggml-cpu from /root/reference), same GGUF shape/recipe, "
-                          f"tg{args.cpu_tg} after pp{args.cpu_pp}, {threads} threads"}
+                "sample": f"reference CPU backend (libllama+ggml-cpu from /root/reference), same GGUF, "
+                          f"tg{args.cpu_tg} and pp{args.cpu_pp} after one warmup each, {threads} threads "
+                          f"(os.cpu_count() = {os.cpu_count()})"}
     except Exception as e:  # noqa: BLE001 — the GPU number stays valid without the baseline
         return {"value": None, "unit": "tok/s", "cores": threads, "kind": "reference", "sample": f"failed: {e}"}
+
+
+def dropin_bench(args):
+    """The drop-in path as a user of the reference runs it: the reference's own libllama
+    (oracle/_ref/ref-llama-bench, llama-bench's test_prompt / test_gen loop,
+    tools/llama-bench/llama-bench.cpp:1962-2010, warmup + -r repetitions) loads
+    libggml-mi355x.so through GGML_BACKEND_PATH with every layer offloaded (-ngl 99), on
+    the same Llama-3-8B Q4_K_M GGUF. Reports tg128 and pp512 at -fa 1 and -fa 0 and the
+    executor's counters per llama_decode."""
+    if not os.path.exists(REF_BENCH) or args.no_dropin:
+        return None
+    out = {"how": "reference libllama (oracle/_ref/ref-llama-bench) + GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, "
+                  f"-r {args.dropin_reps}, llama-bench warmup"}
+    try:
+        gguf = bench_gguf()
+        env = dict(os.environ, GGML_BACKEND_PATH=LIB, GGML_MI355X_STATS="1")
+        for fa in (1, 0):
+            for test, pp, tg in (("tg128", 0, args.tg), ("pp512", args.pp, 0)):
+                if (pp or tg) == 0:
+                    continue
+                r = subprocess.run([REF_BENCH, "-m", gguf, "-t", "8", "-ngl", "99", "-fa", str(fa), "-p", str(pp),
+                                    "-n", str(tg), "-r", str(args.dropin_reps), "-c", str(max(256, pp + tg))],
+                                   capture_output=True, text=True, timeout=900, env=env)
+                line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+                if r.returncode != 0 or not line:
+                    out[f"{test}_fa{fa}"] = f"failed rc={r.returncode}: {r.stderr[-300:]}"
+                    continue
+                res = json.loads(line[-1])
+                out[f"{test}_fa{fa}_tok_s"] = res["tg_tok_s"] if tg else res["pp_tok_s"]
+                st = [json.loads(s.split("stats ", 1)[1]) for s in r.stderr.splitlines() if "[mi355x] stats" in s]
+                if st and tg:
+                    out[f"{test}_fa{fa}_executor"] = st[0]
+    except Exception as e:  # noqa: BLE001
+        out["error"] = str(e)
+    return out
 
 
 MODELS = {  # BASELINE.json configs -> (shape name in the package, default recipe, label)
@@ -228,12 +292,15 @@ class PipelineStage:
         if not self.host:
             self.torch.cuda.synchronize(self.dev)
 
-    def tg(self, rng, n_vocab, n_gen):
-        for s in self.sessions:
+    def tg(self, rng, n_vocab, n_gen, n_active=None):
+        """n_active sequences (default all) decode n_gen tokens each, interleaved so that
+        with n_active == N every stage works on a different sequence at a time"""
+        n_active = n_active or len(self.sessions)
+        for s in self.sessions[:n_active]:
             s.reset()
-        toks = rng.integers(0, n_vocab, size=(len(self.sessions), n_gen), dtype=np.int32)
+        toks = rng.integers(0, n_vocab, size=(n_active, n_gen), dtype=np.int32)
         for k in range(n_gen):
-            for si in range(len(self.sessions)):
+            for si in range(n_active):
                 self.item(si, toks[si, k:k + 1])
         self.drain()
 
@@ -262,9 +329,12 @@ def main():
     ap.add_argument("--recipe", default=None)
     ap.add_argument("--mode", default="auto", choices=["auto", "single", "pipeline", "replicas"],
                     help="N>1: pipeline = layer split over the ranks (default), replicas = one model per GPU")
-    ap.add_argument("--seqs", type=int, default=0, help="pipeline: sequences in flight (default = number of GPUs)")
+    ap.add_argument("--seqs", type=int, default=0,
+                    help="pipeline: sequences of the pipelined_tok_s extra (default = number of GPUs); the headline is 1")
     ap.add_argument("--no-fa", action="store_true", help="llama-bench -fa 0 graph (KQ mul_mat + softmax)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the reference-libllama drop-in measurement")
+    ap.add_argument("--dropin-reps", type=int, default=3)
     ap.add_argument("--cpu-pp", type=int, default=32)
     ap.add_argument("--cpu-tg", type=int, default=16)
     ap.add_argument("--skip-roofline", action="store_true")
@@ -306,8 +376,8 @@ def main():
         n_seq = args.seqs or world
         stage = PipelineStage(pkg, dist, rank, world, local, shape, recipe, not args.no_fa, n_ctx, n_seq)
         be, model = stage.be, stage.model
-        run_tg = lambda: stage.tg(rng, n_vocab, args.tg)   # noqa: E731
-        tokens_per_step = n_seq * args.tg                  # whole job (all ranks together)
+        run_tg = lambda: stage.tg(rng, n_vocab, args.tg, 1)   # noqa: E731 — llama-bench -sm layer: one sequence
+        tokens_per_step = args.tg                             # whole job (all ranks together)
     else:
         be = pkg.Backend(local if world > 1 else 0)
         model = pkg.Model.random(be, shape, recipe, seed=1234 + rank)
@@ -330,6 +400,16 @@ def main():
     else:
         tokens = sum_over_ranks(dist, args.steps * tokens_per_step)
     tg_value = tokens / dt
+
+    pipelined = None
+    if mode == "pipeline" and n_seq > 1:   # extra: N sequences in flight, one per stage
+        stage.tg(rng, n_vocab, args.tg)
+        barrier(dist, local)
+        t2 = time.perf_counter()
+        stage.tg(rng, n_vocab, args.tg)
+        barrier(dist, local)
+        pipelined = {"tok_s": round(n_seq * args.tg / max_over_ranks(dist, time.perf_counter() - t2), 2),
+                     "sequences": n_seq}
 
     # pp512 beside it (not the headline value)
     pp_tok_s = None
@@ -362,11 +442,12 @@ def main():
     decode_bytes = int(sum_over_ranks(dist, model.decode_bytes())) if mode == "pipeline" else model.decode_bytes()
     roof = None if (args.skip_roofline or shape.get("n_expert")) else roofline_glu(pkg, be, model)
     cpu = cpu_baseline(args) if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
+    dropin = dropin_bench(args) if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
 
     if rank == 0:
         per_gpu_bytes_s = decode_bytes * tg_value / world
         par = {"single": "single", "replicas": f"replicas x{world}",
-               "pipeline": f"layer split x{world} (RCCL p2p hidden-state hand-off), {tokens_per_step // max(args.tg, 1)} sequences in flight"}[mode]
+               "pipeline": f"layer split x{world} (RCCL p2p hidden-state hand-off), one sequence (llama-bench -sm layer)"}[mode]
         out = {
             "metric": METRIC,
             "value": round(tg_value, 2),
@@ -376,7 +457,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * dt / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if mode == "pipeline" else "weak",
             "vs_baseline": None,
             "dtype": "quantised weights (%s), int8 x int8 dot (v_dot4) + f32 accumulate" % recipe,
             "data": "synthetic (random %s weights generated on device, random tokens)" % recipe,
@@ -394,6 +475,8 @@ def main():
                                 "frac": round(per_gpu_bytes_s / 1e9 / HBM_PEAK_GBS, 4)},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "dropin": dropin,
+            "pipelined": pipelined,
             "executor": stats,
         }
         print(json.dumps(out), flush=True)

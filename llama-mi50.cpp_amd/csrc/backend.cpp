@@ -10,6 +10,7 @@
 #include "backend.h"
 #include "ggml_mi355x.h"
 
+#include <chrono>
 #include <cstdarg>
 #include <mutex>
 #include <memory>
@@ -153,6 +154,7 @@ static const ggml_backend_buffer_type_i kHostBuftIface = {
 Stream * stream_of(ggml_backend_t b) { return (Stream *) b->context; }
 
 static const char * be_name(ggml_backend_t b) { return stream_of(b)->name.c_str(); }
+static double now_us() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 void klog_dump(const char * path);
 static void be_free(ggml_backend_t b) {
     Stream * s = stream_of(b);
@@ -162,8 +164,12 @@ static void be_free(ggml_backend_t b) {
     // it (drop-in runs: shows the fusions fired on the reference's own node order)
     if (getenv("GGML_MI355X_STATS"))
         fprintf(stderr, "[mi355x] stats {\"backend\": \"%s\", \"graph_compute\": %llu, \"graph_replay\": %llu, "
-                "\"nodes_run\": %llu, \"nodes_fused\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
-                (unsigned long long) s->n_graph_replay, (unsigned long long) s->n_nodes_run, (unsigned long long) s->n_fused);
+                "\"nodes_run\": %llu, \"nodes_fused\": %llu, \"host_us\": {\"graph_compute\": %.0f, \"set_async\": %.0f, "
+                "\"get_async\": %.0f, \"synchronize\": %.0f}, \"n_set\": %llu, \"bytes_set\": %llu, \"n_get\": %llu, "
+                "\"bytes_get\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
+                (unsigned long long) s->n_graph_replay, (unsigned long long) s->n_nodes_run, (unsigned long long) s->n_fused,
+                s->us_compute, s->us_set, s->us_get, s->us_sync, (unsigned long long) s->n_set, (unsigned long long) s->b_set,
+                (unsigned long long) s->n_get, (unsigned long long) s->b_get);
     if (const char * kp = getenv("GGML_MI355X_KLOG")) klog_dump(kp);
     if (s->gcache.exec) hipGraphExecDestroy(s->gcache.exec);
     if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
@@ -178,13 +184,17 @@ static void be_free(ggml_backend_t b) {
 }
 static void be_set_async(ggml_backend_t b, ggml_tensor * t, const void * data, size_t off, size_t size) {
     Stream * s = stream_of(b);
+    const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));
     HIP_CHECK(hipMemcpyAsync((char *) t->data + off, data, size, hipMemcpyHostToDevice, s->stream));
+    s->us_set += now_us() - t0; s->n_set++; s->b_set += size;
 }
 static void be_get_async(ggml_backend_t b, const ggml_tensor * t, void * data, size_t off, size_t size) {
     Stream * s = stream_of(b);
+    const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));
     HIP_CHECK(hipMemcpyAsync(data, (const char *) t->data + off, size, hipMemcpyDeviceToHost, s->stream));
+    s->us_get += now_us() - t0; s->n_get++; s->b_get += size;
 }
 static bool is_our_backend(ggml_backend_t b);
 // Layer-split hand-off (ggml-backend.cpp:1568 → reference ggml-cuda.cu:2799-2852):
@@ -212,13 +222,17 @@ static bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const ggml_te
 }
 static void be_sync(ggml_backend_t b) {
     Stream * s = stream_of(b);
+    const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));
     HIP_CHECK(hipStreamSynchronize(s->stream));
+    s->us_sync += now_us() - t0;
 }
 static ggml_status be_graph_compute(ggml_backend_t b, ggml_cgraph * g) {
     Stream * s = stream_of(b);
+    const double t0 = now_us();
     ggml_status st = GGML_STATUS_SUCCESS;
     graph_compute_impl(s, g, &st);
+    s->us_compute += now_us() - t0;
     return st;
 }
 static void be_event_record(ggml_backend_t b, ggml_backend_event_t e) {

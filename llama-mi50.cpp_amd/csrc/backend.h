@@ -74,6 +74,7 @@ struct DeferredNorm {
     ggml_tensor * norm;
     const ggml_tensor * w;
     ggml_tensor * mul;
+    int pending;      // consumers (GEMVs) that have not run yet; 0: retired, never materialised
 };
 
 constexpr int MX_ROPE_TAB = 512;   // RoPE dimension pairs the per-token table holds
@@ -112,6 +113,11 @@ struct Stream {
     void * abort_data = nullptr;
     // profiling counters (read through mx_backend_stats)
     uint64_t n_graph_compute = 0, n_graph_replay = 0, n_nodes_run = 0, n_fused = 0;
+    // host-side cost of the backend entry points libllama calls per token (GGML_MI355X_STATS):
+    // microseconds spent inside graph_compute / set_async / get_async / synchronize, and
+    // the calls and bytes of the copies
+    double us_compute = 0, us_set = 0, us_get = 0, us_sync = 0;
+    uint64_t n_set = 0, n_get = 0, b_set = 0, b_get = 0;
 };
 
 // ---------------------------------------------------------------------------

@@ -31,26 +31,49 @@ size_t scratch_bytes(const ggml_tensor * n) {
     }
 }
 
-static void sig_tensor(std::vector<uint64_t> & k, const ggml_tensor * t) {
-    k.push_back(((uint64_t) t->op << 32) | (uint64_t) t->type);
-    for (int i = 0; i < 4; ++i) { k.push_back((uint64_t) t->ne[i]); k.push_back((uint64_t) t->nb[i]); }
-    k.push_back((uint64_t) (uintptr_t) t->data);
+// The cgraph signature (every node's op, type, shape, strides, data pointer and op params,
+// and the same of its sources) decides whether the captured hipGraph still applies. It is
+// compared against the stored one in place, word by word, overwriting where it differs:
+// no per-call vector, one pass (the decode graph is ~1,000 nodes and this runs on the
+// host between tokens, with the GPU idle).
+struct SigCursor {
+    std::vector<uint64_t> & k;
+    size_t pos = 0;
+    bool same = true;
+    inline void put(uint64_t v) {
+        if (pos < k.size()) {
+            if (k[pos] != v) { same = false; k[pos] = v; }
+        } else {
+            k.push_back(v);
+            same = false;
+        }
+        ++pos;
+    }
+};
+
+static inline void sig_tensor(SigCursor & c, const ggml_tensor * t) {
+    c.put(((uint64_t) t->op << 32) | (uint64_t) t->type);
+    for (int i = 0; i < 4; ++i) { c.put((uint64_t) t->ne[i]); c.put((uint64_t) t->nb[i]); }
+    c.put((uint64_t) (uintptr_t) t->data);
 }
 
-static void graph_signature(const ggml_cgraph * g, std::vector<uint64_t> & k) {
-    k.clear();
-    k.push_back((uint64_t) g->n_nodes);
+// returns true when g's signature equals the stored key (which is updated to g's)
+static bool graph_signature_same(const ggml_cgraph * g, std::vector<uint64_t> & key) {
+    SigCursor c{key};
+    c.put((uint64_t) g->n_nodes);
     for (int i = 0; i < g->n_nodes; ++i) {
         const ggml_tensor * n = g->nodes[i];
-        sig_tensor(k, n);
+        sig_tensor(c, n);
         const uint64_t * p = (const uint64_t *) n->op_params;
-        for (int j = 0; j < GGML_MAX_OP_PARAMS / 8; ++j) k.push_back(p[j]);
+        for (int j = 0; j < GGML_MAX_OP_PARAMS / 8; ++j) c.put(p[j]);
         for (int j = 0; j < GGML_MAX_SRC; ++j) {
             const ggml_tensor * s = n->src[j];
-            if (!s) { k.push_back(0); continue; }
-            sig_tensor(k, s);
+            if (!s) { c.put(0); continue; }
+            sig_tensor(c, s);
         }
     }
+    if (c.pos != key.size()) { key.resize(c.pos); c.same = false; }
+    return c.same;
 }
 
 // ---- fusion ---------------------------------------------------------------
@@ -168,8 +191,27 @@ static bool try_defer_norm(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
         }
     }
     if (found != need) return false;
-    c.s->deferred.push_back(DeferredNorm{norm, w, mul});
+    c.s->deferred.push_back(DeferredNorm{norm, w, mul, need});
     return true;
+}
+
+// Nodes [first, last] of the graph have run: a deferred norm whose last consumer was
+// among them is retired. Its output is dead from here on, so the allocator may hand its
+// memory (or its input's) to later tensors — without retirement their writes would
+// materialise the norm for nobody (libllama's allocation does exactly that: two wasted
+// RMS-norm launches per layer in the drop-in decode, profiles/r02/dropin_decode_v1).
+static void deferred_retire(Stream * s, ggml_cgraph * g, int first, int last) {
+    if (s->deferred.empty()) return;
+    for (int j = first; j <= last && j < g->n_nodes; ++j) {
+        const ggml_tensor * n = g->nodes[j];
+        if (n->op != GGML_OP_MUL_MAT) continue;
+        for (DeferredNorm & d : s->deferred)
+            if (n->src[1] == d.mul) --d.pending;
+    }
+    for (size_t k = 0; k < s->deferred.size();) {
+        if (s->deferred[k].pending <= 0) s->deferred.erase(s->deferred.begin() + k);
+        else ++k;
+    }
 }
 
 static bool try_fuse_rms_mul(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
@@ -307,19 +349,21 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         if (!done.empty() && done.count(n)) continue;
         s->scratch.reset();
         if (s->use_fusion) {
+            const int i0 = i;
             if (n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }
             if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
             if (n->op == GGML_OP_MUL_MAT && !g_no_qkv) {
                 const int k = fuse_qkv_rope_store(c, g, i, uses);
-                if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; continue; }
+                if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; deferred_retire(s, g, i0, i); continue; }
             }
-            if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
+            if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             if (n->op == GGML_OP_MUL_MAT && try_group_mm(c, g, i, done)) continue;
-            if (n->op == GGML_OP_MUL_MAT && try_fuse_mm_add(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
+            if (n->op == GGML_OP_MUL_MAT && try_fuse_mm_add(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; deferred_retire(s, g, i0, i); continue; }
         }
         deferred_guard_node(c, n);
         act_cache_invalidate(s, n);
         run_node(c, n);
+        deferred_retire(s, g, i, i);
         s->n_nodes_run++;
         if (g_sync_debug) {
             hipError_t e = hipStreamSynchronize(s->stream);
@@ -370,16 +414,14 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
 
     if (!s->use_graphs || g_sync_debug) { run_nodes(s, g); return; }
 
-    static thread_local std::vector<uint64_t> key;
-    graph_signature(g, key);
     GraphCache & gc = s->gcache;
-    if (gc.exec && key == gc.key) {
+    const bool same = graph_signature_same(g, gc.key);   // gc.key now holds g's signature
+    if (gc.exec && same) {
         HIP_CHECK(hipGraphLaunch(gc.exec, s->stream));
         s->n_graph_replay++;
         return;
     }
-    if (key != gc.key) {  // first sighting: run eagerly, remember the signature
-        gc.key = key;
+    if (!same) {  // first sighting: run eagerly, remember the signature
         gc.hits = 0;
         if (gc.exec) { HIP_CHECK(hipGraphExecDestroy(gc.exec)); gc.exec = nullptr; }
         if (gc.graph) { HIP_CHECK(hipGraphDestroy(gc.graph)); gc.graph = nullptr; }
