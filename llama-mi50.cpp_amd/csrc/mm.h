@@ -17,5 +17,16 @@ void mmv_generic_run(OpCtx & c, ggml_tensor * dst);
 bool mmq_type_ok(int t);
 size_t mmq_scratch(const ggml_tensor * dst);
 void mmq_run(OpCtx & c, ggml_tensor * dst);
+// f16 activation rows [cols][kp] of x for a prefill GEMM (act cache; ops_mm.hip)
+_Float16 * mmq_act_f16(OpCtx & c, const ggml_tensor * x, int64_t kp);
+
+// prefill GEMM v4 (ops_mmq4.hip): false when not eligible (nothing launched)
+bool mmq4_on();
+bool mmq4_mul_mat(OpCtx & c, const ggml_tensor * w, const ggml_tensor * x, const _Float16 * xa, int64_t kp,
+                  ggml_tensor * out, const ggml_tensor * res);
+bool mmq4_group(OpCtx & c, ggml_tensor * const * mms, int n, const _Float16 * xa, int64_t kp);
+bool mmq4_glu_ok(const ggml_tensor * wg, const ggml_tensor * wu, const ggml_tensor * x, const ggml_tensor * glu);
+void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const ggml_tensor * x, const _Float16 * xa,
+              int64_t kp, ggml_tensor * glu, _Float16 * h, int64_t h_col);
 
 }  // namespace mx

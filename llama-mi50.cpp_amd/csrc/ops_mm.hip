@@ -884,6 +884,7 @@ static _Float16 * mmq_act(OpCtx & c, const ggml_tensor * x, int64_t kp) {
     if (cacheable) { s->f16_src[k] = x->data; memcpy(s->f16_key[k], key, sizeof key); s->f16_last = k; }
     return xa;
 }
+_Float16 * mmq_act_f16(OpCtx & c, const ggml_tensor * x, int64_t kp) { return mmq_act(c, x, kp); }
 
 // out (default dst) receives the product, + res when given (K-quant MFMA kernels only:
 // the caller checks mmq_kq_ok)
@@ -901,6 +902,7 @@ static void mmq_run_ex(OpCtx & c, ggml_tensor * dst, ggml_tensor * out, const gg
     p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
     p.dbg = g_tune[13];
     const bool kq = w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
+    if (kq && !g_mmq_v1 && p.K % 256 == 0 && mmq4_mul_mat(c, w, x, xa, kp, out, res)) return;
     if (kq && !g_mmq_v1 && p.K % 256 == 0) {
         const int64_t tiles128 = mx_ceil_div(p.N, MM_BT) * mx_ceil_div(p.M, 128) * (x->ne[2] * x->ne[3]);
         int bm = tiles128 < 512 ? 64 : 128;
@@ -975,6 +977,11 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, 
     MmqArgs p{};
     p.w = (const char *) wg->data; p.w2 = (const char *) wu->data; p.w_row = wg->nb[1];
     p.x = mmq_act(c, x, kp); p.kp = kp;
+    if (mmq4_glu_ok(wg, wu, x, glu)) {
+        _Float16 * h = mmq_act_claim(c, glu->data, glu->ne[0], glu->ne[1], glu->nb[1]);
+        mmq4_glu(c, wg, wu, x, p.x, kp, glu, h, glu->ne[0]);
+        return true;
+    }
     p.dst = (float *) glu->data; p.d_col = glu->nb[1] / 4;
     p.M = wg->ne[1]; p.N = x->ne[1]; p.K = wg->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = g_tune[13];
     // the down projection reads this output: write its f16 copy too (claimed after the
@@ -1014,6 +1021,7 @@ bool mmq_group_run(OpCtx & c, ggml_tensor * const * mms, int n) {
     const int64_t kp = mmq_kp(mms[0]);
     MmqArgs p{};
     p.x = mmq_act(c, x, kp); p.kp = kp;
+    if (mmq4_group(c, mms, n, p.x, kp)) return true;
     p.N = x->ne[1]; p.K = x->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = g_tune[13];
     MmqSegs sg{};
     sg.n = n;

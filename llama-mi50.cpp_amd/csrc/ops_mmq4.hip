@@ -1,0 +1,483 @@
+// ops_mmq4.hip — prefill GEMM v4: K-quant weights dequantised in registers straight into
+// the MFMA operand, activations staged by LDS-DMA. Replaces mul_mat_q for batched
+// prefill (ggml-cuda/mmq.cuh:3364-3700, mmq.cu:262-366) on gfx950.
+//
+// Why a new skeleton (profiles/r01/pmc_prefill_sq.json): the v2/v3 kernels
+// dequantised weight tiles into LDS and read them back as MFMA operands — LDS writes,
+// reads, bank conflicts and two barriers per K step for data each wave then used alone;
+// MFMA was ~20 % busy. Here:
+//   * a wave owns 32 weight rows x 128 tokens (4 v_mfma_f32_32x32x16_f16 tiles); its
+//     lanes load their rows' quantised bytes (16-byte qs chunks) into registers one K
+//     chunk ahead and dequantise them just in time into the B operand — weights never
+//     touch LDS. Lane (r, h) holds row r, and k-slice h of every 16-deep MFMA step; the
+//     MFMA's k order is permuted to follow the super-block layout (a 16-byte qs chunk =
+//     16 low nibbles of one sub-block + 16 high nibbles of the next), the activation
+//     fragments are read in the same order;
+//   * the f16 activation tile (128 tokens x 128 k, 32 KB) is double-buffered in LDS and
+//     filled by LDS-DMA (global_load_lds, no registers, counted vmcnt + raw s_barrier:
+//     the weight stream stays in flight); 16-byte chunks XOR-swizzled by (token & 15);
+//   * dequantisation is packed f16 math on bit-assembled values: the nibble OR 0x6400
+//     is the f16 1024 + q (low nibbles), the high nibble in place OR 0x5400 is 64 + q;
+//     one v_pk_add removes the bias exactly, one v_pk_fma applies d*sc and -dmin*m —
+//     ~1.75 VALU per weight, hidden behind the MFMAs of the partner wave on the SIMD.
+//     Weights are scaled by 2^10 so d*sc stays a normal f16; the epilogue undoes it;
+//   * epilogues: store (+ residual), SwiGLU of a gate/up pair (waves 0-1 gate rows,
+//     2-3 up rows of the same 64; combined through LDS), the f16 copy of the output for
+//     the next GEMM (act cache), and the MoE gather/scatter of grouped expert tiles.
+#include "backend.h"
+#include "mm.h"
+#include "gemv.h"
+
+namespace mx {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int M4_TT = 4;          // 32-token MFMA tiles per wave
+constexpr int M4_BT = 32 * M4_TT; // tokens per workgroup
+constexpr int M4_KC = 128;        // K per chunk (half a super-block)
+constexpr int M4_MAXSEG = 3;
+constexpr float M4_WSCALE = 1024.0f;
+
+struct M4Seg {
+    const char * w; size_t w_row;
+    float * dst; size_t d_col;       // in floats
+    const float * res; size_t r_col; // + residual (nullable)
+    int M;
+    int isb;                         // weight type QTB (else QTA)
+    int tile0;                       // first row tile of the segment in grid.y
+};
+
+struct M4Args {
+    M4Seg seg[M4_MAXSEG];
+    int nseg;
+    const char * w2;                 // GLU: the up matrix (layout and type of seg[0])
+    const _Float16 * x; int64_t kp;  // activations f16 [cols][kp]
+    const int32_t * gather;          // MoE: activation column of token slot t (null: t)
+    const int32_t * scatter;         // MoE: output column of token slot t (null: t)
+    const int32_t * tile_tab;        // MoE: per-expert (token-slot start, count) pairs, grid.z = expert
+    size_t w_exp;                    // MoE: expert stride of the weights (bytes)
+    int N, K;
+    _Float16 * h; int64_t h_col;     // f16 copy of the output (next GEMM's input), nullable
+    int dbg;                         // timing experiments (g_tune[19]): 1 no MFMA, 2 no dequantisation,
+                                     // 4 no activation DMA, 8 weights of chunk 0 only
+};
+
+// ---------------------------------------------------------------------------
+// weight registers of one lane for one K chunk (its row, k-slice h = lane >> 5)
+// ---------------------------------------------------------------------------
+template <int QT> struct M4W;
+template <> struct M4W<GGML_TYPE_Q4_K> { int4 hd, q0, q1; };
+template <> struct M4W<GGML_TYPE_Q5_K> { int4 hd, q0, q1, h0, h1; };
+template <> struct M4W<GGML_TYPE_Q6_K> { int4 l0, l1, h0, h1, sc; uint32_t d; };
+
+template <int QT> __host__ __device__ constexpr int m4_loads() {   // vector loads per chunk (lower bound)
+    return QT == GGML_TYPE_Q4_K ? 3 : 5;
+}
+
+__device__ __forceinline__ int4 ldu16(const char * p) {   // 16 bytes at any 2-byte alignment
+    int4 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 2), 16);
+    return v;
+}
+
+template <int QT>
+__device__ __forceinline__ void m4_load(const char * row, int kc, int h, M4W<QT> & r) {
+    const int sb = kc >> 1, hf = kc & 1;
+    if constexpr (QT == GGML_TYPE_Q4_K) {
+        const char * b = row + (size_t) sb * 144;
+        r.hd = *(const int4 *) b;
+        r.q0 = *(const int4 *) (b + 16 + 16 * (4 * hf + 2 * h));
+        r.q1 = *(const int4 *) (b + 32 + 16 * (4 * hf + 2 * h));
+    } else if constexpr (QT == GGML_TYPE_Q5_K) {
+        const char * b = row + (size_t) sb * 176;
+        r.hd = *(const int4 *) b;
+        r.h0 = *(const int4 *) (b + 16);
+        r.h1 = *(const int4 *) (b + 32);
+        r.q0 = *(const int4 *) (b + 48 + 16 * (4 * hf + 2 * h));
+        r.q1 = *(const int4 *) (b + 64 + 16 * (4 * hf + 2 * h));
+    } else {
+        const char * b = row + (size_t) sb * 210;
+        r.l0 = ldu16(b + 64 * hf + 32 * h);
+        r.l1 = ldu16(b + 64 * hf + 32 * h + 16);
+        r.h0 = ldu16(b + 128 + 32 * hf);
+        r.h1 = ldu16(b + 128 + 32 * hf + 16);
+        r.sc = ldu16(b + 192);
+        r.d = *(const uint16_t *) (b + 208);
+    }
+}
+
+__device__ __forceinline__ uint32_t dw(const int4 & v, int i) {
+    return (uint32_t) (i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
+}
+// bytes 0,1 (sel01) or 2,3 (sel23) of w into the low bytes of the two halfwords
+__device__ __forceinline__ uint32_t pair_bytes(uint32_t w, int hi_pair) {
+    return __builtin_amdgcn_perm(0u, w, hi_pair ? 0x0c030c02u : 0x0c010c00u);
+}
+__device__ __forceinline__ h2 as_h2(uint32_t u) { h2 v; __builtin_memcpy(&v, &u, 4); return v; }
+
+// dequantised scales of one lane's unit: lo / hi sub-block (d*sc, -dmin*m) x 2^10, f16;
+// Q5_K also the qh bit index of the two sub-blocks
+struct M4Scale { h2 slo, mlo, shi, mhi; int gb; };
+
+template <int QT>
+__device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, int j) {
+    M4Scale s;
+    const int hf = kc & 1, U = 2 * h + j;
+    if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
+        const int g = 2 * hf + h;                              // sub-block pair (2g, 2g+1) of unit U
+        const uint32_t s0 = dw(r.hd, 1), s1 = dw(r.hd, 2), s2 = dw(r.hd, 3);
+        // get_scale_min_k4 (ggml-quants.c:703) of sub-blocks 2g, 2g+1, packed extraction
+        const uint32_t scw = g < 2 ? (s0 & 0x3F3F3F3Fu) : ((s2 & 0x0F0F0F0Fu) | ((s0 >> 2) & 0x30303030u));
+        const uint32_t mnw = g < 2 ? (s1 & 0x3F3F3F3Fu) : (((s2 >> 4) & 0x0F0F0F0Fu) | ((s1 >> 2) & 0x30303030u));
+        const uint32_t scp = scw >> (16 * (g & 1)), mnp = mnw >> (16 * (g & 1));
+        const float d = h2f((uint16_t) (dw(r.hd, 0) & 0xFFFF)) * M4_WSCALE;
+        const float dm = h2f((uint16_t) (dw(r.hd, 0) >> 16)) * M4_WSCALE;
+        const _Float16 a = (_Float16) (d * (float) (scp & 0xFF)), b = (_Float16) (d * (float) ((scp >> 8) & 0xFF));
+        const _Float16 c = (_Float16) (-dm * (float) (mnp & 0xFF)), e = (_Float16) (-dm * (float) ((mnp >> 8) & 0xFF));
+        s.slo = h2{a, a}; s.shi = h2{b, b}; s.mlo = h2{c, c}; s.mhi = h2{e, e};
+        s.gb = 2 * g;
+    } else {
+        // 16-wide groups: lo k = 128hf + 16U + i -> scale 8hf + U, hi (+64) -> 8hf + 4 + U
+        const int slo = 8 * hf + U, shi = slo + 4;
+        const float d = h2f((uint16_t) r.d) * M4_WSCALE;
+        const int8_t vlo = (int8_t) (dw(r.sc, slo >> 2) >> (8 * (slo & 3)));
+        const int8_t vhi = (int8_t) (dw(r.sc, shi >> 2) >> (8 * (shi & 3)));
+        const _Float16 a = (_Float16) (d * (float) vlo), b = (_Float16) (d * (float) vhi);
+        s.slo = h2{a, a}; s.shi = h2{b, b};
+        s.mlo = h2{0, 0}; s.mhi = h2{0, 0};
+        s.gb = 0;
+    }
+    return s;
+}
+
+// B operand of MFMA step q of unit j (q 0,1: the low sub-block's positions 8q..8q+7 of
+// the 16-byte chunk; q 2,3: the high one's 8(q-2)..), element e = position + e
+template <int QT>
+__device__ __forceinline__ h8 m4_deq(const M4W<QT> & r, const M4Scale & s, int h, int j, int q) {
+    const bool hi = q >= 2;
+    const int pd = 2 * (q & 1);                                // first of the chunk's two dwords
+    h8 out;
+    if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
+        const int4 & qs = j ? r.q1 : r.q0;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd) {
+            const uint32_t w = dw(qs, pd + dd);
+            uint32_t qh = 0;
+            if constexpr (QT == GGML_TYPE_Q5_K) qh = dw(j ? r.h1 : r.h0, pd + dd);   // qh byte = position
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const uint32_t x = pair_bytes(w, pp);
+                uint32_t v = hi ? ((x & 0x00F000F0u) | 0x54005400u)     // 64 + q (high nibble in place)
+                                : ((x & 0x000F000Fu) | 0x64006400u);    // 1024 + q
+                if constexpr (QT == GGML_TYPE_Q5_K) {
+                    const uint32_t y = pair_bytes(qh, pp);
+                    v |= hi ? (((y >> (s.gb + 1)) & 0x00010001u) << 8) : (((y >> s.gb) & 0x00010001u) << 4);
+                }
+                h2 f = as_h2(v) - (hi ? h2{64, 64} : h2{1024, 1024});
+                f = hi ? (f * s.shi + s.mhi) : (f * s.slo + s.mlo);
+                out[4 * dd + 2 * pp] = f[0];
+                out[4 * dd + 2 * pp + 1] = f[1];
+            }
+        }
+    } else {
+        const int4 & ql = j ? r.l1 : r.l0;
+        const int4 & qhv = j ? r.h1 : r.h0;
+        const int sh = (hi ? 4 : 0) + 2 * h;                   // qh bit pair: position < 32 (h 0) or not
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd) {
+            const uint32_t w = dw(ql, pd + dd), qh = dw(qhv, pd + dd);
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const uint32_t x = pair_bytes(w, pp), y = pair_bytes(qh, pp);
+                const uint32_t nib = hi ? (x & 0x00F000F0u) : ((x << 4) & 0x00F000F0u);
+                const uint32_t v = nib | (((y >> sh) & 0x00030003u) << 8) | 0x54005400u;   // 64 + q6
+                const h2 f = (as_h2(v) - h2{96, 96}) * (hi ? s.shi : s.slo);            // (q6 - 32) d sc
+                out[4 * dd + 2 * pp] = f[0];
+                out[4 * dd + 2 * pp + 1] = f[1];
+            }
+        }
+    }
+    return out;
+}
+
+// 16-byte chunk (8 k) of the 128-k activation tile that MFMA step q of unit j reads
+template <int QT>
+__device__ __forceinline__ int m4_ci(int h, int j, int q) {
+    if constexpr (QT == GGML_TYPE_Q6_K) return 4 * h + 2 * j + (q < 2 ? q : 6 + q);   // lo 16U, hi 64 + 16U
+    else return 8 * h + 2 * j + (q < 2 ? q : 2 + q);                                 // lo 64h + 16j, hi + 32
+}
+
+typedef __attribute__((address_space(3))) void * m4_lds_t;
+
+template <int N>
+__device__ __forceinline__ void m4_wait_vm() {   // s_waitcnt vmcnt(N), expcnt / lgkmcnt untouched
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ void m4_barrier() {   // LDS reads/writes of this wave done, then s_barrier
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+}
+
+// The K loop of one wave: rows `wrow` (its lane's row), tokens [tok0, tok0 + 32 TT).
+template <int QT, int TT>
+__device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, const int (&cols)[TT * 2],
+                                         uint4 * lds, f16v (&acc)[TT]) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    constexpr int NDMA = TT * 2;                 // 1-KB LDS-DMA pieces per wave per chunk
+    constexpr int TILE = 32 * TT * 16;           // uint4 per buffer
+    const int nk = p.K / M4_KC;
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+    auto dma = [&](int kc, int buf) {
+        if (p.dbg & 4) return;
+#pragma unroll
+        for (int i = 0; i < NDMA; ++i) {
+            const int trow = (wave * NDMA + i) * 4 + (lane >> 4);
+            const int slot = (lane & 15) ^ (trow & 15);
+            const _Float16 * g = p.x + (size_t) cols[i] * p.kp + (size_t) kc * M4_KC + 8 * slot;
+            __builtin_amdgcn_global_load_lds(g, (m4_lds_t) (lds + buf * TILE + (wave * NDMA + i) * 64), 16, 0, 0);
+        }
+    };
+    auto compute = [&](const M4W<QT> & rw, int kc, int buf) {
+        const uint4 * L = lds + buf * TILE;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const M4Scale s = m4_scales<QT>(rw, kc, h, j);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                h8 b;
+                if (p.dbg & 2) { b = h8{s.slo[0], s.slo[1], s.mlo[0], s.mlo[1], s.shi[0], s.shi[1], s.mhi[0], s.mhi[1]}; }
+                else b = m4_deq<QT>(rw, s, h, j, q);
+                const int ci = m4_ci<QT>(h, j, q) ^ (r & 15);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    const uint4 av = L[(32 * t + r) * 16 + ci];
+                    h8 a;
+                    __builtin_memcpy(&a, &av, 16);
+                    if (p.dbg & 1) acc[t][0] += (float) (a[0] * b[0]);
+                    else acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[t], 0, 0, 0);
+                }
+            }
+        }
+    };
+    M4W<QT> ra, rb;
+    dma(0, 0);
+    m4_load<QT>(wrow, 0, h, ra);
+    for (int kc = 0; kc < nk; kc += 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (kc + 1 < nk) {
+            dma(kc + 1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            m4_load<QT>(wrow, (p.dbg & 8) ? 0 : kc + 1, h, rb);
+            __builtin_amdgcn_sched_barrier(0);
+            m4_wait_vm<NDMA + m4_loads<QT>()>();     // chunk kc's DMA (and loads) landed
+        } else {
+            m4_wait_vm<0>();
+        }
+        m4_barrier();
+        compute(ra, kc, 0);
+        m4_barrier();                                 // buffer 0 free for chunk kc + 2
+        if (kc + 1 >= nk) break;
+        __builtin_amdgcn_sched_barrier(0);
+        if (kc + 2 < nk) {
+            dma(kc + 2, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            m4_load<QT>(wrow, (p.dbg & 8) ? 0 : kc + 2, h, ra);
+            __builtin_amdgcn_sched_barrier(0);
+            m4_wait_vm<NDMA + m4_loads<QT>()>();
+        } else {
+            m4_wait_vm<0>();
+        }
+        m4_barrier();
+        compute(rb, kc + 1, 1);
+        m4_barrier();
+    }
+}
+
+// EPI 0: store (+ residual) to the segment; 1: SwiGLU of a gate/up pair (waves 0-1 gate
+// rows, 2-3 up rows of the same 64); 2: MoE expert tile — grid.z = expert, token slots
+// gathered through p.gather, outputs scattered through p.scatter.
+template <int QTA, int QTB, int TT, int EPI>
+__global__ __launch_bounds__(256, 2) void k_mmq4(M4Args p) {
+    __shared__ __align__(16) uint4 lds[2 * 32 * TT * 16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    constexpr int BT = 32 * TT;
+    int si = 0;
+#pragma unroll
+    for (int i = 1; i < M4_MAXSEG; ++i) if (i < p.nseg && (int) blockIdx.y >= p.seg[i].tile0) si = i;
+    const M4Seg & sg = p.seg[si];
+    const int tile = (int) blockIdx.y - sg.tile0;
+    int tok0 = (int) blockIdx.x * BT, ntok = p.N, slot0 = 0;
+    const char * wb = sg.w;
+    if constexpr (EPI == 2) {
+        const int e = (int) blockIdx.z;
+        slot0 = p.tile_tab[2 * e];
+        ntok = p.tile_tab[2 * e + 1];
+        if (tok0 >= ntok) return;                     // block-uniform, before any barrier
+        wb += (size_t) e * p.w_exp;
+    }
+    // rows of this wave
+    const int rows_per_tile = EPI == 1 ? 64 : 128;
+    const int wr = EPI == 1 ? (wave & 1) : wave;
+    const int row = tile * rows_per_tile + wr * 32 + r;
+    const int rr = row < sg.M ? row : sg.M - 1;
+    const char * wrow = (EPI == 1 && wave >= 2 ? p.w2 : wb) + (size_t) rr * sg.w_row;
+    // activation columns of this wave's DMA pieces (token row clamped into range)
+    int cols[TT * 2];
+#pragma unroll
+    for (int i = 0; i < TT * 2; ++i) {
+        int t = tok0 + (wave * TT * 2 + i) * 4 + (lane >> 4);
+        t = t < ntok ? t : ntok - 1;
+        cols[i] = EPI == 2 ? p.gather[slot0 + t] : t;
+    }
+    f16v acc[TT];
+    if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT>(p, wrow, cols, lds, acc);
+    else m4_kloop<QTB, TT>(p, wrow, cols, lds, acc);
+
+    constexpr float inv = 1.0f / M4_WSCALE;
+    if constexpr (EPI == 1) {
+        float * red = (float *) lds;                  // 2 waves x TT x 16 x 64 floats (<= 2 buffers)
+        if (wave >= 2) {
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) red[(((wave - 2) * TT + t) * 16 + e) * 64 + lane] = acc[t][e];
+        }
+        m4_barrier();
+        if (wave >= 2) return;
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int tok = tok0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const float g = acc[t][e] * inv, u = red[((wave * TT + t) * 16 + e) * 64 + lane] * inv;
+                const float v = g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-g * 1.4426950408889634f)) * u;
+                if (tok < ntok && row < sg.M) {
+                    sg.dst[(size_t) tok * sg.d_col + row] = v;
+                    if (p.h) p.h[(size_t) tok * p.h_col + row] = (_Float16) v;
+                }
+            }
+    } else {
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int tok = tok0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (tok < ntok && row < sg.M) {
+                    float v = acc[t][e] * inv;
+                    const size_t oc = EPI == 2 ? (size_t) p.scatter[slot0 + tok] : (size_t) tok;
+                    if (EPI == 0 && sg.res) v += sg.res[oc * sg.r_col + row];
+                    sg.dst[oc * sg.d_col + row] = v;
+                    if (p.h) p.h[oc * p.h_col + row] = (_Float16) v;
+                }
+            }
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static bool m4_kq(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
+
+// g_tune[17]: 0 = v4 for the gate/up/SwiGLU pair only (where it measured faster), 1 = v4
+// off (the v2/v3 kernels run), 3 = v4 everywhere, 2 / 4 = v4 everywhere at 64 / 128 tokens
+// per tile
+bool mmq4_on() { return g_tune[17] != 1 && getenv("GGML_MI355X_MMQ4_OFF") == nullptr; }
+static bool m4_all() { return g_tune[17] >= 2; }
+
+template <int EPI, int TT>
+static bool m4_go(hipStream_t st, const M4Args & a, int ta, int tb, dim3 g) {
+#define M4K(A, B) if (ta == A && tb == B) { k_mmq4<A, B, TT, EPI><<<g, 256, 0, st>>>(a); return true; }
+    constexpr int Q4 = GGML_TYPE_Q4_K, Q5 = GGML_TYPE_Q5_K, Q6 = GGML_TYPE_Q6_K;
+    if constexpr (EPI == 0) {
+        M4K(Q4, Q4) M4K(Q4, Q6) M4K(Q6, Q4) M4K(Q5, Q5) M4K(Q5, Q6) M4K(Q6, Q5) M4K(Q6, Q6)
+    } else {
+        M4K(Q4, Q4) M4K(Q5, Q5) M4K(Q6, Q6)
+    }
+#undef M4K
+    return false;
+}
+
+// tokens per tile: 128 unless that leaves the chip under-filled (< 1.5 workgroups per CU)
+static int m4_tt(int64_t N, int64_t tiles_y) {
+    if (g_tune[17] == 2 || g_tune[17] == 4) return g_tune[17];
+    if (g_tune[18] == 2 || g_tune[18] == 4) return g_tune[18];
+    return mx_ceil_div(N, 128) * tiles_y >= 384 ? 4 : 2;
+}
+
+template <int EPI>
+static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int nz, int tt) {
+    const dim3 g((unsigned) mx_ceil_div(a.N, 32 * tt), (unsigned) tiles_y, (unsigned) nz);
+    a.dbg = g_tune[19];
+    return tt == 4 ? m4_go<EPI, 4>(c.st, a, ta, tb, g) : m4_go<EPI, 2>(c.st, a, ta, tb, g);
+}
+
+static bool m4_weight_ok(const ggml_tensor * w, int64_t K) {
+    return m4_kq(w->type) && w->ne[0] == K && K % 256 == 0 && w->ne[2] == 1 && w->ne[3] == 1 &&
+           w->nb[0] == (size_t) mx_type(w->type).size && ((uintptr_t) w->data % 16) == 0 && w->nb[1] % 16 == 0;
+}
+
+// out = W·x (+ res): one K-quant weight, x already in the f16 act cache (xa, kp)
+bool mmq4_mul_mat(OpCtx & c, const ggml_tensor * w, const ggml_tensor * x, const _Float16 * xa, int64_t kp,
+                  ggml_tensor * out, const ggml_tensor * res) {
+    if (!mmq4_on() || !m4_all() || !m4_weight_ok(w, x->ne[0]) || x->ne[2] * x->ne[3] != 1 || x->ne[1] > INT32_MAX) return false;
+    if (out->nb[0] != 4 || out->nb[1] % 4 || (res && (res->nb[0] != 4 || res->nb[1] % 4))) return false;
+    M4Args a{};
+    a.nseg = 1;
+    a.seg[0] = M4Seg{(const char *) w->data, w->nb[1], (float *) out->data, out->nb[1] / 4,
+                     res ? (const float *) res->data : nullptr, res ? res->nb[1] / 4 : 0, (int) w->ne[1], 0, 0};
+    a.x = xa; a.kp = kp; a.N = (int) x->ne[1]; a.K = (int) x->ne[0];
+    const int tiles = (int) mx_ceil_div(w->ne[1], 128), tt = m4_tt(a.N, tiles);
+    MX_KLOG("mmq4 qt=%d tt=%d M=%lld N=%d K=%d res=%d", (int) w->type, tt, (long long) w->ne[1], a.N, a.K, res != nullptr);
+    return m4_dispatch<0>(c, a, w->type, w->type, tiles, 1, tt);
+}
+
+// 2-3 MUL_MATs sharing x (q/k/v) in one launch; weights of at most two K-quant types
+bool mmq4_group(OpCtx & c, ggml_tensor * const * mms, int n, const _Float16 * xa, int64_t kp) {
+    if (!mmq4_on() || !m4_all() || n < 1 || n > M4_MAXSEG) return false;
+    const ggml_tensor * x = mms[0]->src[1];
+    const int ta = mms[0]->src[0]->type;
+    int tb = ta;
+    M4Args a{};
+    a.nseg = n;
+    int tiles = 0;
+    for (int k = 0; k < n; ++k) {
+        const ggml_tensor * m = mms[k], * w = m->src[0];
+        if (m->src[1] != x || !m4_weight_ok(w, x->ne[0]) || m->nb[0] != 4 || m->nb[1] % 4) return false;
+        if (w->type != ta) { if (tb != ta && tb != w->type) return false; tb = w->type; }
+        a.seg[k] = M4Seg{(const char *) w->data, w->nb[1], (float *) m->data, m->nb[1] / 4, nullptr, 0, (int) w->ne[1],
+                         w->type != ta, tiles};
+        tiles += (int) mx_ceil_div(w->ne[1], 128);
+    }
+    a.x = xa; a.kp = kp; a.N = (int) x->ne[1]; a.K = (int) x->ne[0];
+    const int tt = m4_tt(a.N, tiles);
+    MX_KLOG("mmq4 group n=%d qta=%d qtb=%d tt=%d N=%d K=%d", n, ta, tb, tt, a.N, a.K);
+    return m4_dispatch<0>(c, a, ta, tb, tiles, 1, tt);
+}
+
+// silu(Wg·x) * (Wu·x) into glu (+ its f16 copy h for the down projection)
+bool mmq4_glu_ok(const ggml_tensor * wg, const ggml_tensor * wu, const ggml_tensor * x, const ggml_tensor * glu) {
+    if (!mmq4_on() || !m4_weight_ok(wg, x->ne[0]) || !m4_weight_ok(wu, x->ne[0]) || wg->type != wu->type) return false;
+    return wg->nb[1] == wu->nb[1] && wg->ne[1] == wu->ne[1] && glu->nb[0] == 4 && glu->nb[1] % 4 == 0;
+}
+
+void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const ggml_tensor * x, const _Float16 * xa,
+              int64_t kp, ggml_tensor * glu, _Float16 * h, int64_t h_col) {
+    M4Args a{};
+    a.nseg = 1;
+    a.seg[0] = M4Seg{(const char *) wg->data, wg->nb[1], (float *) glu->data, glu->nb[1] / 4, nullptr, 0, (int) wg->ne[1], 0, 0};
+    a.w2 = (const char *) wu->data;
+    a.x = xa; a.kp = kp; a.N = (int) x->ne[1]; a.K = (int) x->ne[0];
+    a.h = h; a.h_col = h_col;
+    const int tiles = (int) mx_ceil_div(wg->ne[1], 64), tt = m4_tt(a.N, tiles);
+    MX_KLOG("mmq4 glu qt=%d tt=%d M=%lld N=%d K=%d", (int) wg->type, tt, (long long) wg->ne[1], a.N, a.K);
+    MX_ASSERT(m4_dispatch<1>(c, a, wg->type, wg->type, tiles, 1, tt));
+}
+
+}  // namespace mx

@@ -90,6 +90,8 @@ def kinds(klog):
     for ln in klog:
         f = dict(re.findall(r"(\w+)=(-?\d+)", ln))
         name = ln.split()[0]
+        if name == "mmq4" and ln.split()[1] in ("glu", "group"):
+            name = "mmq4 " + ln.split()[1]
         if name == "gemv2":
             name = f"gemv2 epi={f['epi']} mode={f['mode']} M={f['M']} q8o={f['q8o']}"
         c[name] += 1
@@ -149,8 +151,8 @@ def test_llama3_8b_width_pp512(l8b, tmp_path, fa):
     err = nmse(gpu, cpu)
     assert err < TOL, err
     k = kinds(klog)
-    assert k["mmq3g"] == 2, k            # fused gate/up/SwiGLU per layer
-    assert k["mmq3m"] == 2, k            # q/k/v in one launch per layer
+    assert k["mmq3g"] + k["mmq4 glu"] == 2, k     # fused gate/up/SwiGLU per layer
+    assert k["mmq3m"] + k["mmq4 group"] == 2, k   # q/k/v in one launch per layer
     if fa:
         assert k["fa_mma2"] == 2, k
 
@@ -167,7 +169,7 @@ def test_llama3_8b_width_pp2048(l8b, tmp_path):
     k = kinds(klog)
     # ubatches without outputs (the first three: --last 8) skip the last layer's FFN
     # (inp_out_ids selects no rows); the 8 output rows of the last take the GEMV path
-    assert k["fa_mma2"] == 4 * 2 and k["mmq3g"] == 4 + 0, k
+    assert k["fa_mma2"] == 4 * 2 and k["mmq3g"] + k["mmq4 glu"] == 4 + 0, k
     assert any("n_kv=2048" in ln or "n_kv=2304" in ln for ln in klog if ln.startswith("fa_mma2")), \
         [ln for ln in klog if ln.startswith("fa_mma2")]
 

@@ -82,6 +82,21 @@ def case_gemm(pkg, be, rng, tname, K, M, N=512):
     return ctx, [g]
 
 
+def case_gemm_glu(pkg, be, rng, tname, K, M, N=512):
+    """prefill gate/up/SwiGLU GEMM pair (fused): 2 x M weight rows x N tokens over K."""
+    tid = NAMES[tname]
+    wg, _ = rand_quant(tid, M, K, rng)
+    ctx = pkg.Context()
+    x = ctx.new_tensor("f32", K, N)
+    tg, tu = ctx.new_tensor(tid, K, M), ctx.new_tensor(tid, K, M)
+    g = ctx.build(ctx.swiglu_split(ctx.mul_mat(tg, x), ctx.mul_mat(tu, x)))
+    ctx.alloc(be)
+    tg.set(wg)
+    tu.set(wg)
+    x.set(rng.standard_normal((N, K)).astype(np.float32))
+    return ctx, [g]
+
+
 def case_ffn(pkg, be, rng, tname="q4_K", tdown="q4_K", K=4096, F=14336):
     """ffn_norm-less FFN block: gate/up SwiGLU GEMV (+q8 of its output) -> down + residual."""
     tid, tdn = NAMES[tname], NAMES[tdown]
@@ -210,6 +225,8 @@ CASES = {
     "pp_gate_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 14336),
     "pp_down_q6k": lambda p, b, r: case_gemm(p, b, r, "q6_K", 14336, 4096),
     "pp_k_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 1024),
+    "pp_glu_q4k": lambda p, b, r: case_gemm_glu(p, b, r, "q4_K", 4096, 14336),
+    "pp_down_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 14336, 4096),
     "ffn_q4k": lambda p, b, r: case_ffn(p, b, r),
     "ffn_block": lambda p, b, r: case_ffn_block(p, b, r),
     "ffn_q4k_q6k": lambda p, b, r: case_ffn(p, b, r, tdown="q6_K"),
