@@ -39,6 +39,7 @@ struct Scratch {
         return base + a;
     }
     void reset() { off = 0; }
+    size_t avail() const { const size_t a = (off + 255) & ~(size_t) 255; return a < cap ? cap - a : 0; }
 };
 
 // quantised activation columns: int8 values + per-32 f32 scale d and d·Σq

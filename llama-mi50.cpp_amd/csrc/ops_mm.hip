@@ -1094,7 +1094,7 @@ size_t mul_mat_scratch(const ggml_tensor * dst) {
     const ggml_tensor * x = dst->src[1];
     size_t s = 0;
     if (x->ne[1] <= 8 && quant_fast_path_ok(dst)) s = quantize_scratch(x);
-    else if (mmq_ok(dst)) s = mmq_scratch(dst);
+    else if (mmq_ok(dst)) s = mmq_scratch(dst) + mmq4_scratch(dst);
     return s;
 }
 

@@ -34,8 +34,6 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-constexpr int M4_TT = 4;          // 32-token MFMA tiles per wave
-constexpr int M4_BT = 32 * M4_TT; // tokens per workgroup
 constexpr int M4_KC = 128;        // K per chunk (half a super-block)
 constexpr int M4_MAXSEG = 3;
 constexpr float M4_WSCALE = 1024.0f;
@@ -60,8 +58,11 @@ struct M4Args {
     size_t w_exp;                    // MoE: expert stride of the weights (bytes)
     int N, K;
     _Float16 * h; int64_t h_col;     // f16 copy of the output (next GEMM's input), nullable
-    int dbg;                         // timing experiments (g_tune[19]): 1 no MFMA, 2 no dequantisation,
-                                     // 4 no activation DMA, 8 weights of chunk 0 only
+    int ksplit;                      // EPI 0: K shares over grid.z (1: no split)
+    float * part; int part_ld;       // split-K partial sums [ksplit][N][part_ld] (part_ld = padded rows)
+    unsigned long long * trace;      // debug (opbench --trace, slot 3): phase stamps of workgroup 0
+    int dbg;                         // timing experiments (g_tune[19]): 4 no activation DMA, 8 weights of
+                                     // chunk 0 only
 };
 
 // ---------------------------------------------------------------------------
@@ -221,90 +222,108 @@ __device__ __forceinline__ void m4_barrier() {   // LDS reads/writes of this wav
     __builtin_amdgcn_s_barrier();
 }
 
-// The K loop of one wave: rows `wrow` (its lane's row), tokens [tok0, tok0 + 32 TT).
+constexpr int M4_WAVES = 8;        // waves per workgroup (two per SIMD)
+constexpr int M4_S = 4;            // activation ring stages (prefetch distance M4_S - 1 chunks)
+
+// The K loop of one wave over chunks [c0, c0 + nc): its lane's row `wrow`, tokens
+// [tok0, tok0 + 32 TT) of the workgroup's activation ring (cols: activation column of
+// each of this wave's DMA pieces). Weight registers rotate over three sets (loads two
+// chunks ahead), the activation ring runs M4_S - 1 chunks ahead; one barrier per chunk
+// (it also retires the stage the previous chunk read, which the DMA then refills).
 template <int QT, int TT>
-__device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, const int (&cols)[TT * 2],
-                                         uint4 * lds, f16v (&acc)[TT]) {
+__device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, const int (&cols)[TT],
+                                         uint4 * lds, int c0, int nc, f16v (&acc)[TT], unsigned long long * tr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    constexpr int NDMA = TT * 2;                 // 1-KB LDS-DMA pieces per wave per chunk
-    constexpr int TILE = 32 * TT * 16;           // uint4 per buffer
-    const int nk = p.K / M4_KC;
+    constexpr int NDMA = TT;                     // 1-KB LDS-DMA pieces per wave per chunk (32 TT rows / 8 waves / 4 rows)
+    constexpr int TILE = 32 * TT * 16;           // uint4 per stage
+    constexpr int NW = m4_loads<QT>();
 #pragma unroll
     for (int t = 0; t < TT; ++t)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-    auto dma = [&](int kc, int buf) {
+    auto dma = [&](int i) {
         if (p.dbg & 4) return;
+        const int st = (i % M4_S) * TILE, kc = c0 + i;
 #pragma unroll
-        for (int i = 0; i < NDMA; ++i) {
-            const int trow = (wave * NDMA + i) * 4 + (lane >> 4);
+        for (int d = 0; d < NDMA; ++d) {
+            const int trow = (wave * NDMA + d) * 4 + (lane >> 4);
             const int slot = (lane & 15) ^ (trow & 15);
-            const _Float16 * g = p.x + (size_t) cols[i] * p.kp + (size_t) kc * M4_KC + 8 * slot;
-            __builtin_amdgcn_global_load_lds(g, (m4_lds_t) (lds + buf * TILE + (wave * NDMA + i) * 64), 16, 0, 0);
+            const _Float16 * g = p.x + (size_t) cols[d] * p.kp + (size_t) kc * M4_KC + 8 * slot;
+            __builtin_amdgcn_global_load_lds(g, (m4_lds_t) (lds + st + (wave * NDMA + d) * 64), 16, 0, 0);
         }
     };
-    auto compute = [&](const M4W<QT> & rw, int kc, int buf) {
-        const uint4 * L = lds + buf * TILE;
+    // activation fragments of step (j, q) for every token tile, read one step ahead so
+    // the LDS latency overlaps the previous step's MFMAs and this step's dequantisation.
+    // (No runtime switches in here: even a never-taken branch costs the loop its MFMA
+    // schedule — branches around every MFMA and accumulator copies at the joins.)
+    auto lda = [&](const uint4 * L, int j, int q, h8 (&a)[TT]) {
+        const int ci = m4_ci<QT>(h, j, q) ^ (r & 15);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int t = 0; t < TT; ++t) {
+            const uint4 av = L[(32 * t + r) * 16 + ci];
+            __builtin_memcpy(&a[t], &av, 16);
+        }
+    };
+    auto compute = [&](const M4W<QT> & rw, int i) {
+        const uint4 * L = lds + (i % M4_S) * TILE;
+        const int kc = c0 + i;
+        h8 a0[TT], a1[TT];
+        lda(L, 0, 0, a0);
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+            const int j = st >> 2, q = st & 3;
             const M4Scale s = m4_scales<QT>(rw, kc, h, j);
+            h8 (&cur)[TT] = (st & 1) ? a1 : a0;
+            h8 (&nxt)[TT] = (st & 1) ? a0 : a1;
+            if (st < 7) lda(L, (st + 1) >> 2, (st + 1) & 3, nxt);
+            const h8 b = m4_deq<QT>(rw, s, h, j, q);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                h8 b;
-                if (p.dbg & 2) { b = h8{s.slo[0], s.slo[1], s.mlo[0], s.mlo[1], s.shi[0], s.shi[1], s.mhi[0], s.mhi[1]}; }
-                else b = m4_deq<QT>(rw, s, h, j, q);
-                const int ci = m4_ci<QT>(h, j, q) ^ (r & 15);
-#pragma unroll
-                for (int t = 0; t < TT; ++t) {
-                    const uint4 av = L[(32 * t + r) * 16 + ci];
-                    h8 a;
-                    __builtin_memcpy(&a, &av, 16);
-                    if (p.dbg & 1) acc[t][0] += (float) (a[0] * b[0]);
-                    else acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[t], 0, 0, 0);
-                }
-            }
+            for (int t = 0; t < TT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], b, acc[t], 0, 0, 0);
         }
     };
-    M4W<QT> ra, rb;
-    dma(0, 0);
-    m4_load<QT>(wrow, 0, h, ra);
-    for (int kc = 0; kc < nk; kc += 2) {
+    auto wl = [&](int i, M4W<QT> & rw) { m4_load<QT>(wrow, (p.dbg & 8) ? c0 : c0 + i, h, rw); };
+    M4W<QT> r0, r1, r2;
+    // prologue: ring stages 0 .. S-2, weights of chunks 0 and 1
+#pragma unroll
+    for (int i = 0; i < M4_S - 1; ++i) if (i < nc) dma(i);
+    __builtin_amdgcn_sched_barrier(0);
+    wl(0, r0);
+    if (nc > 1) wl(1, r1);
+    __builtin_amdgcn_sched_barrier(0);
+    MX_TRACE(tr, 1);
+    auto iter = [&](int i, const M4W<QT> & rc, M4W<QT> & rn) {
+        // instructions issued after DMA(i): >= DMA(i+1), DMA(i+2) and two chunks of weight
+        // loads in steady state; the last chunks drain everything
+        if (i + 2 < nc) m4_wait_vm<2 * NDMA + 2 * NW>();
+        else m4_wait_vm<0>();
+        if (i == 2) MX_TRACE(tr, 2);
+        m4_barrier();
+        if (i == 2) MX_TRACE(tr, 3);
         __builtin_amdgcn_sched_barrier(0);
-        if (kc + 1 < nk) {
-            dma(kc + 1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            m4_load<QT>(wrow, (p.dbg & 8) ? 0 : kc + 1, h, rb);
-            __builtin_amdgcn_sched_barrier(0);
-            m4_wait_vm<NDMA + m4_loads<QT>()>();     // chunk kc's DMA (and loads) landed
-        } else {
-            m4_wait_vm<0>();
-        }
-        m4_barrier();
-        compute(ra, kc, 0);
-        m4_barrier();                                 // buffer 0 free for chunk kc + 2
-        if (kc + 1 >= nk) break;
+        if (i + M4_S - 1 < nc) dma(i + M4_S - 1);
         __builtin_amdgcn_sched_barrier(0);
-        if (kc + 2 < nk) {
-            dma(kc + 2, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            m4_load<QT>(wrow, (p.dbg & 8) ? 0 : kc + 2, h, ra);
-            __builtin_amdgcn_sched_barrier(0);
-            m4_wait_vm<NDMA + m4_loads<QT>()>();
-        } else {
-            m4_wait_vm<0>();
-        }
-        m4_barrier();
-        compute(rb, kc + 1, 1);
-        m4_barrier();
+        if (i + 2 < nc) wl(i + 2, rn);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(rc, i);
+        if (i == 2) MX_TRACE(tr, 4);
+        if (i == 5) MX_TRACE(tr, 5);
+    };
+    for (int i = 0; i < nc; i += 3) {
+        iter(i, r0, r2);
+        if (i + 1 < nc) iter(i + 1, r1, r0);
+        if (i + 2 < nc) iter(i + 2, r2, r1);
     }
+    MX_TRACE(tr, 6);
 }
 
-// EPI 0: store (+ residual) to the segment; 1: SwiGLU of a gate/up pair (waves 0-1 gate
-// rows, 2-3 up rows of the same 64); 2: MoE expert tile — grid.z = expert, token slots
+// EPI 0: store (+ residual) to the segment; 1: SwiGLU of a gate/up pair (waves 0-3 gate
+// rows, 4-7 up rows of the same 128); 2: MoE expert tile — grid.z = expert, token slots
 // gathered through p.gather, outputs scattered through p.scatter.
+// Split K (EPI 0, grid.z = p.ksplit > 1): each workgroup sums its share of the K chunks
+// into p.part[z][token][global row]; k_mmq4_reduce adds the shares in order.
 template <int QTA, int QTB, int TT, int EPI>
-__global__ __launch_bounds__(256, 2) void k_mmq4(M4Args p) {
-    __shared__ __align__(16) uint4 lds[2 * 32 * TT * 16];
+__global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
+    extern __shared__ __align__(16) uint4 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     constexpr int BT = 32 * TT;
     int si = 0;
@@ -314,42 +333,50 @@ __global__ __launch_bounds__(256, 2) void k_mmq4(M4Args p) {
     const int tile = (int) blockIdx.y - sg.tile0;
     int tok0 = (int) blockIdx.x * BT, ntok = p.N, slot0 = 0;
     const char * wb = sg.w;
+    const int nk = p.K / M4_KC;
+    int c0 = 0, nc = nk;
     if constexpr (EPI == 2) {
         const int e = (int) blockIdx.z;
         slot0 = p.tile_tab[2 * e];
         ntok = p.tile_tab[2 * e + 1];
         if (tok0 >= ntok) return;                     // block-uniform, before any barrier
         wb += (size_t) e * p.w_exp;
+    } else if (p.ksplit > 1) {
+        c0 = (int) blockIdx.z * nk / p.ksplit;
+        nc = ((int) blockIdx.z + 1) * nk / p.ksplit - c0;
     }
     // rows of this wave
-    const int rows_per_tile = EPI == 1 ? 64 : 128;
-    const int wr = EPI == 1 ? (wave & 1) : wave;
-    const int row = tile * rows_per_tile + wr * 32 + r;
+    constexpr int RPT = EPI == 1 ? 32 * M4_WAVES / 2 : 32 * M4_WAVES;   // output rows per tile
+    const int wr = EPI == 1 ? (wave & (M4_WAVES / 2 - 1)) : wave;
+    const int row = tile * RPT + wr * 32 + r;
     const int rr = row < sg.M ? row : sg.M - 1;
-    const char * wrow = (EPI == 1 && wave >= 2 ? p.w2 : wb) + (size_t) rr * sg.w_row;
+    const char * wrow = (EPI == 1 && wave >= M4_WAVES / 2 ? p.w2 : wb) + (size_t) rr * sg.w_row;
     // activation columns of this wave's DMA pieces (token row clamped into range)
-    int cols[TT * 2];
+    int cols[TT];
 #pragma unroll
-    for (int i = 0; i < TT * 2; ++i) {
-        int t = tok0 + (wave * TT * 2 + i) * 4 + (lane >> 4);
+    for (int i = 0; i < TT; ++i) {
+        int t = tok0 + (wave * TT + i) * 4 + (lane >> 4);
         t = t < ntok ? t : ntok - 1;
         cols[i] = EPI == 2 ? p.gather[slot0 + t] : t;
     }
     f16v acc[TT];
-    if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT>(p, wrow, cols, lds, acc);
-    else m4_kloop<QTB, TT>(p, wrow, cols, lds, acc);
+    unsigned long long * tr = (blockIdx.x | blockIdx.y | blockIdx.z) == 0 ? p.trace : nullptr;
+    MX_TRACE(tr, 0);
+    if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT>(p, wrow, cols, lds, c0, nc, acc, tr);
+    else m4_kloop<QTB, TT>(p, wrow, cols, lds, c0, nc, acc, tr);
 
     constexpr float inv = 1.0f / M4_WSCALE;
     if constexpr (EPI == 1) {
-        float * red = (float *) lds;                  // 2 waves x TT x 16 x 64 floats (<= 2 buffers)
-        if (wave >= 2) {
+        float * red = (float *) lds;                  // 4 waves x TT x 16 x 64 floats (<= the ring)
+        m4_barrier();                                 // every wave is done with the ring
+        if (wave >= M4_WAVES / 2) {
 #pragma unroll
             for (int t = 0; t < TT; ++t)
 #pragma unroll
-                for (int e = 0; e < 16; ++e) red[(((wave - 2) * TT + t) * 16 + e) * 64 + lane] = acc[t][e];
+                for (int e = 0; e < 16; ++e) red[(((wave - M4_WAVES / 2) * TT + t) * 16 + e) * 64 + lane] = acc[t][e];
         }
         m4_barrier();
-        if (wave >= 2) return;
+        if (wave >= M4_WAVES / 2) return;
 #pragma unroll
         for (int t = 0; t < TT; ++t)
 #pragma unroll
@@ -361,6 +388,15 @@ __global__ __launch_bounds__(256, 2) void k_mmq4(M4Args p) {
                     sg.dst[(size_t) tok * sg.d_col + row] = v;
                     if (p.h) p.h[(size_t) tok * p.h_col + row] = (_Float16) v;
                 }
+            }
+    } else if (EPI == 0 && p.ksplit > 1) {
+        float * part = p.part + (size_t) blockIdx.z * p.N * p.part_ld + sg.tile0 * RPT;
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int tok = tok0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (tok < ntok && row < sg.M) part[(size_t) tok * p.part_ld + row] = acc[t][e] * inv;
             }
     } else {
 #pragma unroll
@@ -379,21 +415,49 @@ __global__ __launch_bounds__(256, 2) void k_mmq4(M4Args p) {
     }
 }
 
+// split-K reduction: out = sum over shares z (in order) + residual, per segment
+__global__ void k_mmq4_reduce(M4Args p) {
+    const int tok = (int) blockIdx.y;
+    const int row = (int) (blockIdx.x * blockDim.x + threadIdx.x);   // global row over segments
+    if (row >= p.part_ld) return;
+    int si = 0;
+    for (int i = 1; i < p.nseg; ++i) if (row >= p.seg[i].tile0 * 32 * M4_WAVES) si = i;
+    const M4Seg & sg = p.seg[si];
+    const int lr = row - sg.tile0 * 32 * M4_WAVES;
+    if (lr >= sg.M) return;
+    float v = 0.f;
+    for (int z = 0; z < p.ksplit; ++z) v += p.part[((size_t) z * p.N + tok) * p.part_ld + row];
+    if (sg.res) v += sg.res[(size_t) tok * sg.r_col + lr];
+    sg.dst[(size_t) tok * sg.d_col + lr] = v;
+    if (p.h) p.h[(size_t) tok * p.h_col + lr] = (_Float16) v;
+}
 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static bool m4_kq(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
 
-// g_tune[17]: 0 = v4 for the gate/up/SwiGLU pair only (where it measured faster), 1 = v4
-// off (the v2/v3 kernels run), 3 = v4 everywhere, 2 / 4 = v4 everywhere at 64 / 128 tokens
-// per tile
+// g_tune[17]: 0 = v4 where it measured faster than v2/v3 (profiles/r02/opbench_mmq4.txt:
+// the gate/up/SwiGLU pair, and plain GEMMs over K >= 8192 — the FFN down projection), 1 =
+// v4 off, 3 = v4 everywhere, 2 / 4 = v4 everywhere at 64 / 128 tokens per tile
 bool mmq4_on() { return g_tune[17] != 1 && getenv("GGML_MI355X_MMQ4_OFF") == nullptr; }
 static bool m4_all() { return g_tune[17] >= 2; }
+static bool m4_plain_ok(int64_t K) { return m4_all() || (g_tune[17] == 0 && K >= 8192); }
+
+template <int QTA, int QTB, int TT, int EPI>
+static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
+    constexpr int lds = M4_S * 32 * TT * 256;
+    static const bool attr = [] {
+        HIP_CHECK(hipFuncSetAttribute((const void *) k_mmq4<QTA, QTB, TT, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        return true;
+    }();
+    (void) attr;
+    k_mmq4<QTA, QTB, TT, EPI><<<g, 64 * M4_WAVES, lds, st>>>(a);
+}
 
 template <int EPI, int TT>
 static bool m4_go(hipStream_t st, const M4Args & a, int ta, int tb, dim3 g) {
-#define M4K(A, B) if (ta == A && tb == B) { k_mmq4<A, B, TT, EPI><<<g, 256, 0, st>>>(a); return true; }
+#define M4K(A, B) if (ta == A && tb == B) { m4_kernel<A, B, TT, EPI>(st, a, g); return true; }
     constexpr int Q4 = GGML_TYPE_Q4_K, Q5 = GGML_TYPE_Q5_K, Q6 = GGML_TYPE_Q6_K;
     if constexpr (EPI == 0) {
         M4K(Q4, Q4) M4K(Q4, Q6) M4K(Q6, Q4) M4K(Q5, Q5) M4K(Q5, Q6) M4K(Q6, Q5) M4K(Q6, Q6)
@@ -404,18 +468,54 @@ static bool m4_go(hipStream_t st, const M4Args & a, int ta, int tb, dim3 g) {
     return false;
 }
 
-// tokens per tile: 128 unless that leaves the chip under-filled (< 1.5 workgroups per CU)
-static int m4_tt(int64_t N, int64_t tiles_y) {
+// tokens per tile: 128 (g_tune[18] = 2 forces 64)
+static int m4_tt() {
     if (g_tune[17] == 2 || g_tune[17] == 4) return g_tune[17];
     if (g_tune[18] == 2 || g_tune[18] == 4) return g_tune[18];
-    return mx_ceil_div(N, 128) * tiles_y >= 384 ? 4 : 2;
+    return 4;
+}
+
+// K shares so that the grid holds >= one workgroup per CU (the workgroup takes the CU:
+// 128 KB ring), each share >= 4 chunks; g_tune[20] forces it
+static int m4_ksplit(int64_t wgs, int nk) {
+    if (g_tune[20] > 0) return std::min(g_tune[20], nk);
+    int ks = 1;
+    while (wgs * ks < 256 && nk / (2 * ks) >= 4 && ks < 8) ks *= 2;
+    return ks;
+}
+
+size_t mmq4_scratch(const ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0], * x = dst->src[1];
+    if (!m4_kq(w->type) || x->ne[1] <= 8) return 0;
+    const int64_t rows = mx_ceil_div(w->ne[1] + w->ne[1] / 2, 256) * 256;   // room for a q/k/v group
+    const int ks = m4_ksplit(mx_ceil_div(x->ne[1], 128) * mx_ceil_div(w->ne[1], 256), (int) (w->ne[0] / M4_KC));
+    return ks > 1 ? (size_t) ks * x->ne[1] * rows * 4 + 256 : 0;
 }
 
 template <int EPI>
 static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int nz, int tt) {
-    const dim3 g((unsigned) mx_ceil_div(a.N, 32 * tt), (unsigned) tiles_y, (unsigned) nz);
     a.dbg = g_tune[19];
-    return tt == 4 ? m4_go<EPI, 4>(c.st, a, ta, tb, g) : m4_go<EPI, 2>(c.st, a, ta, tb, g);
+    a.trace = mx_trace_slot(3);
+    const int nk = a.K / M4_KC;
+    const int64_t gx = mx_ceil_div(a.N, 32 * tt);
+    a.ksplit = 1;
+    if (EPI == 0) {
+        int ks = m4_ksplit(gx * tiles_y, nk);
+        const size_t need = (size_t) ks * a.N * tiles_y * 32 * M4_WAVES * 4;
+        if (ks > 1 && c.scratch->avail() >= need + 256) {
+            a.ksplit = ks;
+            a.part_ld = tiles_y * 32 * M4_WAVES;
+            a.part = (float *) c.scratch->take(need);
+            nz = ks;
+        }
+    }
+    const dim3 g((unsigned) gx, (unsigned) tiles_y, (unsigned) nz);
+    const bool ok = tt == 4 ? m4_go<EPI, 4>(c.st, a, ta, tb, g) : m4_go<EPI, 2>(c.st, a, ta, tb, g);
+    if (ok && a.ksplit > 1) {
+        const dim3 gr((unsigned) mx_ceil_div(a.part_ld, 256), (unsigned) a.N);
+        k_mmq4_reduce<<<gr, 256, 0, c.st>>>(a);
+    }
+    return ok;
 }
 
 static bool m4_weight_ok(const ggml_tensor * w, int64_t K) {
@@ -426,14 +526,14 @@ static bool m4_weight_ok(const ggml_tensor * w, int64_t K) {
 // out = W·x (+ res): one K-quant weight, x already in the f16 act cache (xa, kp)
 bool mmq4_mul_mat(OpCtx & c, const ggml_tensor * w, const ggml_tensor * x, const _Float16 * xa, int64_t kp,
                   ggml_tensor * out, const ggml_tensor * res) {
-    if (!mmq4_on() || !m4_all() || !m4_weight_ok(w, x->ne[0]) || x->ne[2] * x->ne[3] != 1 || x->ne[1] > INT32_MAX) return false;
+    if (!mmq4_on() || !m4_plain_ok(x->ne[0]) || !m4_weight_ok(w, x->ne[0]) || x->ne[2] * x->ne[3] != 1 || x->ne[1] > INT32_MAX) return false;
     if (out->nb[0] != 4 || out->nb[1] % 4 || (res && (res->nb[0] != 4 || res->nb[1] % 4))) return false;
     M4Args a{};
     a.nseg = 1;
     a.seg[0] = M4Seg{(const char *) w->data, w->nb[1], (float *) out->data, out->nb[1] / 4,
                      res ? (const float *) res->data : nullptr, res ? res->nb[1] / 4 : 0, (int) w->ne[1], 0, 0};
     a.x = xa; a.kp = kp; a.N = (int) x->ne[1]; a.K = (int) x->ne[0];
-    const int tiles = (int) mx_ceil_div(w->ne[1], 128), tt = m4_tt(a.N, tiles);
+    const int tiles = (int) mx_ceil_div(w->ne[1], 32 * M4_WAVES), tt = m4_tt();
     MX_KLOG("mmq4 qt=%d tt=%d M=%lld N=%d K=%d res=%d", (int) w->type, tt, (long long) w->ne[1], a.N, a.K, res != nullptr);
     return m4_dispatch<0>(c, a, w->type, w->type, tiles, 1, tt);
 }
@@ -453,10 +553,10 @@ bool mmq4_group(OpCtx & c, ggml_tensor * const * mms, int n, const _Float16 * xa
         if (w->type != ta) { if (tb != ta && tb != w->type) return false; tb = w->type; }
         a.seg[k] = M4Seg{(const char *) w->data, w->nb[1], (float *) m->data, m->nb[1] / 4, nullptr, 0, (int) w->ne[1],
                          w->type != ta, tiles};
-        tiles += (int) mx_ceil_div(w->ne[1], 128);
+        tiles += (int) mx_ceil_div(w->ne[1], 32 * M4_WAVES);
     }
     a.x = xa; a.kp = kp; a.N = (int) x->ne[1]; a.K = (int) x->ne[0];
-    const int tt = m4_tt(a.N, tiles);
+    const int tt = m4_tt();
     MX_KLOG("mmq4 group n=%d qta=%d qtb=%d tt=%d N=%d K=%d", n, ta, tb, tt, a.N, a.K);
     return m4_dispatch<0>(c, a, ta, tb, tiles, 1, tt);
 }
@@ -475,7 +575,7 @@ void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const g
     a.w2 = (const char *) wu->data;
     a.x = xa; a.kp = kp; a.N = (int) x->ne[1]; a.K = (int) x->ne[0];
     a.h = h; a.h_col = h_col;
-    const int tiles = (int) mx_ceil_div(wg->ne[1], 64), tt = m4_tt(a.N, tiles);
+    const int tiles = (int) mx_ceil_div(wg->ne[1], 16 * M4_WAVES), tt = m4_tt();
     MX_KLOG("mmq4 glu qt=%d tt=%d M=%lld N=%d K=%d", (int) wg->type, tt, (long long) wg->ne[1], a.N, a.K);
     MX_ASSERT(m4_dispatch<1>(c, a, wg->type, wg->type, tiles, 1, tt));
 }

@@ -303,7 +303,7 @@ def main():
             be.synchronize()
             lib.ggml_backend_mi355x_trace_read(buf, 2048)
             lib.ggml_backend_mi355x_set_tune(6, 0)
-            for slot, sname in enumerate(["fa_dec", "gemv", "qkv"]):
+            for slot, sname in enumerate(["fa_dec", "gemv", "qkv", "mmq4"]):
                 for w in range(16):
                     t = [buf[slot * 128 + w * 8 + k] for k in range(8)]
                     if t[0] == 0:
