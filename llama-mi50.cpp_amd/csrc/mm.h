@@ -23,6 +23,8 @@ _Float16 * mmq_act_f16(OpCtx & c, const ggml_tensor * x, int64_t kp);
 // prefill GEMM v4 (ops_mmq4.hip): false when not eligible (nothing launched)
 bool mmq4_on();
 size_t mmq4_scratch(const ggml_tensor * dst);   // split-K partial sums
+size_t mmq4_moe_scratch(const ggml_tensor * dst);
+bool mmq4_moe(OpCtx & c, ggml_tensor * dst);     // MUL_MAT_ID prefill, expert-grouped
 bool mmq4_mul_mat(OpCtx & c, const ggml_tensor * w, const ggml_tensor * x, const _Float16 * xa, int64_t kp,
                   ggml_tensor * out, const ggml_tensor * res);
 bool mmq4_group(OpCtx & c, ggml_tensor * const * mms, int n, const _Float16 * xa, int64_t kp);

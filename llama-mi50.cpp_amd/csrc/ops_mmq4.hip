@@ -580,4 +580,91 @@ void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const g
     MX_ASSERT(m4_dispatch<1>(c, a, wg->type, wg->type, tiles, 1, tt));
 }
 
+
+// ---------------------------------------------------------------------------
+// MUL_MAT_ID (MoE) prefill: expert-grouped GEMM. The (token, slot) items are sorted by
+// expert on the device (no host sync, graph-capturable — reference: mm_ids_helper,
+// ggml-cuda/mmid.cu:28-160, and mul_mat_id's per-expert mmq, mmq.cu:160-217); each
+// expert's items then run as k_mmq4 tiles (grid.z = expert), the activation rows gathered
+// and the outputs scattered through the sorted lists.
+// ---------------------------------------------------------------------------
+constexpr int M4_MAXEXP = 1024;
+
+__global__ __launch_bounds__(1024) void k_moe_sort(const char * ids, size_t id0, size_t id1, int n_used, int n_tok,
+                                                  int n_expert, int ne11, int32_t * gather, int32_t * scatter,
+                                                  int32_t * tile_tab) {
+    __shared__ int cnt[M4_MAXEXP], cur[M4_MAXEXP];
+    const int tid = threadIdx.x, n = n_used * n_tok;
+    for (int e = tid; e < n_expert; e += blockDim.x) cnt[e] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += blockDim.x) {
+        const int t = i / n_used, sl = i % n_used;
+        const int ex = *(const int32_t *) (ids + (size_t) sl * id0 + (size_t) t * id1);
+        if (ex >= 0 && ex < n_expert) atomicAdd(&cnt[ex], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int e = 0; e < n_expert; ++e) {
+            tile_tab[2 * e] = acc;
+            tile_tab[2 * e + 1] = cnt[e];
+            cur[e] = acc;
+            acc += cnt[e];
+        }
+    }
+    __syncthreads();
+    // positions inside an expert's list depend on arrival order; each item's result does not
+    for (int i = tid; i < n; i += blockDim.x) {
+        const int t = i / n_used, sl = i % n_used;
+        const int ex = *(const int32_t *) (ids + (size_t) sl * id0 + (size_t) t * id1);
+        if (ex < 0 || ex >= n_expert) continue;
+        const int pos = atomicAdd(&cur[ex], 1);
+        gather[pos] = t * ne11 + sl % ne11;     // activation column of b [K, ne11, n_tok]
+        scatter[pos] = t * n_used + sl;         // output column of dst [M, n_used, n_tok]
+    }
+}
+
+static bool m4_moe_ok(const ggml_tensor * dst) {
+    const ggml_tensor * as = dst->src[0], * b = dst->src[1], * ids = dst->src[2];
+    if (!mmq4_on() || !m4_kq(as->type) || as->ne[0] % 256 || as->ne[3] != 1 || as->ne[2] > M4_MAXEXP) return false;
+    if (as->nb[0] != (size_t) mx_type(as->type).size || ((uintptr_t) as->data % 16) || as->nb[1] % 16 || as->nb[2] % 16) return false;
+    if (b->type != GGML_TYPE_F32 || b->ne[0] != as->ne[0] || b->ne[3] != 1 || b->nb[0] != 4) return false;
+    if (ids->type != GGML_TYPE_I32 || dst->type != GGML_TYPE_F32 || dst->nb[0] != 4) return false;
+    if (dst->nb[2] != dst->nb[1] * dst->ne[1] || dst->nb[1] % 4) return false;     // [M, n_used, n_tok] rows
+    const int64_t items = ids->ne[0] * ids->ne[1];
+    return items >= 32 && ids->ne[1] == b->ne[2] && dst->ne[1] == ids->ne[0];
+}
+
+size_t mmq4_moe_scratch(const ggml_tensor * dst) {
+    if (!m4_moe_ok(dst)) return 0;
+    const ggml_tensor * b = dst->src[1], * ids = dst->src[2];
+    const size_t items = ids->ne[0] * ids->ne[1];
+    return (size_t) b->ne[1] * b->ne[2] * b->ne[0] * 2 + 2 * items * 4 + 2 * M4_MAXEXP * 4 + 1024;
+}
+
+bool mmq4_moe(OpCtx & c, ggml_tensor * dst) {
+    if (!m4_moe_ok(dst)) return false;
+    const ggml_tensor * as = dst->src[0], * b = dst->src[1], * ids = dst->src[2];
+    const int n_used = (int) ids->ne[0], n_tok = (int) ids->ne[1], n_exp = (int) as->ne[2];
+    const int items = n_used * n_tok;
+    int32_t * gather = (int32_t *) c.scratch->take((size_t) items * 4);
+    int32_t * scatter = (int32_t *) c.scratch->take((size_t) items * 4);
+    int32_t * tab = (int32_t *) c.scratch->take((size_t) 2 * M4_MAXEXP * 4);
+    k_moe_sort<<<1, 1024, 0, c.st>>>((const char *) ids->data, ids->nb[0], ids->nb[1], n_used, n_tok, n_exp,
+                                     (int) b->ne[1], gather, scatter, tab);
+    const int64_t kp = as->ne[0];
+    const _Float16 * xa = mmq_act_f16(c, b, kp);
+    M4Args a{};
+    a.nseg = 1;
+    a.seg[0] = M4Seg{(const char *) as->data, as->nb[1], (float *) dst->data, dst->nb[1] / 4, nullptr, 0, (int) as->ne[1], 0, 0};
+    a.x = xa; a.kp = kp; a.N = items; a.K = (int) as->ne[0];
+    a.gather = gather; a.scatter = scatter; a.tile_tab = tab; a.w_exp = as->nb[2];
+    const int tt = m4_tt(), tiles = (int) mx_ceil_div(as->ne[1], 32 * M4_WAVES);
+    MX_KLOG("mmq4 moe qt=%d tt=%d M=%lld items=%d experts=%d K=%d", (int) as->type, tt, (long long) as->ne[1], items, n_exp, a.K);
+    // grid.x covers the worst case (every item on one expert); the tiles past an expert's
+    // count exit at once
+    MX_ASSERT(m4_dispatch<2>(c, a, as->type, as->type, tiles, n_exp, tt));
+    return true;
+}
+
 }  // namespace mx

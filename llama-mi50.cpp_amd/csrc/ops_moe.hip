@@ -84,6 +84,7 @@ bool mul_mat_id_supported(const ggml_tensor * dst) {
 
 size_t mul_mat_id_scratch(const ggml_tensor * dst) {
     const ggml_tensor * as = dst->src[0];
+    if (const size_t g = mmq4_moe_scratch(dst)) return g;
     if (mmvq_type_ok(as->type) && as->ne[0] % qk_of_type(as->type) == 0) return quantize_scratch(dst->src[1]);
     return 0;
 }
@@ -108,6 +109,7 @@ void op_mul_mat_id(OpCtx & c, ggml_tensor * dst) {
     p.n_used = ids->ne[0]; p.ne11 = b->ne[1]; p.n_expert = as->ne[2];
     const int64_t items = ids->ne[0] * ids->ne[1];
     if (items == 0) return;
+    if (mmq4_moe(c, dst)) return;     // prefill: expert-grouped MFMA GEMM (ops_mmq4.hip)
     if (mmvq_type_ok(as->type) && as->ne[0] % qk_of_type(as->type) == 0) {
         ActQ a = quantize_activations(c, b);
         switch (as->type) {
