@@ -264,6 +264,35 @@ static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     return mmvq_fused_glu(c, gate, up, glu) || mmq_fused_glu(c, gate, up, glu);
 }
 
+// MUL_MAT_ID(gate), MUL_MAT_ID(up), GLU of a decode step (llama build_moe_ffn): one v2
+// GEMV over both expert streams per (slot, token) item, SwiGLU epilogue, and the q8 of
+// the result for the down projection's prologue
+static bool try_fuse_moe_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
+    if (i + 2 >= g->n_nodes) return false;
+    ggml_tensor * a = g->nodes[i];
+    ggml_tensor * b = g->nodes[i + 1];
+    ggml_tensor * glu = g->nodes[i + 2];
+    if (a->op != GGML_OP_MUL_MAT_ID || b->op != GGML_OP_MUL_MAT_ID || glu->op != GGML_OP_GLU || !glu->src[1]) return false;
+    if (mx_op_param<int32_t>(glu, 0) != GGML_GLU_OP_SWIGLU || mx_op_param<int32_t>(glu, 1) != 0) return false;
+    const ggml_tensor * gate = glu->src[0] == a && glu->src[1] == b ? a : (glu->src[0] == b && glu->src[1] == a ? b : nullptr);
+    if (!gate) return false;
+    const ggml_tensor * up = gate == a ? b : a;
+    if (gate->src[1] != up->src[1] || gate->src[2] != up->src[2] || up->src[2]->ne[1] > 8) return false;
+    if (uses[a] != 1 || uses[b] != 1 || ((a->flags | b->flags) & GGML_TENSOR_FLAG_OUTPUT)) return false;
+    if (!mx_are_same_shape(glu, gate) || glu->type != GGML_TYPE_F32 || !mx_is_contiguous(glu)) return false;
+    for (const ggml_tensor * t : {gate->src[1], gate->src[2], gate->src[0], up->src[0]})
+        if (t_overlaps(t, glu)) return false;
+    deferred_guard_read(c, gate->src[1]);
+    deferred_guard_write(c, glu);
+    act_cache_invalidate(c.s, glu);
+    ActQ * q8 = glu->ne[0] % 32 == 0 ? act_cache_alloc(c.s, glu) : nullptr;
+    if (!gemv2_moe(c, gate, up->src[0], glu, q8)) {
+        if (q8) act_cache_invalidate(c.s, glu);
+        return false;
+    }
+    return true;
+}
+
 static void run_node(OpCtx & c, ggml_tensor * n) {
     switch (n->op) {
         case GGML_OP_GET_ROWS:   op_get_rows(c, n); break;
@@ -356,6 +385,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
                 const int k = fuse_qkv_rope_store(c, g, i, uses);
                 if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; deferred_retire(s, g, i0, i); continue; }
             }
+            if (n->op == GGML_OP_MUL_MAT_ID && try_fuse_moe_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
             if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             if (n->op == GGML_OP_MUL_MAT && try_group_mm(c, g, i, done)) continue;
             if (n->op == GGML_OP_MUL_MAT && try_fuse_mm_add(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; deferred_retire(s, g, i0, i); continue; }

@@ -33,6 +33,9 @@ bool gemv2_type_ok(int t);
 bool gemv2_ok(const ggml_tensor * w, const ggml_tensor * x, const ggml_tensor * dst);
 // dst[r] = epi(W[r]·x): w2 != null → silu(W·x)*(W2·x); res != null → + res[r].
 // q8out (SwiGLU only, rows % 32 == 0): also write the q8 form of dst there.
+// MUL_MAT_ID `mm` of a decode step (<= 8 tokens) into dst; w2 = the up experts of a fused
+// gate/up SwiGLU (dst = the GLU output), q8out its q8 copy. false: not eligible, nothing run
+bool gemv2_moe(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * w2, ggml_tensor * dst, ActQ * q8out = nullptr);
 void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, const XStage & xs, float * dst,
                   const float * res, ActQ * q8out = nullptr);
 

@@ -19,7 +19,30 @@ struct G2Args {
     int8_t * q8o; float * q8od; float * q8os;   // EPI 1 with 8 waves: q8 form of the output
     unsigned long long * trace;                 // debug (MX_TRACE), workgroup 0
     unsigned long long * trace_blk;             // debug (MX_TRACE_BLK), every workgroup
+    // MUL_MAT_ID (MoE decode): grid.y = item = (slot sl, token t) = (item % n_used,
+    // item / n_used); the expert id is read on the device (graph-replay safe)
+    const char * ids; size_t id0, id1;           // ids [n_used, n_tok] i32, byte strides
+    int n_used, n_expert, ne11, n_items;
+    size_t w_exp;                                // weight expert stride (bytes)
+    int64_t x_col;                               // f32 source: floats per activation column
+    size_t d_slot, d_tok;                        // dst strides (floats)
 };
+
+// per-item bases of a MUL_MAT_ID GEMV workgroup; false: no valid expert (block-uniform)
+__device__ __forceinline__ bool g2_item(const G2Args & p, const char *& w, const char *& w2, XStage & xs,
+                                        float *& dst, int8_t *& q8o, float *& q8od, float *& q8os) {
+    const int item = blockIdx.y, sl = item % p.n_used, t = item / p.n_used;
+    const int ex = *(const int32_t *) (p.ids + (size_t) sl * p.id0 + (size_t) t * p.id1);
+    if (ex < 0 || ex >= p.n_expert) return false;
+    w += (size_t) ex * p.w_exp;
+    if (w2) w2 += (size_t) ex * p.w_exp;
+    const int64_t col = (int64_t) t * p.ne11 + sl % p.ne11;
+    if (xs.q8) { xs.q8 += col * p.K; xs.q8d += col * (p.K / 32); xs.q8s += col * (p.K / 32); }
+    else xs.x += col * p.x_col;
+    dst += sl * p.d_slot + t * p.d_tok;
+    if (q8o) { q8o += (int64_t) item * p.nrows; q8od += (int64_t) item * (p.nrows / 32); q8os += (int64_t) item * (p.nrows / 32); }
+    return true;
+}
 
 // EPI 0 store, 1 SwiGLU(w, w2), 2 + residual. W waves per block; with W = 8 and
 // LPR = 16 a block owns 32 consecutive rows and (q8o != null) also emits the q8
@@ -35,9 +58,14 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     const int row = (blk * W + wave) * RPW + lane / LPR;
     const bool valid = row < p.nrows;
     const int64_t rr = valid ? row : p.nrows - 1;
+    const char * wb = p.w, * wb2 = p.w2;
+    XStage xs = p.xs;
+    float * dst = p.dst;
+    int8_t * q8o = p.q8o; float * q8od = p.q8od, * q8os = p.q8os;
+    if (p.ids && !g2_item(p, wb, wb2, xs, dst, q8o, q8od, q8os)) return;
     const char * rows[NM];
-    rows[0] = p.w + rr * p.w_row;
-    if constexpr (NM == 2) rows[1] = p.w2 + rr * p.w_row;
+    rows[0] = wb + rr * p.w_row;
+    if constexpr (NM == 2) rows[1] = wb2 + rr * p.w_row;
     const LdsAct a = lds_act(smem, p.K);
     float * red = gemv_lds_red(smem, p.K);
     float acc[NM];
@@ -48,7 +76,7 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     // would add a memory round trip to every workgroup's tail
     float res = 0.f;
     if constexpr (EPI == 2) res = p.res[rr];
-    gemv_rows<QT, LPR, UPL, NM, 64 * W, MODE>(rows, p.units, sub, a, p.xs, p.K, red, acc,
+    gemv_rows<QT, LPR, UPL, NM, 64 * W, MODE>(rows, p.units, sub, a, xs, p.K, red, acc,
                                               [&] { if constexpr (EPI == 2) asm volatile("" : "+v"(res)); });
     MX_TRACE(tr, 3);
     float v = acc[0];
@@ -56,12 +84,12 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     // workgroup's tail
     if constexpr (EPI == 1) v = v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f)) * acc[1];
     if constexpr (EPI == 2) v += res;
-    if (sub == LPR - 1 && valid) p.dst[row] = v;
+    if (sub == LPR - 1 && valid) dst[row] = v;
     MX_TRACE(tr, 4);
     MX_TRACE_BLK(p.trace_blk, 1);
     constexpr int RPB = W * RPW;
     if constexpr (RPB % 32 == 0 && RPB / 32 <= W) {
-        if (p.q8o) {     // block-uniform: the q8 form of this block's RPB outputs, one wave per 32
+        if (q8o) {       // block-uniform: the q8 form of this block's RPB outputs, one wave per 32
             __shared__ float orow[RPB];
             if (sub == LPR - 1) orow[row - blk * RPB] = v;
             __syncthreads();
@@ -73,8 +101,8 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
                 const int qi = q8_round(x, qs.id);
                 const int sum = __builtin_amdgcn_readlane(dpp_sum_group_i<32>(qi), 31);
                 const int qb = blk * (RPB / 32) + wave;
-                p.q8o[qb * 32 + lane] = (int8_t) qi;
-                if (lane == 0) { p.q8od[qb] = dd; p.q8os[qb] = dd * (float) sum; }
+                q8o[qb * 32 + lane] = (int8_t) qi;
+                if (lane == 0) { q8od[qb] = dd; q8os[qb] = dd * (float) sum; }
             }
         }
     }
@@ -83,9 +111,9 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
 template <int QT, int LPR, int UPL, int EPI, int W = 4>
 static void launch_cfg(hipStream_t st, const G2Args & p, bool regs = false) {
     constexpr int RPB = W * (64 / LPR);
-    const unsigned grid = (unsigned) ((p.nrows + RPB - 1) / RPB);
+    const dim3 grid((unsigned) ((p.nrows + RPB - 1) / RPB), p.ids ? (unsigned) p.n_items : 1u);
     // regs: register staging of x even on a large grid (the q8-emitting SwiGLU)
-    const int mode = gemv_mode(p.xs, p.K, regs && g_tune[9] == 0 ? 0 : (int64_t) grid * W, 64 * W);
+    const int mode = gemv_mode(p.xs, p.K, regs && g_tune[9] == 0 ? 0 : (int64_t) grid.x * grid.y * W, 64 * W);
     const size_t lds = gemv_lds_bytes(p.K, mode);
     MX_KLOG("gemv2 qt=%d lpr=%d upl=%d epi=%d w=%d mode=%d K=%d M=%d q8o=%d", QT, LPR, UPL, EPI, W, mode, p.K, p.nrows, p.q8o != nullptr);
     switch (mode) {
@@ -165,6 +193,8 @@ bool gemv2_ok(const ggml_tensor * w, const ggml_tensor * x, const ggml_tensor * 
     return true;
 }
 
+static void gemv2_launch_p(OpCtx & c, G2Args & p, int type, bool glu, bool res);
+
 void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, const XStage & xs, float * dst,
                   const float * res, ActQ * q8out) {
     G2Args p{};
@@ -184,20 +214,68 @@ void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, cons
         MX_ASSERT(glu && p.nrows % 32 == 0);
         p.q8o = (int8_t *) q8out->q; p.q8od = (float *) q8out->d; p.q8os = (float *) q8out->s;
     }
-    int lpr, upl;
-    pick_cfg(w->type, p.units, p.nrows, glu, lpr, upl);
     MX_ASSERT(!(glu && res));
+    gemv2_launch_p(c, p, w->type, glu, res != nullptr);
+}
+
+static void gemv2_launch_p(OpCtx & c, G2Args & p, int type, bool glu, bool res) {
+    int lpr, upl;
+    pick_cfg(type, p.units, p.nrows, glu, lpr, upl);
     const int epi = glu ? 1 : (res ? 2 : 0);
 #define TY(T) case T: \
         if (epi == 0) launch_type<T, 0>(c.st, p, lpr, upl); \
         else if (epi == 1) launch_type<T, 1>(c.st, p, lpr, upl); \
         else launch_type<T, 2>(c.st, p, lpr, upl); \
         break;
-    switch (w->type) {
+    switch (type) {
         TY(GGML_TYPE_Q4_K) TY(GGML_TYPE_Q5_K) TY(GGML_TYPE_Q6_K) TY(GGML_TYPE_Q4_0) TY(GGML_TYPE_Q8_0)
-        default: MX_ABORT("gemv2 type %d", w->type);
+        default: MX_ABORT("gemv2 type %d", type);
     }
 #undef TY
+}
+
+// MUL_MAT_ID of a decode step (n_tok <= 8): one v2 GEMV launch, grid.y = (slot, token)
+// items, the expert of each read on the device. gate/up (w2 != null): silu(Wg x) * (Wu x)
+// of the two MUL_MAT_IDs in one pass (and the q8 of the result for the down projection's
+// prologue when q8out is given: [item][M] int8 + per-32 d, d*sum).
+bool gemv2_moe(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * w2, ggml_tensor * dst, ActQ * q8out) {
+    const ggml_tensor * as = mm->src[0], * b = mm->src[1], * ids = mm->src[2];
+    if (!g_gemv2 || !gemv2_type_ok(as->type) || b->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
+    const int64_t K = as->ne[0];
+    const int64_t qk = (as->type == GGML_TYPE_Q4_0 || as->type == GGML_TYPE_Q8_0) ? 32 : 256;
+    if (K % qk || K > GEMV2_MAX_K || b->ne[0] != K || b->nb[0] != 4 || b->ne[3] != 1 || as->ne[3] != 1) return false;
+    if (as->nb[0] != (size_t) mx_type(as->type).size || as->ne[1] > INT32_MAX) return false;
+    if (ids->type != GGML_TYPE_I32 || ids->ne[1] > 8 || ids->ne[0] * ids->ne[1] > 65535 || ids->ne[1] != b->ne[2]) return false;
+    if (dst->nb[0] != 4 || dst->ne[0] != as->ne[1] || dst->ne[1] != ids->ne[0]) return false;
+    if (b->nb[2] != b->nb[1] * b->ne[1] || b->nb[1] != (size_t) K * 4 || ((uintptr_t) b->data & 15)) return false;
+    if (w2 && (w2->type != as->type || w2->nb[1] != as->nb[1] || w2->nb[2] != as->nb[2] || w2->ne[1] != as->ne[1])) return false;
+    G2Args p{};
+    p.w = (const char *) as->data;
+    p.w2 = w2 ? (const char *) w2->data : nullptr;
+    p.w_row = as->nb[1];
+    p.dst = (float *) dst->data;
+    p.nrows = (int) as->ne[1];
+    p.K = (int) K;
+    p.units = units_of(as->type, K);
+    // a q8 copy of b in the act cache (the gate/up SwiGLU's emission) is staged as is
+    p.xs = XStage{(const float *) b->data, nullptr, 0.0f, 0};
+    p.xs.xcd = g_tune[15] != 1;
+    if (const ActQ * a = act_cache_find(c.s, b)) if (a->kp == K) { p.xs.q8 = a->q; p.xs.q8d = a->d; p.xs.q8s = a->s; }
+    p.trace = mx_trace_slot(1);
+    p.ids = (const char *) ids->data; p.id0 = ids->nb[0]; p.id1 = ids->nb[1];
+    p.n_used = (int) ids->ne[0]; p.n_expert = (int) as->ne[2]; p.ne11 = (int) b->ne[1];
+    p.n_items = (int) (ids->ne[0] * ids->ne[1]);
+    p.w_exp = as->nb[2];
+    p.x_col = K;
+    p.d_slot = dst->nb[1] / 4; p.d_tok = dst->nb[2] / 4;
+    if (q8out) {
+        MX_ASSERT(w2 && p.nrows % 32 == 0);
+        p.q8o = (int8_t *) q8out->q; p.q8od = (float *) q8out->d; p.q8os = (float *) q8out->s;
+    }
+    MX_KLOG("gemv2 moe qt=%d K=%d M=%d items=%d glu=%d q8in=%d", (int) as->type, p.K, p.nrows, p.n_items, w2 != nullptr,
+            p.xs.q8 != nullptr);
+    gemv2_launch_p(c, p, as->type, w2 != nullptr, false);
+    return true;
 }
 
 }  // namespace mx

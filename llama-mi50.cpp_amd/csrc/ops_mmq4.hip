@@ -61,6 +61,7 @@ struct M4Args {
     int ksplit;                      // EPI 0: K shares over grid.z (1: no split)
     float * part; int part_ld;       // split-K partial sums [ksplit][N][part_ld] (part_ld = padded rows)
     unsigned long long * trace;      // debug (opbench --trace, slot 3): phase stamps of workgroup 0
+    unsigned long long * trace_blk;  // debug (opbench --trace-blocks): {start, end} of every workgroup
     int dbg;                         // timing experiments (g_tune[19]): 4 no activation DMA, 8 weights of
                                      // chunk 0 only
 };
@@ -326,20 +327,31 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
     extern __shared__ __align__(16) uint4 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     constexpr int BT = 32 * TT;
+    // MoE (EPI 2): grid.x = row tile, grid.y = token tile. Workgroups go to the XCDs
+    // round-robin by linear index, and most token tiles of an expert are empty: with the
+    // token tile fastest every busy workgroup (token tile 0) landed on XCD 0 (measured:
+    // 1.8 ms instead of ~0.3 for a Mixtral pp512 gate projection)
+    const int by = EPI == 2 ? (int) blockIdx.x : (int) blockIdx.y;
+    const int bx = EPI == 2 ? (int) blockIdx.y : (int) blockIdx.x;
     int si = 0;
 #pragma unroll
-    for (int i = 1; i < M4_MAXSEG; ++i) if (i < p.nseg && (int) blockIdx.y >= p.seg[i].tile0) si = i;
+    for (int i = 1; i < M4_MAXSEG; ++i) if (i < p.nseg && by >= p.seg[i].tile0) si = i;
     const M4Seg & sg = p.seg[si];
-    const int tile = (int) blockIdx.y - sg.tile0;
-    int tok0 = (int) blockIdx.x * BT, ntok = p.N, slot0 = 0;
+    const int tile = by - sg.tile0;
+    int tok0 = bx * BT, ntok = p.N, slot0 = 0;
     const char * wb = sg.w;
     const int nk = p.K / M4_KC;
     int c0 = 0, nc = nk;
+    const size_t bid = blockIdx.x + (size_t) gridDim.x * (blockIdx.y + (size_t) gridDim.y * blockIdx.z);
+    if (p.trace_blk && tid == 0 && bid < 65536) p.trace_blk[2 * bid] = __builtin_amdgcn_s_memrealtime();
     if constexpr (EPI == 2) {
         const int e = (int) blockIdx.z;
         slot0 = p.tile_tab[2 * e];
         ntok = p.tile_tab[2 * e + 1];
-        if (tok0 >= ntok) return;                     // block-uniform, before any barrier
+        if (tok0 >= ntok) {                           // block-uniform, before any barrier
+            if (p.trace_blk && tid == 0 && bid < 65536) p.trace_blk[2 * bid + 1] = __builtin_amdgcn_s_memrealtime();
+            return;
+        }
         wb += (size_t) e * p.w_exp;
     } else if (p.ksplit > 1) {
         c0 = (int) blockIdx.z * nk / p.ksplit;
@@ -365,6 +377,7 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
     if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT>(p, wrow, cols, lds, c0, nc, acc, tr);
     else m4_kloop<QTB, TT>(p, wrow, cols, lds, c0, nc, acc, tr);
 
+    if (p.trace_blk && tid == 0 && bid < 65536) p.trace_blk[2 * bid + 1] = __builtin_amdgcn_s_memrealtime();
     constexpr float inv = 1.0f / M4_WSCALE;
     if constexpr (EPI == 1) {
         float * red = (float *) lds;                  // 4 waves x TT x 16 x 64 floats (<= the ring)
@@ -496,6 +509,7 @@ template <int EPI>
 static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int nz, int tt) {
     a.dbg = g_tune[19];
     a.trace = mx_trace_slot(3);
+    a.trace_blk = mx_trace_blocks();
     const int nk = a.K / M4_KC;
     const int64_t gx = mx_ceil_div(a.N, 32 * tt);
     a.ksplit = 1;
@@ -509,7 +523,7 @@ static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int 
             nz = ks;
         }
     }
-    const dim3 g((unsigned) gx, (unsigned) tiles_y, (unsigned) nz);
+    const dim3 g = EPI == 2 ? dim3((unsigned) tiles_y, (unsigned) gx, (unsigned) nz) : dim3((unsigned) gx, (unsigned) tiles_y, (unsigned) nz);
     const bool ok = tt == 4 ? m4_go<EPI, 4>(c.st, a, ta, tb, g) : m4_go<EPI, 2>(c.st, a, ta, tb, g);
     if (ok && a.ksplit > 1) {
         const dim3 gr((unsigned) mx_ceil_div(a.part_ld, 256), (unsigned) a.N);

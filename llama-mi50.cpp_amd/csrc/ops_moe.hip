@@ -9,6 +9,7 @@
 // whole MoE layer stays capturable in a HIP graph.
 #include "backend.h"
 #include "mm.h"
+#include "gemv.h"
 
 namespace mx {
 
@@ -110,6 +111,7 @@ void op_mul_mat_id(OpCtx & c, ggml_tensor * dst) {
     const int64_t items = ids->ne[0] * ids->ne[1];
     if (items == 0) return;
     if (mmq4_moe(c, dst)) return;     // prefill: expert-grouped MFMA GEMM (ops_mmq4.hip)
+    if (gemv2_moe(c, dst, nullptr, dst)) return;   // decode: v2 GEMV per (slot, token) item
     if (mmvq_type_ok(as->type) && as->ne[0] % qk_of_type(as->type) == 0) {
         ActQ a = quantize_activations(c, b);
         switch (as->type) {

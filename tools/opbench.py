@@ -97,6 +97,26 @@ def case_gemm_glu(pkg, be, rng, tname, K, M, N=512):
     return ctx, [g]
 
 
+def case_moe(pkg, be, rng, tname="q5_K", K=4096, M=14336, n_exp=8, used=2, T=512, skew=0.0):
+    """MUL_MAT_ID at Mixtral shapes: T tokens x top-`used` of `n_exp` experts (uniform random
+    routing; skew > 0 sends that fraction of the tokens to experts 0 and 1)"""
+    tid = NAMES[tname]
+    w1, _ = rand_quant(tid, M, K, rng)
+    ctx = pkg.Context()
+    tw = ctx.new_tensor(tid, K, M, n_exp)
+    tx = ctx.new_tensor("f32", K, 1, T)
+    ti = ctx.new_tensor("i32", used, T)
+    g = ctx.build(ctx.mul_mat_id(tw, tx, ti))
+    ctx.alloc(be)
+    tw.set(np.tile(w1, n_exp))
+    tx.set(rng.standard_normal((T, 1, K)).astype(np.float32))
+    ids = np.stack([rng.permutation(n_exp)[:used] for _ in range(T)]).astype(np.int32)
+    ns = int(skew * T)
+    ids[:ns] = np.array([0, 1][:used], np.int32)
+    ti.set(ids)
+    return ctx, [g]
+
+
 def case_ffn(pkg, be, rng, tname="q4_K", tdown="q4_K", K=4096, F=14336):
     """ffn_norm-less FFN block: gate/up SwiGLU GEMV (+q8 of its output) -> down + residual."""
     tid, tdn = NAMES[tname], NAMES[tdown]
@@ -226,6 +246,10 @@ CASES = {
     "pp_down_q6k": lambda p, b, r: case_gemm(p, b, r, "q6_K", 14336, 4096),
     "pp_k_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 1024),
     "pp_glu_q4k": lambda p, b, r: case_gemm_glu(p, b, r, "q4_K", 4096, 14336),
+    "pp_glu_q5k": lambda p, b, r: case_gemm_glu(p, b, r, "q5_K", 4096, 14336),
+    "pp_moe_q5k": lambda p, b, r: case_moe(p, b, r),
+    "pp_moe_q5k_skew": lambda p, b, r: case_moe(p, b, r, skew=0.9),
+    "tg_moe_q5k": lambda p, b, r: case_moe(p, b, r, T=1),
     "pp_down_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 14336, 4096),
     "ffn_q4k": lambda p, b, r: case_ffn(p, b, r),
     "ffn_block": lambda p, b, r: case_ffn_block(p, b, r),
