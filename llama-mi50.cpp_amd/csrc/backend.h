@@ -189,6 +189,11 @@ size_t mmq_act_bytes(const ggml_tensor * mm);                 // f16 activation 
 using UseCount = std::unordered_map<const ggml_tensor *, int>;
 // decode Q/K/V projections + RoPE + KV-cache stores in one launch; returns nodes consumed
 int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
+// MoE router chain / expert combine in one launch each (ops_moe.hip); nodes consumed
+int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i);
+int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
+// the executor's guard for a node about to run (deferred norms it reads or overwrites)
+void deferred_guard_node_ext(OpCtx & c, const ggml_tensor * n);
 
 Stream * stream_of(ggml_backend_t b);
 

@@ -81,6 +81,7 @@ static bool graph_signature_same(const ggml_cgraph * g, std::vector<uint64_t> & 
 // reference fusion gate ggml-cuda.cu:3844-3854).
 using UseMap = UseCount;
 static bool g_no_qkv = getenv("GGML_MI355X_NO_QKV_FUSION") != nullptr;
+static bool g_no_moe_fusion = getenv("GGML_MI355X_NO_MOE_FUSION") != nullptr;   // A/B
 
 // ---- deferred RMS norm --------------------------------------------------------
 // An attn_norm / ffn_norm pair whose every consumer is a single-token GEMV is not
@@ -165,6 +166,8 @@ static void deferred_guard_node(OpCtx & c, const ggml_tensor * n) {
     }
     deferred_guard_write(c, n);
 }
+
+void deferred_guard_node_ext(OpCtx & c, const ggml_tensor * n) { deferred_guard_node(c, n); }
 
 static bool try_defer_norm(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     if (!g_gemv2 || i + 1 >= g->n_nodes) return false;
@@ -386,6 +389,14 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
                 if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; deferred_retire(s, g, i0, i); continue; }
             }
             if (n->op == GGML_OP_MUL_MAT_ID && try_fuse_moe_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
+            if (n->op == GGML_OP_SOFT_MAX && !g_no_moe_fusion) {
+                const int k = fuse_topk_moe(c, g, i);
+                if (k > 0) { i += k - 1; s->n_fused += 3; s->n_nodes_run += 4; deferred_retire(s, g, i0, i); continue; }
+            }
+            if (n->op == GGML_OP_MUL && !g_no_moe_fusion) {
+                const int k = fuse_moe_combine(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
+            }
             if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             if (n->op == GGML_OP_MUL_MAT && try_group_mm(c, g, i, done)) continue;
             if (n->op == GGML_OP_MUL_MAT && try_fuse_mm_add(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; deferred_retire(s, g, i0, i); continue; }
@@ -416,6 +427,9 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         if (g->nodes[i]->op == GGML_OP_MUL_MAT) f16need = std::max(f16need, mmq_act_bytes(g->nodes[i]));
         if (g->nodes[i]->op == GGML_OP_MUL_MAT && mmvq_small_batch_ok(g->nodes[i])) slot = std::max(slot, act_slot_bytes(g->nodes[i]->src[1]));
         if (g->nodes[i]->op == GGML_OP_MUL && mx_nrows(g->nodes[i]) <= 8) slot = std::max(slot, act_slot_bytes(g->nodes[i]));
+        // MoE decode: the q8 copy of the gate/up SwiGLU output (= this node's shape) and of src1
+        if (g->nodes[i]->op == GGML_OP_MUL_MAT_ID && g->nodes[i]->src[2]->ne[1] <= 8)
+            slot = std::max({slot, act_slot_bytes(g->nodes[i]), act_slot_bytes(g->nodes[i]->src[1])});
     }
     if (slot > s->act_slot) {
         HIP_CHECK(hipStreamSynchronize(s->stream));

@@ -471,6 +471,35 @@ __global__ __launch_bounds__(256) void k_mmv_generic(MmvGen p) {
     if (lane == 0) *(float *) (p.dst + row * p.d_row + col * p.d_col + i12 * p.d_c2 + i13 * p.d_c3) = acc;
 }
 
+// f32 / f16 weight rows (the MoE router ffn_gate_inp [n_embd, n_expert] f32, small
+// unquantised projections) against f32 columns: one workgroup per (row, column), every
+// thread's 16-byte loads issued at once, block reduction. The per-wave strided loop above
+// took 28.5 us for Mixtral's 8-row router (profiles/r02/prof_mixtral_decode*).
+template <typename TW>
+__global__ __launch_bounds__(256) void k_mmv_dense(MmvGen p) {
+    __shared__ float red[16];
+    const int64_t row = blockIdx.x, col = blockIdx.y % p.N, ch = blockIdx.y / p.N;
+    const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
+    const char * wr = p.w + row * p.w_row + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
+    const float * xr = (const float *) (p.x + col * p.x_col + i12 * p.x_c2 + i13 * p.x_c3);
+    float acc = 0.f;
+    constexpr int V = 16 / sizeof(TW);      // weights per 16-byte load
+    for (int64_t k = (int64_t) threadIdx.x * V; k < p.K; k += 256 * V) {
+        TW wv[V];
+        __builtin_memcpy(wv, wr + k * sizeof(TW), 16);
+#pragma unroll
+        for (int j = 0; j < V; j += 4) {
+            const float4 xv = *(const float4 *) (xr + k + j);
+            float w0, w1, w2, w3;
+            if constexpr (sizeof(TW) == 4) { w0 = wv[j]; w1 = wv[j + 1]; w2 = wv[j + 2]; w3 = wv[j + 3]; }
+            else { w0 = h2f(wv[j]); w1 = h2f(wv[j + 1]); w2 = h2f(wv[j + 2]); w3 = h2f(wv[j + 3]); }
+            acc += w0 * xv.x + w1 * xv.y + w2 * xv.z + w3 * xv.w;
+        }
+    }
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) *(float *) (p.dst + row * p.d_row + col * p.d_col + i12 * p.d_c2 + i13 * p.d_c3) = acc;
+}
+
 void mmv_generic_run(OpCtx & c, ggml_tensor * dst) {
     const ggml_tensor * w = dst->src[0];
     const ggml_tensor * x = dst->src[1];
@@ -480,6 +509,16 @@ void mmv_generic_run(OpCtx & c, ggml_tensor * dst) {
     p.dst = (char *) dst->data; p.d_row = dst->nb[0]; p.d_col = dst->nb[1]; p.d_c2 = dst->nb[2]; p.d_c3 = dst->nb[3];
     p.K = w->ne[0]; p.M = w->ne[1]; p.N = x->ne[1]; p.ne12 = x->ne[2];
     p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
+    const size_t ws = w->type == GGML_TYPE_F32 ? 4 : 2;
+    if ((w->type == GGML_TYPE_F32 || w->type == GGML_TYPE_F16) && p.w_nb0 == ws && p.x_nb0 == 4 && p.K % (16 / ws) == 0 &&
+        p.M * p.N <= 65536 && (((uintptr_t) p.w | p.w_row | p.w_c2 | p.w_c3) % 16) == 0 &&
+        (((uintptr_t) p.x | p.x_col | p.x_c2 | p.x_c3) % 16) == 0) {
+        const dim3 gd((unsigned) p.M, (unsigned) (p.N * x->ne[2] * x->ne[3]));
+        MX_KLOG("mmv_dense type=%d K=%lld M=%lld N=%lld", (int) w->type, (long long) p.K, (long long) p.M, (long long) p.N);
+        if (w->type == GGML_TYPE_F32) k_mmv_dense<float><<<gd, 256, 0, c.st>>>(p);
+        else k_mmv_dense<uint16_t><<<gd, 256, 0, c.st>>>(p);
+        return;
+    }
     dim3 grid((unsigned) mx_ceil_div(p.M * p.N, 4), (unsigned) (x->ne[2] * x->ne[3]));
     switch (w->type) {
 #define GEN(T) case T: k_mmv_generic<T><<<grid, 256, 0, c.st>>>(p); break;

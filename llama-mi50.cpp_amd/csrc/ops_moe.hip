@@ -137,3 +137,207 @@ void op_mul_mat_id(OpCtx & c, ggml_tensor * dst) {
 }
 
 }  // namespace mx
+
+namespace mx {
+
+// ---------------------------------------------------------------------------
+// MoE router in one launch (reference fusion: ggml-cuda/topk-moe.cu): the node chain
+// SOFT_MAX(logits) -> ARGSORT(desc) [-> top-k view] -> GET_ROWS(probs, top-k)
+// [-> SUM_ROWS -> CLAMP -> DIV] of llama's build_moe_ffn (src/llama-graph.cpp:1201-1296).
+// One wave per token, one lane per expert (n_expert <= 64); every node of the chain still
+// gets its output written (they are tiny), so any other reader stays correct.
+// ---------------------------------------------------------------------------
+struct TopkArgs {
+    const float * logits; size_t l1;        // [n_exp, n_tok], row stride in floats
+    float * probs; size_t p1;
+    int32_t * order; size_t o1;              // argsort output [n_exp, n_tok]
+    float * w; size_t w1;                    // get_rows output [1, k, n_tok]: stride per token (floats)
+    float * sum; float * clamped;            // [1, n_tok] (nullable)
+    float * wn; size_t wn1;                  // div output [k, n_tok] (nullable)
+    float cmin, cmax, scale;
+    int n_exp, k;
+};
+
+__global__ __launch_bounds__(64) void k_topk_moe(TopkArgs a) {
+    const int lane = threadIdx.x, t = blockIdx.x;
+    const bool on = lane < a.n_exp;
+    const float x = on ? a.logits[(size_t) t * a.l1 + lane] * a.scale : -INFINITY;
+    const float m = wave_max(x);
+    const float e = on ? expf(x - m) : 0.0f;
+    const float s = wave_sum(e);
+    const float p = on ? e / s : -INFINITY;
+    if (on) a.probs[(size_t) t * a.p1 + lane] = p;
+    // descending rank, ties to the lower index
+    int rank = 0;
+    for (int j = 0; j < a.n_exp; ++j) {
+        const float pj = __shfl(p, j, 64);
+        rank += (pj > p) || (pj == p && j < lane);
+    }
+    if (on) a.order[(size_t) t * a.o1 + rank] = lane;
+    const bool top = on && rank < a.k;
+    if (top) a.w[(size_t) t * a.w1 + rank] = p;
+    if (a.sum) {
+        // sum in rank order (the CPU's SUM_ROWS adds the selected weights in that order)
+        float ws = 0.f;
+        for (int r = 0; r < a.k; ++r) {
+            float v = 0.f;
+            for (int j = 0; j < a.n_exp; ++j) {
+                const int rj = __shfl(rank, j, 64);
+                const float pj = __shfl(p, j, 64);
+                if (rj == r) v = pj;
+            }
+            ws += v;
+        }
+        const float cl = fminf(fmaxf(ws, a.cmin), a.cmax);
+        if (lane == 0) { a.sum[t] = ws; a.clamped[t] = cl; }
+        if (top) a.wn[(size_t) t * a.wn1 + rank] = p / cl;
+    }
+}
+
+static const ggml_tensor * view_base(const ggml_tensor * t) {
+    while (t && (t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW || t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE))
+        t = t->src[0];
+    return t;
+}
+
+// returns the number of graph nodes consumed from i (0: no match)
+int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i) {
+    ggml_tensor * sm = g->nodes[i];
+    if (sm->op != GGML_OP_SOFT_MAX || sm->src[1] || sm->type != GGML_TYPE_F32 || sm->src[0]->type != GGML_TYPE_F32) return 0;
+    if (mx_op_param<float>(sm, 1) != 0.0f || sm->ne[0] > 64 || sm->ne[2] != 1 || sm->ne[3] != 1) return 0;
+    if (!mx_is_contiguous(sm) || sm->src[0]->nb[0] != 4) return 0;
+    ggml_tensor * as = nullptr, * gr = nullptr, * sr = nullptr, * cl = nullptr, * dv = nullptr;
+    int last = i;
+    for (int j = i + 1; j < g->n_nodes && j < i + 16; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (n->op == GGML_OP_RESHAPE || n->op == GGML_OP_VIEW || n->op == GGML_OP_PERMUTE || n->op == GGML_OP_TRANSPOSE) continue;
+        if (!as && n->op == GGML_OP_ARGSORT && view_base(n->src[0]) == sm) { as = n; last = j; continue; }
+        if (as && !gr && n->op == GGML_OP_GET_ROWS && view_base(n->src[0]) == sm && view_base(n->src[1]) == as) { gr = n; last = j; continue; }
+        if (gr && !sr && n->op == GGML_OP_SUM_ROWS && view_base(n->src[0]) == gr) { sr = n; last = j; continue; }
+        if (sr && !cl && n->op == GGML_OP_CLAMP && n->src[0] == sr) { cl = n; last = j; continue; }
+        if (cl && !dv && n->op == GGML_OP_DIV && view_base(n->src[0]) == gr && n->src[1] == cl) { dv = n; last = j; continue; }
+        break;
+    }
+    if (!as || !gr) return 0;
+    if (sr && (!cl || !dv)) { sr = cl = dv = nullptr; }
+    // shapes: argsort [n_exp, n_tok] desc; get_rows [1, k, n_tok] of probs [1, n_exp, n_tok]
+    const int n_exp = (int) sm->ne[0], n_tok = (int) sm->ne[1];
+    if (mx_op_param<int32_t>(as, 0) != GGML_SORT_ORDER_DESC || as->type != GGML_TYPE_I32 || !mx_is_contiguous(as)) return 0;
+    if (as->ne[0] != n_exp || as->ne[1] != n_tok) return 0;
+    const ggml_tensor * idx = gr->src[1];
+    const int k = (int) idx->ne[0];
+    if (gr->type != GGML_TYPE_F32 || gr->ne[0] != 1 || gr->ne[1] != k || gr->ne[2] != n_tok || !mx_is_contiguous(gr)) return 0;
+    if (idx->ne[1] != n_tok || idx->nb[0] != 4 || idx->nb[1] != as->nb[1] || idx->data != as->data) return 0;
+    if (dv && (dv->type != GGML_TYPE_F32 || mx_nelements(dv) != (int64_t) k * n_tok || !mx_is_contiguous(dv) ||
+               sr->type != GGML_TYPE_F32 || cl->type != GGML_TYPE_F32 || mx_nelements(sr) != n_tok || mx_nelements(cl) != n_tok))
+        return 0;
+    // nothing between i and last may be a different node (the fused launch runs them at i)
+    for (int j = i + 1; j <= last; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (n == as || n == gr || n == sr || n == cl || n == dv) continue;
+        if (n->op != GGML_OP_RESHAPE && n->op != GGML_OP_VIEW && n->op != GGML_OP_PERMUTE && n->op != GGML_OP_TRANSPOSE) return 0;
+    }
+    TopkArgs a{};
+    a.logits = (const float *) sm->src[0]->data; a.l1 = sm->src[0]->nb[1] / 4;
+    a.probs = (float *) sm->data; a.p1 = sm->nb[1] / 4;
+    a.order = (int32_t *) as->data; a.o1 = as->nb[1] / 4;
+    a.w = (float *) gr->data; a.w1 = gr->nb[2] / 4;
+    a.scale = mx_op_param<float>(sm, 0);
+    a.n_exp = n_exp; a.k = k;
+    if (dv) {
+        a.sum = (float *) sr->data; a.clamped = (float *) cl->data;
+        a.cmin = mx_op_param<float>(cl, 0); a.cmax = mx_op_param<float>(cl, 1);
+        a.wn = (float *) dv->data; a.wn1 = (size_t) k;
+    }
+    for (int j = i; j <= last; ++j) {
+        deferred_guard_node_ext(c, g->nodes[j]);
+        act_cache_invalidate(c.s, g->nodes[j]);
+    }
+    MX_KLOG("topk_moe n_exp=%d k=%d n_tok=%d norm=%d", n_exp, k, n_tok, dv != nullptr);
+    k_topk_moe<<<(unsigned) n_tok, 64, 0, c.st>>>(a);
+    return last - i + 1;
+}
+
+// ---------------------------------------------------------------------------
+// expert combine: MUL(experts [M, n_used, n_tok], weights [1, n_used, n_tok]), the ADDs of
+// its per-slot views (llama's "aggregate experts" loop), optionally + the residual —
+// one elementwise launch instead of n_used + 1
+// ---------------------------------------------------------------------------
+__global__ void k_moe_combine(const float * ex, size_t e1, size_t e2, const float * w, size_t w1, size_t w2, int n_used,
+                              const float * res, size_t r1, float * mulout, float * out, size_t o1, int M) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x, t = blockIdx.y;
+    if (row >= M) return;
+    float acc = 0.f;
+    for (int e = 0; e < n_used; ++e) {
+        const float v = ex[(size_t) t * e2 + (size_t) e * e1 + row] * w[(size_t) t * w2 + (size_t) e * w1];
+        if (mulout) mulout[(size_t) t * e2 + (size_t) e * e1 + row] = v;
+        acc = e == 0 ? v : acc + v;
+    }
+    if (res) acc += res[(size_t) t * r1 + row];
+    out[(size_t) t * o1 + row] = acc;
+}
+
+int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map) {
+    auto uses = [&](const ggml_tensor * t) { auto it = use_map.find(t); return it == use_map.end() ? 0 : it->second; };
+    ggml_tensor * mul = g->nodes[i];
+    if (mul->op != GGML_OP_MUL || mul->type != GGML_TYPE_F32) return 0;
+    const ggml_tensor * ex = mul->src[0], * w = mul->src[1];
+    if (!ex || !w || ex->op != GGML_OP_MUL_MAT_ID || ex->type != GGML_TYPE_F32 || w->type != GGML_TYPE_F32) return 0;
+    const int M = (int) ex->ne[0], n_used = (int) ex->ne[1], n_tok = (int) ex->ne[2];
+    if (n_used < 2 || n_used > 16 || w->ne[0] != 1 || w->ne[1] != n_used || w->ne[2] != n_tok || ex->nb[0] != 4) return 0;
+    if (!mx_are_same_shape(mul, ex) || !mx_is_contiguous(mul)) return 0;
+    // the chain: ADD(view(mul, 0), view(mul, 1)), ADD(prev, view(mul, 2)), ... [, ADD(prev, residual)]
+    ggml_tensor * prev = nullptr;
+    int last = i, found = 1;
+    std::vector<ggml_tensor *> chain;
+    for (int j = i + 1; j < g->n_nodes && j < i + 8 + 2 * n_used && found < n_used; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (n->op == GGML_OP_VIEW || n->op == GGML_OP_RESHAPE) continue;
+        if (n->op != GGML_OP_ADD || n->type != GGML_TYPE_F32) return 0;
+        const ggml_tensor * a0 = n->src[0], * a1 = n->src[1];
+        // slot views: [M, n_tok] at offset slot * nb1 with the token stride of mul
+        auto slot_view = [&](const ggml_tensor * v, int slot) {
+            return v->op == GGML_OP_VIEW && v->src[0] == mul && v->view_offs == (size_t) slot * mul->nb[1] && v->ne[0] == M &&
+                   v->ne[1] == n_tok && v->nb[1] == mul->nb[2] && v->nb[0] == 4;
+        };
+        if (!slot_view(a1, found) || !(prev ? a0 == prev : slot_view(a0, 0))) return 0;
+        prev = n; last = j; ++found; chain.push_back(n);
+    }
+    if (found != n_used || !prev || prev->ne[0] != M || prev->ne[1] != n_tok || prev->nb[0] != 4) return 0;
+    // every intermediate read only inside the chain
+    for (size_t k = 0; k + 1 < chain.size(); ++k) if (uses(chain[k]) != 1) return 0;
+    // optional residual add right after
+    ggml_tensor * out = prev;
+    const float * res = nullptr;
+    size_t r1 = 0;
+    for (int j = last + 1; j < g->n_nodes && j < last + 4; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (n->op == GGML_OP_VIEW || n->op == GGML_OP_RESHAPE) continue;
+        if (n->op == GGML_OP_ADD && n->type == GGML_TYPE_F32 && uses(prev) == 1 && !(prev->flags & GGML_TENSOR_FLAG_OUTPUT) &&
+            (n->src[0] == prev || n->src[1] == prev) && mx_are_same_shape(n, prev) && n->nb[0] == 4) {
+            const ggml_tensor * r = n->src[0] == prev ? n->src[1] : n->src[0];
+            if (r->type == GGML_TYPE_F32 && r->nb[0] == 4 && mx_are_same_shape(r, prev)) {
+                bool between_ok = true;
+                for (int q = last + 1; q < j; ++q) {
+                    const int op = g->nodes[q]->op;
+                    if (op != GGML_OP_VIEW && op != GGML_OP_RESHAPE) between_ok = false;
+                }
+                if (between_ok) { res = (const float *) r->data; r1 = r->nb[1] / 4; out = n; last = j; }
+            }
+        }
+        break;
+    }
+    const bool mul_needed = uses(mul) != n_used || (mul->flags & GGML_TENSOR_FLAG_OUTPUT);
+    for (int j = i; j <= last; ++j) {
+        deferred_guard_node_ext(c, g->nodes[j]);
+        act_cache_invalidate(c.s, g->nodes[j]);
+    }
+    MX_KLOG("moe_combine M=%d n_used=%d n_tok=%d res=%d", M, n_used, n_tok, res != nullptr);
+    const dim3 grid((unsigned) mx_ceil_div(M, 256), (unsigned) n_tok);
+    k_moe_combine<<<grid, 256, 0, c.st>>>((const float *) ex->data, ex->nb[1] / 4, ex->nb[2] / 4, (const float *) w->data,
+                                          w->nb[1] / 4, w->nb[2] / 4, n_used, res, r1, mul_needed ? (float *) mul->data : nullptr,
+                                          (float *) out->data, out->nb[1] / 4, M);
+    return last - i + 1;
+}
+
+}  // namespace mx
