@@ -194,6 +194,30 @@ __global__ __launch_bounds__(64) void k_topk_moe(TopkArgs a) {
     }
 }
 
+// A fused chain runs its nodes at once, one workgroup per token (per row tile): a thread's
+// outputs must not land on data another thread still reads or writes. ggml-alloc gives
+// dead tensors' memory to later nodes and runs SOFT_MAX / DIV / CLAMP / ADD / MUL in
+// place, so e.g. SUM_ROWS can sit inside the logits. Two regions may overlap only when
+// they start at the same address with the same per-token stride (an in-place op: the
+// thread that reads an element is the one that overwrites it); with one token the
+// stride does not matter.
+struct ChainReg { const void * p; size_t n, stride; };
+
+static bool chain_alias_ok(const ChainReg * r, int n, bool one_tok) {
+    for (int x = 0; x < n; ++x)
+        for (int y = x + 1; y < n; ++y) {
+            const char * up = (const char *) r[x].p, * vp = (const char *) r[y].p;
+            if (!up || !vp || !(up < vp + r[y].n && vp < up + r[x].n)) continue;
+            if (up == vp && (one_tok || r[x].stride == r[y].stride)) continue;
+            return false;
+        }
+    return true;
+}
+
+static ChainReg chain_reg(const ggml_tensor * t, int tok_dim) {
+    return t ? ChainReg{t->data, mx_nbytes(t), t->nb[tok_dim]} : ChainReg{nullptr, 0, 0};
+}
+
 static const ggml_tensor * view_base(const ggml_tensor * t) {
     while (t && (t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW || t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE))
         t = t->src[0];
@@ -237,6 +261,11 @@ int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i) {
         if (n == as || n == gr || n == sr || n == cl || n == dv) continue;
         if (n->op != GGML_OP_RESHAPE && n->op != GGML_OP_VIEW && n->op != GGML_OP_PERMUTE && n->op != GGML_OP_TRANSPOSE) return 0;
     }
+    // one token is one wave that reads its logits before any store, and stores in the
+    // chain's order: any aliasing is then harmless
+    const ChainReg regs[] = {chain_reg(sm->src[0], 1), chain_reg(sm, 1), chain_reg(as, 1), chain_reg(gr, 2),
+                             chain_reg(sr, 1), chain_reg(cl, 1), chain_reg(dv, 1)};
+    if (n_tok > 1 && !chain_alias_ok(regs, 7, false)) return 0;
     TopkArgs a{};
     a.logits = (const float *) sm->src[0]->data; a.l1 = sm->src[0]->nb[1] / 4;
     a.probs = (float *) sm->data; a.p1 = sm->nb[1] / 4;
@@ -328,6 +357,14 @@ int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map
         break;
     }
     const bool mul_needed = uses(mul) != n_used || (mul->flags & GGML_TENSOR_FLAG_OUTPUT);
+    {
+        // the weights are read by every thread of a token: nothing written may touch them
+        const ChainReg regs[] = {chain_reg(ex, 2), chain_reg(mul_needed ? mul : nullptr, 2), chain_reg(out, 1),
+                                 {res, res ? mx_nbytes(out) : 0, res ? r1 * 4 : 0}};
+        const ChainReg wr[] = {chain_reg(w, 2), regs[1], regs[2]};
+        if (!chain_alias_ok(regs, 4, n_tok == 1)) return 0;
+        if (!chain_alias_ok(wr, 3, false) || (wr[1].p && wr[1].p == wr[0].p) || wr[2].p == wr[0].p) return 0;
+    }
     for (int j = i; j <= last; ++j) {
         deferred_guard_node_ext(c, g->nodes[j]);
         act_cache_invalidate(c.s, g->nodes[j]);

@@ -184,6 +184,9 @@ class Context:
     def div(self, a, b):
         return self._t(self.lib.mxg_binary(self.ptr, 8, a.ptr, b.ptr))
 
+    def clamp(self, a, lo, hi):
+        return self._t(self.lib.mxg_clamp(self.ptr, a.ptr, lo, hi))
+
     def scale(self, a, s):
         return self._t(self.lib.mxg_scale(self.ptr, a.ptr, s))
 

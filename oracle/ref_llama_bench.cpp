@@ -30,11 +30,20 @@
 static FILE * g_dump = nullptr;
 static std::string g_dump_dir;   // --dump-dir: also the raw f32 values, one file per node
 static int g_dump_idx = 0;
+static std::string g_dump_filter;   // --dump-filter <substring>: observe only nodes whose name contains it
+                                    // (keeps the rest of the graph in one piece, so backend fusions still run)
 static bool dump_cb(ggml_tensor * t, bool ask, void *) {
-    if (ask) return t->type == GGML_TYPE_F32;
-    if (!g_dump || t->type != GGML_TYPE_F32 || !ggml_is_contiguous(t)) return true;
+    const bool want = (t->type == GGML_TYPE_F32 || t->type == GGML_TYPE_I32) &&
+                      (g_dump_filter.empty() || strstr(t->name, g_dump_filter.c_str()) != nullptr);
+    if (ask) return want;
+    if (!g_dump || !want || !ggml_is_contiguous(t)) return true;
     std::vector<float> v(ggml_nelements(t));
-    ggml_backend_tensor_get(t, v.data(), 0, ggml_nbytes(t));
+    if (t->type == GGML_TYPE_F32) ggml_backend_tensor_get(t, v.data(), 0, ggml_nbytes(t));
+    else {
+        std::vector<int32_t> iv(ggml_nelements(t));
+        ggml_backend_tensor_get(t, iv.data(), 0, ggml_nbytes(t));
+        for (size_t i = 0; i < iv.size(); ++i) v[i] = (float) iv[i];
+    }
     double s = 0, s2 = 0;
     for (float x : v) { s += x; s2 += (double) x * x; }
     fprintf(g_dump, "%s %s %lld %lld %lld %lld %.9g %.9g", t->name, ggml_op_desc(t), (long long) t->ne[0],
@@ -76,6 +85,7 @@ int main(int argc, char ** argv) {
         else if (a == "-ctk") ctk = std::stoi(next());
         else if (a == "--dump") g_dump = fopen(next().c_str(), "w");
         else if (a == "--dump-dir") g_dump_dir = next();
+        else if (a == "--dump-filter") g_dump_filter = next();
     }
     llama_log_set([](ggml_log_level, const char *, void *) {}, nullptr);
     llama_backend_init();

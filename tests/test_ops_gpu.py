@@ -389,3 +389,50 @@ def test_gemv_lds_dma_staging_forced(pkg, backend, orc, tname, norm):
     assert nmse(y, orc.mul_mat(tid, w, rb, xin, exact=True)) < 5e-4
     mode = 4 if norm else 3
     assert any(ln.startswith("gemv2 ") and f" mode={mode} " in ln for ln in log), log
+
+
+@pytest.mark.parametrize("n_tok,n_exp,producer", [(1, 8, False), (40, 8, False), (40, 4, True), (1, 4, True), (64, 8, True)])
+def test_moe_router_fusion(pkg, backend, n_tok, n_exp, producer):
+    """llama build_moe_ffn's router chain (SOFT_MAX -> ARGSORT -> top-k GET_ROWS -> SUM_ROWS
+    -> CLAMP -> DIV) runs as one k_topk_moe launch; every node's output is checked against
+    numpy (softmax 1e-6 like test-backend-ops, selection exact)"""
+    rng = np.random.default_rng(91 + n_tok)
+    k, E = 2, 256
+    wr = (rng.standard_normal((n_exp, E)) * 0.1).astype(np.float32)
+    xr = rng.standard_normal((n_tok, E)).astype(np.float32)
+    logits = rng.standard_normal((n_tok, n_exp)).astype(np.float32) * 2
+    if producer:   # the logits come from the router MUL_MAT in the same graph (f32 weights)
+        logits = (xr.astype(np.float64) @ wr.T.astype(np.float64)).astype(np.float32)
+
+    def build(ctx):
+        if producer:
+            tw = ctx.new_tensor("f32", E, n_exp)
+            tx = ctx.new_tensor("f32", E, n_tok)
+            tl = ctx.mul_mat(tw, tx)
+            feed = [(tw, wr), (tx, xr)]
+        else:
+            tl = ctx.new_tensor("f32", n_exp, n_tok)
+            feed = [(tl, logits)]
+        probs = ctx.soft_max_ext(tl, None, 1.0)
+        order = ctx.argsort(probs, desc=True)
+        nb1 = order.nb[1]
+        topk = ctx.view_4d(order, k, n_tok, 1, 1, nb1, nb1 * n_tok, nb1 * n_tok, 0)
+        w = ctx.get_rows(ctx.reshape(probs, 1, n_exp, n_tok), topk)
+        w2 = ctx.reshape(w, k, n_tok)
+        cl = ctx.clamp(ctx.sum_rows(w2), 6.103515625e-5, float("inf"))
+        wn = ctx.div(w2, cl)
+        return [probs, order, w, wn], feed
+
+    backend.klog(True)
+    probs, order, w, wn = run(pkg, backend, build)
+    log = backend.klog_read()
+    backend.klog(False)
+    e = np.exp(logits - logits.max(1, keepdims=True))
+    ref_p = e / e.sum(1, keepdims=True)
+    assert nmse(probs.reshape(n_tok, n_exp), ref_p) < (1e-5 if producer else 1e-6)
+    ref_o = np.argsort(-ref_p, axis=1, kind="stable")
+    assert np.array_equal(order.reshape(n_tok, n_exp)[:, :k], ref_o[:, :k])
+    ref_w = np.take_along_axis(ref_p, ref_o[:, :k], 1)
+    assert nmse(w.reshape(n_tok, k), ref_w) < 1e-6
+    assert nmse(wn.reshape(n_tok, k), ref_w / ref_w.sum(1, keepdims=True)) < 1e-6
+    assert any(ln.startswith("topk_moe") for ln in log), log
