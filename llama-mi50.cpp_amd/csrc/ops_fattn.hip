@@ -13,6 +13,7 @@
 // reads), block softmax update, then threads over (head, dim) accumulate P·V with
 // coalesced V row reads. Splits are merged by a combine kernel.
 #include "backend.h"
+#include "quants.cuh"
 #include <type_traits>
 
 namespace mx {
@@ -42,9 +43,42 @@ struct FaArgs {
 
 #define FA_TRACE(ph) MX_TRACE((blockIdx.x == 0 && blockIdx.y == 0) ? p.trace : nullptr, ph)
 
-template <typename T> __device__ __forceinline__ float ldkv(const T * p);
-template <> __device__ __forceinline__ float ldkv<uint16_t>(const uint16_t * p) { return h2f(*p); }
-template <> __device__ __forceinline__ float ldkv<float>(const float * p) { return *p; }
+// K/V element types of the tile kernel: f16 (uint16_t), f32 (float) and the tags below.
+// Element i of a row: the quantised caches store 32-element blocks, an f16 scale first
+// (block_q8_0 / block_q4_0, ggml-common.h), dequantised as the CPU's v_to_float does.
+struct KvBF16 {};
+struct KvQ8 {};
+struct KvQ4 {};
+template <typename T> __device__ __forceinline__ float kv_get(const char * row, int i);
+template <> __device__ __forceinline__ float kv_get<uint16_t>(const char * row, int i) { return h2f(((const uint16_t *) row)[i]); }
+template <> __device__ __forceinline__ float kv_get<float>(const char * row, int i) { return ((const float *) row)[i]; }
+template <> __device__ __forceinline__ float kv_get<KvBF16>(const char * row, int i) {
+    return __uint_as_float((uint32_t) ((const uint16_t *) row)[i] << 16);
+}
+template <> __device__ __forceinline__ float kv_get<KvQ8>(const char * row, int i) {
+    const char * b = row + (i >> 5) * 34;
+    return h2f(ld_u16(b)) * (float) (int8_t) b[2 + (i & 31)];
+}
+template <> __device__ __forceinline__ float kv_get<KvQ4>(const char * row, int i) {
+    const char * b = row + (i >> 5) * 18;
+    const int j = i & 31;
+    const int x = (uint8_t) b[2 + (j & 15)];
+    return h2f(ld_u16(b)) * (float) ((j < 16 ? x & 15 : x >> 4) - 8);
+}
+// q in the K type's vec-dot type (type_traits_cpu[k->type].vec_dot_type): f16 / bf16
+// rounding; the quantised K types dot against q8_0 blocks (quantize_row_q8_0_ref,
+// ggml-quants.c: d = amax/127 stored as f16, q = round(x/d)) — applied per 32-block
+// after the row is in LDS (fa_q8_blocks)
+template <typename TK> __device__ __forceinline__ float q_round(float x) {
+    if constexpr (std::is_same<TK, uint16_t>::value) return (float) (_Float16) x;
+    else if constexpr (std::is_same<TK, KvBF16>::value) {
+        uint32_t u = __float_as_uint(x);
+        if ((u & 0x7fffffff) > 0x7f800000) return __uint_as_float((u | 0x00400000u) & 0xffff0000u);   // quiet NaN
+        u += 0x7fff + ((u >> 16) & 1);
+        return __uint_as_float(u & 0xffff0000u);
+    } else return x;
+}
+template <typename TK> __host__ __device__ constexpr bool kv_q8dot() { return std::is_same<TK, KvQ8>::value || std::is_same<TK, KvQ4>::value; }
 
 template <typename TK, typename TV, int D>
 __global__ __launch_bounds__(256) void k_fattn(FaArgs p) {
@@ -67,7 +101,18 @@ __global__ __launch_bounds__(256) void k_fattn(FaArgs p) {
         const int g = i / D, d = i % D;
         const int64_t h = hk * G + g;
         const float x = *(const float *) (p.q + iq1 * p.q1 + h * p.q2 + iq3 * p.q3 + d * 4);
-        qs[g][d] = (float) (_Float16) x;
+        qs[g][d] = q_round<TK>(x);
+    }
+    if constexpr (kv_q8dot<TK>()) {
+        __syncthreads();
+        for (int b = tid; b < G * D / 32; b += blockDim.x) {
+            float * qb = &qs[0][0] + (b / (D / 32)) * D + (b % (D / 32)) * 32;
+            float amax = 0.f;
+            for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(qb[j]));
+            const float dq = amax / 127.0f, id = dq != 0.0f ? 1.0f / dq : 0.0f;
+            const float dh = (float) (_Float16) dq;
+            for (int j = 0; j < 32; ++j) qb[j] = dh * roundf(qb[j] * id);
+        }
     }
     if (tid < G) { mrun[tid] = -INFINITY; lrun[tid] = 0.f; }
     float slope[FA_MAXG];
@@ -99,17 +144,17 @@ __global__ __launch_bounds__(256) void k_fattn(FaArgs p) {
                 float acc[FA_MAXG];
 #pragma unroll
                 for (int g = 0; g < FA_MAXG; ++g) acc[g] = 0.f;
-                const TK * kr = (const TK *) (kb + key * p.k1);
+                const char * kr = kb + key * p.k1;
                 for (int d = 0; d < D; d += 8) {
                     float kv[8];
-                    if (sizeof(TK) == 2 && p.k_aligned) {
-                        const uint4 raw = *(const uint4 *) (kr + d);
+                    if (std::is_same<TK, uint16_t>::value && p.k_aligned) {
+                        const uint4 raw = *(const uint4 *) (kr + 2 * d);
                         const uint16_t * hh = (const uint16_t *) &raw;
 #pragma unroll
                         for (int i = 0; i < 8; ++i) kv[i] = h2f(hh[i]);
                     } else {
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) kv[i] = ldkv<TK>(kr + d + i);
+                        for (int i = 0; i < 8; ++i) kv[i] = kv_get<TK>(kr, d + i);
                     }
 #pragma unroll
                     for (int g = 0; g < FA_MAXG; ++g) {
@@ -167,10 +212,10 @@ __global__ __launch_bounds__(256) void k_fattn(FaArgs p) {
             const int g = o / D, d = o % D;
             if (g < G) {
                 float a = oacc[j] * alpha[g];
-                const TV * vp = (const TV *) (vb + t0 * p.v1) + d;
+                const char * vp = vb + t0 * p.v1;
                 for (int64_t i = 0; i < nk; ++i) {
                     const float pw = sc[g][i];
-                    a += pw * ldkv<TV>((const TV *) ((const char *) vp + i * p.v1));
+                    a += pw * kv_get<TV>(vp + i * p.v1, d);
                 }
                 oacc[j] = a;
             }
@@ -514,6 +559,7 @@ static int64_t fa_chunk(const ggml_tensor * dst, int64_t * nsplit_out) {
 }
 
 bool fa_dec2_ok(const ggml_tensor * dst);
+bool fa_mma_ok(const ggml_tensor * dst);
 size_t fa_dec2_scratch(const ggml_tensor * dst);
 void fa_dec2_run(OpCtx & c, ggml_tensor * dst);
 static bool g_fa_dec1 = getenv("GGML_MI355X_FA_DEC1") != nullptr;   // A/B: the v1 decode kernel
@@ -526,6 +572,9 @@ size_t flash_attn_scratch(const ggml_tensor * dst) {
     const int64_t rows = q->ne[1] * q->ne[2] * q->ne[3];
     size_t need = nsplit * rows * (v->ne[0] + 2) * sizeof(float) + 4 * 256;
     if (fa_dec2_ok(dst)) need = std::max(need, fa_dec2_scratch(dst));
+    const ggml_tensor * k = dst->src[1];
+    if (k->type != GGML_TYPE_F16 && fa_mma_ok(dst))      // f16 copies of quantised / bf16 K and V
+        need = std::max(need, (size_t) 2 * (mx_nelements(k) / k->ne[3]) * 2 + 512);
     return need;
 }
 
@@ -535,10 +584,14 @@ bool flash_attn_supported(const ggml_tensor * dst) {
     const ggml_tensor * v = dst->src[2];
     const ggml_tensor * m = dst->src[3];
     if (q->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
-    if (!((k->type == GGML_TYPE_F16 && v->type == GGML_TYPE_F16) || (k->type == GGML_TYPE_F32 && v->type == GGML_TYPE_F32))) return false;
+    if (k->type != v->type) return false;
     if (k->ne[0] != v->ne[0]) return false;
     const int64_t D = k->ne[0];
-    if (D != 32 && D != 40 && D != 48 && D != 64 && D != 80 && D != 96 && D != 112 && D != 128 && D != 256) return false;
+    if (k->type == GGML_TYPE_F16 || k->type == GGML_TYPE_F32) {
+        if (D != 32 && D != 40 && D != 48 && D != 64 && D != 80 && D != 96 && D != 112 && D != 128 && D != 256) return false;
+    } else if (k->type == GGML_TYPE_BF16 || k->type == GGML_TYPE_Q8_0 || k->type == GGML_TYPE_Q4_0) {
+        if (D != 64 && D != 128 && D != 256) return false;   // quantised / bf16 caches: the tile kernel's common head sizes
+    } else return false;
     if (q->ne[2] % k->ne[2] != 0 || q->ne[2] / k->ne[2] > FA_MAXG) return false;
     if (k->ne[2] != v->ne[2]) return false;
     if (m && m->type != GGML_TYPE_F16) return false;
@@ -550,6 +603,14 @@ bool flash_attn_supported(const ggml_tensor * dst) {
 
 template <typename TK, typename TV>
 static void fa_launch(OpCtx & c, int D, dim3 grid, const FaArgs & a) {
+    if constexpr (!std::is_same<TK, uint16_t>::value && !std::is_same<TK, float>::value) {
+        switch (D) {
+            case 64:  k_fattn<TK, TV, 64><<<grid, 256, 0, c.st>>>(a); return;
+            case 128: k_fattn<TK, TV, 128><<<grid, 256, 0, c.st>>>(a); return;
+            case 256: k_fattn<TK, TV, 256><<<grid, 256, 0, c.st>>>(a); return;
+            default: MX_ABORT("fattn D=%d", D);
+        }
+    }
     switch (D) {
         case 32:  k_fattn<TK, TV, 32><<<grid, 256, 0, c.st>>>(a); break;
         case 40:  k_fattn<TK, TV, 40><<<grid, 256, 0, c.st>>>(a); break;
@@ -566,6 +627,39 @@ static void fa_launch(OpCtx & c, int D, dim3 grid, const FaArgs & a) {
 
 bool fa_mma_ok(const ggml_tensor * dst);
 void fa_mma_run(OpCtx & c, ggml_tensor * dst);
+
+// bf16 / q8_0 / q4_0 K or V ([D, n_kv, Hkv] view) -> contiguous f16 [D, n_kv, Hkv] for the
+// MFMA prefill kernel (the reference's CUDA backend converts quantised K/V to f16 for its
+// tile / mma kernels the same way, fattn-common.cuh launch_fattn)
+template <typename T>
+__global__ void k_kv_to_f16(const char * __restrict__ src, size_t s1, size_t s2, int D, int n_kv, int Hkv, uint16_t * __restrict__ dst) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;   // one 8-element group
+    const int64_t ng = (int64_t) D / 8 * n_kv * Hkv;
+    if (i >= ng) return;
+    const int d0 = (int) (i % (D / 8)) * 8;
+    const int64_t r = i / (D / 8);
+    const int key = (int) (r % n_kv), h = (int) (r / n_kv);
+    const char * row = src + (size_t) h * s2 + (size_t) key * s1;
+    uint16_t o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2h(kv_get<T>(row, d0 + j));
+    uint4 w;
+    __builtin_memcpy(&w, o, 16);
+    *(uint4 *) (dst + (size_t) r * D + d0) = w;
+}
+
+void fa_kv_to_f16(OpCtx & c, const ggml_tensor * t, uint16_t * dst) {
+    const int D = (int) t->ne[0], n_kv = (int) t->ne[1], Hkv = (int) t->ne[2];
+    const int64_t ng = (int64_t) D / 8 * n_kv * Hkv;
+    const unsigned blocks = (unsigned) mx_ceil_div(ng, 256);
+    MX_KLOG("fa_kv_to_f16 type=%d D=%d n_kv=%d Hkv=%d", (int) t->type, D, n_kv, Hkv);
+    switch (t->type) {
+        case GGML_TYPE_BF16: k_kv_to_f16<KvBF16><<<blocks, 256, 0, c.st>>>((const char *) t->data, t->nb[1], t->nb[2], D, n_kv, Hkv, dst); break;
+        case GGML_TYPE_Q8_0: k_kv_to_f16<KvQ8><<<blocks, 256, 0, c.st>>>((const char *) t->data, t->nb[1], t->nb[2], D, n_kv, Hkv, dst); break;
+        case GGML_TYPE_Q4_0: k_kv_to_f16<KvQ4><<<blocks, 256, 0, c.st>>>((const char *) t->data, t->nb[1], t->nb[2], D, n_kv, Hkv, dst); break;
+        default: MX_ABORT("fa_kv_to_f16 type %d", (int) t->type);
+    }
+}
 static bool g_fa_mma_off = getenv("GGML_MI355X_FA_TILE") != nullptr;
 
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
@@ -626,8 +720,16 @@ void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
 #undef DECG
 #undef DEC
         if (nsplit == 1) return;
-    } else if (k->type == GGML_TYPE_F16) { MX_KLOG("fattn_tile D=%d f16", D); fa_launch<uint16_t, uint16_t>(c, D, grid, b); }
-    else fa_launch<float, float>(c, D, grid, b);
+    } else {
+        MX_KLOG("fattn_tile D=%d type=%d", D, (int) k->type);
+        switch (k->type) {
+            case GGML_TYPE_F16:  fa_launch<uint16_t, uint16_t>(c, D, grid, b); break;
+            case GGML_TYPE_BF16: fa_launch<KvBF16, KvBF16>(c, D, grid, b); break;
+            case GGML_TYPE_Q8_0: fa_launch<KvQ8, KvQ8>(c, D, grid, b); break;
+            case GGML_TYPE_Q4_0: fa_launch<KvQ4, KvQ4>(c, D, grid, b); break;
+            default:             fa_launch<float, float>(c, D, grid, b); break;
+        }
+    }
     // decode: also emit the q8 activation of the output for the O-projection GEMV
     ActQ * q8 = nullptr;
     if (D % 32 == 0 && q->ne[1] * q->ne[3] > 1 && q->ne[1] * q->ne[3] <= 8 && mx_is_contiguous(dst))

@@ -20,6 +20,7 @@
 //    last one to arrive (device-scope counter, reset by it for the next launch / graph
 //    replay) combines them — no second kernel, no second launch gap.
 #include "backend.h"
+#include "quants.cuh"
 
 namespace mx { extern int g_tune[32]; }
 
@@ -35,14 +36,26 @@ struct FaDecArgs {
     unsigned int * cnt;            // per (q row, seq, KV head) arrival counters, zero between launches
     int n_q, n_kv, H, Hkv, ns_kv, nsplit;
     float scale;
+    unsigned long long * trace;    // debug (MX_TRACE), workgroup 0
+    unsigned long long * trace_blk;
 };
 
 constexpr int FD_NI = 4;          // key-row load instructions per wave per chunk
 constexpr int FD_MAXSPLIT = 16;   // workgroups per (q row, KV head); longer caches loop over chunks
 
+// q8_0 K/V (KQ, `-ctk q8_0 -ctv q8_0`): a lane's 8 dimensions are 8 int8 of one 32-block
+// (its f16 scale first: block_q8_0), q is quantised to q8_0 per 32-block as the CPU's
+// vec_dot_type conversion does (amax over the block's 4 lanes by DPP, d = amax/127 kept
+// as f16), q·k = Σ_blocks d_q·d_k·Σ q_i k_i, V dequantised d·q_i into the f32 sums.
+__device__ __forceinline__ uint2 ldu8(const char * p) {   // 8 bytes, any 2-byte alignment
+    uint2 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 2), 8);
+    return v;
+}
+
 // G = query heads per workgroup (a divisor of the GQA ratio Gt; K/V are read once per
 // workgroup), NW = waves per workgroup (the chunk is NW x 16/32 keys)
-template <int D, int G, int NW>
+template <int D, int G, int NW, bool KQ = false>
 __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     constexpr int NT = 64 * NW;
     constexpr int LPK = D / 8;            // lanes per key row
@@ -65,14 +78,42 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     const int split = blockIdx.y;
     const int hb = hk * Gt + gb * G;                         // first query head
     const int hslot = hk * NGB + gb;                         // partial / counter slot
-    const char * kb = p.k + (size_t) hk * p.k2 + (size_t) (iq3 % p.ns_kv) * p.k3 + c * 16;
-    const char * vb = p.v + (size_t) hk * p.v2 + (size_t) (iq3 % p.ns_kv) * p.v3 + c * 16;
+    // this lane's 8 dimensions of a row: f16 at 16 c; q8_0 at block c/4 (34 B), byte 8 (c%4)
+    const int lofs = KQ ? (c >> 2) * 34 + 2 + 8 * (c & 3) : c * 16;
+    const int dofs = (c >> 2) * 34;
+    const char * kb = p.k + (size_t) hk * p.k2 + (size_t) (iq3 % p.ns_kv) * p.k3 + lofs;
+    const char * vb = p.v + (size_t) hk * p.v2 + (size_t) (iq3 % p.ns_kv) * p.v3 + lofs;
     const uint16_t * mrow = (const uint16_t *) (p.mask ? p.mask + (size_t) iq1 * p.m1 + (size_t) (iq3 % p.mne3) * p.m3 : p.k);
     const int nch = (p.n_kv + CS - 1) / CS, cpb = (nch + p.nsplit - 1) / p.nsplit;
+    unsigned long long * tr = (blockIdx.x == 0 && blockIdx.y == 0) ? p.trace : nullptr;
+    MX_TRACE(tr, 0);
+    MX_TRACE_BLK(p.trace_blk, 0);
 
     // q first (it is consumed first): the CPU vec-dot rounds q to the K type (f16)
     h2v qh[G][4];
-    {
+    int qq8[G][2];                                           // KQ: q as q8_0, 8 int8
+    float qd[G];                                             // KQ: its block scale (f16-rounded)
+    if constexpr (KQ) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const float * qp = (const float *) (p.q + (size_t) iq1 * p.q1 + (size_t) (hb + h) * p.q2 + (size_t) iq3 * p.q3) + 8 * c;
+            const float4 a0 = *(const float4 *) qp, a1 = *(const float4 *) (qp + 4);
+            const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            float amax = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(x[j]));
+            amax = dpp_max_group<4>(amax);
+            const float dq = amax / 127.0f, id = dq != 0.0f ? 1.0f / dq : 0.0f;
+            qd[h] = (float) (_Float16) dq;
+            int w0 = 0, w1 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                w0 |= ((int) roundf(x[j] * id) & 0xFF) << (8 * j);
+                w1 |= ((int) roundf(x[4 + j] * id) & 0xFF) << (8 * j);
+            }
+            qq8[h][0] = w0; qq8[h][1] = w1;
+        }
+    } else {
         float4 qa[G], qb[G];
 #pragma unroll
         for (int h = 0; h < G; ++h) {
@@ -102,26 +143,52 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         // costs a wait at the join): mask, K rows, V rows — coalesced, LPK lanes per row
         uint16_t mraw[FD_NI];
         uint4 kr[FD_NI], vr[FD_NI];
+        uint16_t kd[FD_NI], vd[FD_NI];                        // KQ: block scales
 #pragma unroll
         for (int t = 0; t < FD_NI; ++t) mraw[t] = mrow[min(key0 + t * KPI, p.n_kv - 1)];
+        if constexpr (KQ) {
 #pragma unroll
-        for (int t = 0; t < FD_NI; ++t) kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
+            for (int t = 0; t < FD_NI; ++t) {
+                const size_t ko = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1;
+                const uint2 w = ldu8(kb + ko);
+                kr[t] = make_uint4(w.x, w.y, 0, 0);
+                kd[t] = ld_u16(kb - lofs + dofs + ko);
+            }
 #pragma unroll
-        for (int t = 0; t < FD_NI; ++t) vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
+            for (int t = 0; t < FD_NI; ++t) {
+                const size_t vo = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1;
+                const uint2 w = ldu8(vb + vo);
+                vr[t] = make_uint4(w.x, w.y, 0, 0);
+                vd[t] = ld_u16(vb - lofs + dofs + vo);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < FD_NI; ++t) kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
+#pragma unroll
+            for (int t = 0; t < FD_NI; ++t) vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
+        }
         __builtin_amdgcn_sched_barrier(0);
+        if (ci == 0) MX_TRACE(tr, 1);
         float mk[FD_NI];
 #pragma unroll
         for (int t = 0; t < FD_NI; ++t) mk[t] = key0 + t * KPI < p.n_kv ? (p.mask ? h2f(mraw[t]) : 0.f) : -INFINITY;
         // scores: q·k over the row's LPK lanes (DPP), one per (head, key) in every lane of the row
         float s[G][FD_NI];
+        if (ci == 0) { asm volatile("" :: "v"(kr[0].x), "v"(vr[0].x), "v"(vr[FD_NI - 1].w)); MX_TRACE(tr, 2); }
 #pragma unroll
         for (int t = 0; t < FD_NI; ++t) {
 #pragma unroll
             for (int h = 0; h < G; ++h) {
-                float acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[h][0], 0.f, false);
-                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[h][1], acc, false);
-                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[h][2], acc, false);
-                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[h][3], acc, false);
+                float acc;
+                if constexpr (KQ) {
+                    const int si = dot4_i8((int) kr[t].y, qq8[h][1], dot4_i8((int) kr[t].x, qq8[h][0], 0));
+                    acc = (float) si * (qd[h] * h2f(kd[t]));
+                } else {
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[h][0], 0.f, false);
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[h][1], acc, false);
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[h][2], acc, false);
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[h][3], acc, false);
+                }
                 acc = dpp_sum_group<LPK>(acc);
                 // log2 domain (v_exp_f32 below): s = (q·k·scale + mask) · log2(e)
                 s[h][t] = mk[t] == -INFINITY ? -INFINITY : (acc * p.scale + mk[t]) * 1.4426950408889634f;
@@ -148,11 +215,19 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             for (int i = 0; i < 8; ++i) o[h][i] *= a;
 #pragma unroll
             for (int t = 0; t < FD_NI; ++t) {
-                const uint32_t vw[4] = {vr[t].x, vr[t].y, vr[t].z, vr[t].w};
+                if constexpr (KQ) {
+                    const float dv = h2f(vd[t]);
+                    const uint32_t vw[2] = {vr[t].x, vr[t].y};
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    o[h][2 * i] += pr[t] * h2f((uint16_t) (vw[i] & 0xFFFF));
-                    o[h][2 * i + 1] += pr[t] * h2f((uint16_t) (vw[i] >> 16));
+                    for (int i = 0; i < 8; ++i)
+                        o[h][i] += pr[t] * (dv * (float) (int8_t) ((vw[i >> 2] >> (8 * (i & 3))) & 0xFF));
+                } else {
+                    const uint32_t vw[4] = {vr[t].x, vr[t].y, vr[t].z, vr[t].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        o[h][2 * i] += pr[t] * h2f((uint16_t) (vw[i] & 0xFFFF));
+                        o[h][2 * i + 1] += pr[t] * h2f((uint16_t) (vw[i] >> 16));
+                    }
                 }
             }
         }
@@ -169,7 +244,9 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             *(float4 *) &wo[wave][h][8 * c + 4] = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
         }
     }
+    MX_TRACE(tr, 3);
     __syncthreads();
+    MX_TRACE(tr, 4);
 
     // ---- merge the four waves: (O, M, L) of this split for the G heads
     constexpr int PW = G * (D + 2);                          // partial floats per workgroup
@@ -200,6 +277,8 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             }
         }
     }
+    MX_TRACE(tr, 5);
+    MX_TRACE_BLK(p.trace_blk, 1);
     if (p.nsplit == 1) return;
 
     // ---- split merge by the last workgroup of this (q row, KV head) to arrive
@@ -252,7 +331,8 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
 // no softcap / ALiBi / sinks, few query rows (decode)
 bool fa_dec2_ok(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
-    if (q->ne[1] > 4 || k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16) return false;
+    const bool kq = k->type == GGML_TYPE_Q8_0 && v->type == GGML_TYPE_Q8_0;
+    if (q->ne[1] > 4 || !((k->type == GGML_TYPE_F16 && v->type == GGML_TYPE_F16) || kq)) return false;
     const int64_t D = k->ne[0];
     if ((D != 64 && D != 128) || v->ne[0] != D) return false;
     const int64_t G = q->ne[2] / k->ne[2];
@@ -260,14 +340,17 @@ bool fa_dec2_ok(const ggml_tensor * dst) {
     if (dst->src[4]) return false;                                        // sinks
     if (mx_op_param<float>(dst, 1) != 0.0f || mx_op_param<float>(dst, 2) != 0.0f) return false;   // ALiBi, softcap
     if (m && (m->type != GGML_TYPE_F16 || m->ne[2] > 1)) return false;
-    if (k->nb[1] % 16 || v->nb[1] % 16 || k->nb[2] % 16 || v->nb[2] % 16 || (uintptr_t) k->data % 16 || (uintptr_t) v->data % 16) return false;
+    if (kq) {   // q8_0 rows: 2-byte aligned blocks, 8-byte loads at any 2-byte alignment
+        if (k->nb[1] % 2 || v->nb[1] % 2 || k->nb[2] % 2 || v->nb[2] % 2 || (uintptr_t) k->data % 2 || (uintptr_t) v->data % 2) return false;
+    } else if (k->nb[1] % 16 || v->nb[1] % 16 || k->nb[2] % 16 || v->nb[2] % 16 || (uintptr_t) k->data % 16 || (uintptr_t) v->data % 16) return false;
     if (q->nb[1] % 16 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return false;
     if (q->ne[3] != k->ne[3] && k->ne[3] != 1) return false;
     if (k->ne[1] > INT32_MAX / 2 || q->ne[1] * q->ne[3] * q->ne[2] > MX_FA_CNT) return false;
     // longer caches: the split-merging geometry measured slower than the v1 kernel +
     // combine (fa_1024 12.3 vs 12.6 us, fa_4096 17.5 vs 16.3, opbench on MI355X), so only
     // the single-split geometry is used unless g_tune[10] = 3 forces the split one
-    if (g_tune[10] != 3 && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;
+    // (q8_0 caches have no v1 kernel: every length takes this one)
+    if (g_tune[10] != 3 && !kq && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;
     return true;
 }
 
@@ -308,9 +391,15 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     a.nsplit = f.nsplit;
     a.part = (float *) c.scratch->take(fa_dec2_scratch(dst));
     a.cnt = c.s->fa_cnt;
+    a.trace = mx_trace_slot(0);
+    a.trace_blk = mx_trace_blocks();
     const dim3 grid((unsigned) (a.Hkv * (Gt / f.G) * a.n_q * q->ne[3]), (unsigned) a.nsplit);
-MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv);
-#define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { k_fattn_dec2<DD, GG, NWW><<<grid, 64 * NWW, 0, c.st>>>(a); return; }
+    const bool kq = k->type == GGML_TYPE_Q8_0;
+    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv, (int) kq);
+#define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { \
+        if (kq) k_fattn_dec2<DD, GG, NWW, true><<<grid, 64 * NWW, 0, c.st>>>(a); \
+        else k_fattn_dec2<DD, GG, NWW><<<grid, 64 * NWW, 0, c.st>>>(a); \
+        return; }
     FD(128, 1, 16) FD(64, 1, 16)
     FD(128, 4, 4) FD(128, 1, 4) FD(128, 2, 4) FD(128, 8, 4) FD(64, 1, 4) FD(64, 2, 4) FD(64, 4, 4) FD(64, 8, 4)
 #undef FD

@@ -484,3 +484,70 @@ void orc_flash_attn(const float * q, const uint16_t * k, const uint16_t * v, con
     free(qh);
     free(acc);
 }
+
+/* FLASH_ATTN_EXT with K/V of any cache type (f32, f16, bf16, q8_0, q4_0): the one_chunk
+ * loop of ggml_compute_forward_flash_attn_ext_f16 (ops.cpp:8045-8260). q is converted to
+ * the K type's vec_dot_type (type_traits_cpu: f16 -> f16, bf16 -> bf16, q8_0 / q4_0 ->
+ * q8_0 blocks, f32 -> f32), q·k is the vec_dot of the two rows (computed here exactly on
+ * the dequantised values, double accumulation), V rows are converted to f32 (v_to_float).
+ * k, v: [Hkv][n_kv] rows of ggml_row_size(kv_type, D) bytes. */
+static float orc_round_bf16(float f) {
+    uint32_t u = f2u(f);
+    if ((u & 0x7fffffff) > 0x7f800000) return u2f((u | 0x00400000u) & 0xffff0000u);
+    u += 0x7fff + ((u >> 16) & 1);
+    return u2f(u & 0xffff0000u);
+}
+
+int orc_flash_attn_t(const float * q, const void * k, const void * v, const uint16_t * mask,
+                     float * out, int64_t D, int64_t n_q, int64_t n_kv, int64_t H, int64_t Hkv,
+                     float scale, float max_bias, float softcap, int kv_type) {
+    if (kv_type != T_F32 && kv_type != T_F16 && kv_type != T_BF16 && kv_type != T_Q8_0 && kv_type != T_Q4_0) return -1;
+    if (D % blck(kv_type)) return -1;
+    const size_t rb = (size_t) (D / blck(kv_type)) * bsize(kv_type);
+    if (softcap != 0) scale /= softcap;
+    const uint32_t n_head_log2 = 1u << (uint32_t) floor(log2((double) H));
+    const float m0 = powf(2.0f, -(max_bias) / n_head_log2);
+    const float m1 = powf(2.0f, -(max_bias / 2.0f) / n_head_log2);
+    float * qh = (float *) malloc((size_t) D * sizeof(float));
+    float * kr = (float *) malloc((size_t) D * sizeof(float));
+    float * vr = (float *) malloc((size_t) D * sizeof(float));
+    uint8_t * q8 = (uint8_t *) malloc((size_t) (D / 32 + 1) * 34);
+    double * acc = (double *) malloc((size_t) D * sizeof(double));
+    for (int64_t iq = 0; iq < n_q; ++iq) {
+        for (int64_t h = 0; h < H; ++h) {
+            const uint32_t hh = (uint32_t) h;
+            const float slope = max_bias > 0.0f ? (hh < n_head_log2 ? powf(m0, hh + 1) : powf(m1, 2 * (hh - n_head_log2) + 1)) : 1.0f;
+            const int64_t hk = h / (H / Hkv);
+            const float * qr = q + (h * n_q + iq) * D;
+            if (kv_type == T_Q8_0 || kv_type == T_Q4_0) {
+                orc_quantize_row_q8_0(qr, q8, D);
+                orc_dequantize_row(T_Q8_0, q8, qh, D);
+            } else {
+                for (int64_t d = 0; d < D; ++d)
+                    qh[d] = kv_type == T_F16 ? orc_fp16_to_fp32(orc_fp32_to_fp16(qr[d])) : kv_type == T_BF16 ? orc_round_bf16(qr[d]) : qr[d];
+            }
+            double M = -INFINITY, S = 0;
+            for (int64_t d = 0; d < D; ++d) acc[d] = 0;
+            for (int64_t ic = 0; ic < n_kv; ++ic) {
+                const float mv = mask ? slope * orc_fp16_to_fp32(mask[iq * n_kv + ic]) : 0.0f;
+                if (mv == -INFINITY) continue;
+                orc_dequantize_row(kv_type, (const uint8_t *) k + (size_t) (hk * n_kv + ic) * rb, kr, D);
+                double s = 0;
+                for (int64_t d = 0; d < D; ++d) s += (double) qh[d] * kr[d];
+                float sf = (float) s * scale;
+                if (softcap != 0.0f) sf = softcap * tanhf(sf);
+                sf += mv;
+                double ms = 1, vs = 1;
+                if (sf > M) { const double Mold = M; M = sf; ms = isinf(Mold) ? 0 : exp(Mold - M); for (int64_t d = 0; d < D; ++d) acc[d] *= ms; }
+                else vs = exp(sf - M);
+                orc_dequantize_row(kv_type, (const uint8_t *) v + (size_t) (hk * n_kv + ic) * rb, vr, D);
+                for (int64_t d = 0; d < D; ++d) acc[d] += vs * vr[d];
+                S = S * ms + vs;
+            }
+            const double inv = S == 0 ? 0 : 1.0 / S;
+            for (int64_t d = 0; d < D; ++d) out[(iq * H + h) * D + d] = (float) (acc[d] * inv);
+        }
+    }
+    free(qh); free(kr); free(vr); free(q8); free(acc);
+    return 0;
+}

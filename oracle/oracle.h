@@ -60,6 +60,12 @@ void orc_flash_attn(const float * q, const uint16_t * k, const uint16_t * v, con
                     float * out, int64_t D, int64_t n_q, int64_t n_kv, int64_t H, int64_t Hkv,
                     float scale, float max_bias, float softcap);
 
+/* the same with K/V rows of kv_type (0 f32, 1 f16, 30 bf16, 8 q8_0, 2 q4_0), q in the K
+ * type's vec_dot_type (q8_0 blocks for the quantised caches); -1: unsupported */
+int orc_flash_attn_t(const float * q, const void * k, const void * v, const uint16_t * mask,
+                     float * out, int64_t D, int64_t n_q, int64_t n_kv, int64_t H, int64_t Hkv,
+                     float scale, float max_bias, float softcap, int kv_type);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,6 +30,8 @@ class Oracle:
         L.orc_swiglu.argtypes = [P, P, P, ctypes.c_int64]
         L.orc_f32_to_f16.argtypes = [P, P, ctypes.c_int64]
         L.orc_flash_attn.argtypes = [P, P, P, P, P] + [ctypes.c_int64] * 5 + [ctypes.c_float] * 3
+        L.orc_flash_attn_t.restype = ctypes.c_int
+        L.orc_flash_attn_t.argtypes = [P, P, P, P, P] + [ctypes.c_int64] * 5 + [ctypes.c_float] * 3 + [ctypes.c_int]
 
     @staticmethod
     def _p(a):
@@ -102,6 +104,71 @@ class Oracle:
         self.lib.orc_flash_attn(q.ctypes.data, k.ctypes.data, v.ctypes.data, self._p(mask), out.ctypes.data,
                                 D, n_q, n_kv, H, Hkv, scale, max_bias, softcap)
         return out
+
+    def flash_attn_t(self, q, k, v, mask, scale, kv_type, max_bias=0.0, softcap=0.0):
+        """k, v: [Hkv, n_kv, row_bytes] uint8 rows of ggml type kv_type (f32 0, f16 1, q4_0 2, q8_0 8, bf16 30)"""
+        H, n_q, D = q.shape
+        Hkv, n_kv = k.shape[:2]
+        out = np.empty((n_q, H, D), np.float32)
+        q = np.ascontiguousarray(q, np.float32); k = np.ascontiguousarray(k); v = np.ascontiguousarray(v)
+        assert self.lib.orc_flash_attn_t(q.ctypes.data, k.ctypes.data, v.ctypes.data, self._p(mask), out.ctypes.data,
+                                         D, n_q, n_kv, H, Hkv, scale, max_bias, softcap, kv_type) == 0
+        return out
+
+
+REF_OPS = os.path.join(ROOT, "oracle", "_ref", "libref-ops.so")
+
+
+class RefOps:
+    """single ops on the reference's own CPU ggml (oracle/ref_ops.cpp over libggml-ref.so)"""
+
+    def __init__(self, lib):
+        self.lib = lib
+        lib.refop_flash_attn.restype = ctypes.c_int
+        lib.refop_flash_attn.argtypes = [P, P, P, P, P] + [ctypes.c_int64] * 5 + [ctypes.c_float] * 3 + [ctypes.c_int]
+        lib.refop_rope.restype = ctypes.c_int
+        lib.refop_rope.argtypes = [P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, P, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int] + [ctypes.c_float] * 6 + [P]
+        lib.refop_soft_max.restype = ctypes.c_int
+        lib.refop_soft_max.argtypes = [P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, P, ctypes.c_float, ctypes.c_float]
+        lib.refop_rms_norm.restype = ctypes.c_int
+        lib.refop_rms_norm.argtypes = [P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_float]
+
+    def flash_attn(self, q, k, v, mask, scale, kv_type, max_bias=0.0, softcap=0.0):
+        H, n_q, D = q.shape
+        Hkv, n_kv = k.shape[:2]
+        out = np.empty((n_q, H, D), np.float32)
+        q = np.ascontiguousarray(q, np.float32); k = np.ascontiguousarray(k); v = np.ascontiguousarray(v)
+        assert self.lib.refop_flash_attn(q.ctypes.data, k.ctypes.data, v.ctypes.data, Oracle._p(mask), out.ctypes.data,
+                                         D, n_q, n_kv, H, Hkv, scale, max_bias, softcap, kv_type) == 0
+        return out
+
+    def rope(self, x, pos, n_dims, mode, n_ctx_orig, base, freq_scale=1.0, ext=0.0, attn=1.0, bf=32.0, bs=1.0, ff=None):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.empty_like(x)
+        pos = np.ascontiguousarray(pos, np.int32)
+        ne2, ne1, ne0 = x.shape
+        assert self.lib.refop_rope(x.ctypes.data, y.ctypes.data, ne0, ne1, ne2, pos.ctypes.data, n_dims, mode, n_ctx_orig,
+                                   base, freq_scale, ext, attn, bf, bs, Oracle._p(ff)) == 0
+        return y
+
+    def soft_max(self, x, mask_f16, scale, max_bias=0.0):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.empty_like(x)
+        ne02, ne01, ne00 = x.shape
+        assert self.lib.refop_soft_max(x.ctypes.data, y.ctypes.data, ne00, ne01, ne02, Oracle._p(mask_f16), scale, max_bias) == 0
+        return y
+
+    def rms_norm(self, x, eps):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.empty_like(x)
+        assert self.lib.refop_rms_norm(x.ctypes.data, y.ctypes.data, x.shape[-1], x.size // x.shape[-1], eps) == 0
+        return y
+
+
+def load_ref_ops():
+    """None when the reference build (oracle/_ref) is absent"""
+    return RefOps(ctypes.CDLL(REF_OPS)) if os.path.exists(REF_OPS) else None
 
 
 def load():

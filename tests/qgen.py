@@ -30,3 +30,30 @@ def nmse(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.sum((a - b) ** 2) / max(np.sum(b ** 2), 1e-30))
+
+
+# KV-cache rows of every cache type FLASH_ATTN_EXT takes: name -> ggml type id
+KV_TYPES = {"f32": 0, "f16": 1, "q4_0": 2, "q8_0": 8, "bf16": 30}
+
+
+def kv_rows(kind, Hkv, n_kv, D, rng, orc):
+    """[Hkv, n_kv, row bytes] uint8 K or V rows of cache type `kind` holding N(0, 1) data
+    (q8_0 by the oracle's quantize_row_q8_0_ref; q4_0 as random nibbles with d ~ 0.25)"""
+    x = rng.standard_normal((Hkv, n_kv, D)).astype(np.float32)
+    if kind == "f32":
+        return x.view(np.uint8).reshape(Hkv, n_kv, -1)
+    if kind == "f16":
+        return x.astype(np.float16).view(np.uint8).reshape(Hkv, n_kv, -1)
+    if kind == "bf16":
+        u = x.view(np.uint32)
+        u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+        return u.astype(np.uint16).view(np.uint8).reshape(Hkv, n_kv, -1)
+    if kind == "q8_0":
+        rows = [orc.quantize_q8_0(r) for r in x.reshape(-1, D)]
+        return np.stack(rows).reshape(Hkv, n_kv, -1)
+    if kind == "q4_0":
+        nb = Hkv * n_kv * D // 32
+        raw = rng.integers(0, 256, size=(nb, 18), dtype=np.uint8)
+        raw[:, 0:2] = (0.25 * rng.uniform(0.5, 1.5, size=nb)).astype(np.float16).view(np.uint8).reshape(nb, 2)
+        return raw.reshape(Hkv, n_kv, -1)
+    raise ValueError(kind)

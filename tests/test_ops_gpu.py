@@ -297,6 +297,51 @@ def test_flash_attn_split_merge(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
         lib.ggml_backend_mi355x_set_tune(10, 0)
 
 
+@pytest.mark.parametrize("kind", ["q8_0", "q4_0", "bf16", "f32"])
+@pytest.mark.parametrize("n_q,n_kv,H,Hkv,D,softcap", [
+    (1, 256, 32, 8, 128, 0.0),      # tg128 decode step: k_fattn_dec2 (q8_0 native), tile kernel otherwise
+    (1, 1500, 32, 8, 128, 0.0),     # long cache: dec2 split merge (q8_0)
+    (2, 130, 8, 2, 64, 0.0),        # two query rows, D 64
+    (512, 512, 32, 8, 128, 0.0),    # pp512 prefill: f16 copies + k_fa_mma2
+    (40, 320, 8, 2, 64, 0.0),       # prefill D 64: f16 copies + k_fa_mma
+    (5, 200, 4, 2, 128, 10.0),      # softcap: tile kernel
+])
+def test_flash_attn_kv_types(pkg, backend, orc, kind, n_q, n_kv, H, Hkv, D, softcap):
+    """quantised / bf16 / f32 KV caches (llama-bench -ctk/-ctv, tests/test-backend-ops.cpp:8232)
+    against orc_flash_attn_t, which is pinned to the reference CPU backend (test_oracle.py)"""
+    from qgen import KV_TYPES, kv_rows
+    if kind == "f32" and (n_q >= 512 or n_kv > 1000):
+        pytest.skip("f32 caches: the tile kernel only; large shapes add nothing")
+    rng = np.random.default_rng(n_q * 1000 + n_kv + D)
+    q = rng.standard_normal((H, n_q, D)).astype(np.float32)
+    k = kv_rows(kind, Hkv, n_kv, D, rng, orc)
+    v = kv_rows(kind, Hkv, n_kv, D, rng, orc)
+    mask = np.zeros((n_q, n_kv), np.float32)
+    for i in range(n_q):
+        mask[i, n_kv - n_q + i + 1:] = -np.inf
+    m16 = mask.astype(np.float16).view(np.uint16)
+    scale = 1.0 / np.sqrt(D)
+    tid = KV_TYPES[kind]
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, n_q, H)
+        tk = ctx.new_tensor(tid, D, n_kv, Hkv)
+        tv = ctx.new_tensor(tid, D, n_kv, Hkv)
+        tm = ctx.new_tensor("f16", n_kv, n_q)
+        return [ctx.flash_attn_ext(tq, tk, tv, tm, scale, 0.0, softcap)], [(tq, q), (tk, k), (tv, v), (tm, m16)]
+
+    backend.klog(True)
+    y = run(pkg, backend, build)[0].reshape(n_q, H, D)
+    log = backend.klog_read()
+    backend.klog(False)
+    ref = orc.flash_attn_t(q, k, v, m16, scale, tid, 0.0, softcap)
+    assert nmse(y, ref) < 5e-4, nmse(y, ref)
+    if kind == "q8_0" and n_q <= 4 and softcap == 0.0:
+        assert any(ln.startswith("fattn_dec2") and "kq8=1" in ln for ln in log), log
+    if n_q >= 16 and softcap == 0.0 and kind != "f32":
+        assert any(ln.startswith("fa_kv_to_f16") for ln in log) and any(ln.startswith("fa_mma") for ln in log), log
+
+
 def test_mul_mat_id(pkg, backend, orc):
     tid = NAMES["q4_K"]
     rng = np.random.default_rng(8)

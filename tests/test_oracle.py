@@ -115,3 +115,72 @@ def test_flash_attn_oracle_vs_dense_softmax(orc):
         p /= p.sum(-1, keepdims=True)
         ref = p @ v[kv].astype(np.float64)
         assert np.allclose(out[:, h], ref, rtol=1e-4, atol=1e-5)
+
+
+# ---------------------------------------------------------------------------
+# the oracle op by op against the reference's own CPU ggml (oracle/ref_ops.cpp over
+# oracle/_ref/libggml-ref.so, compiled from /root/reference by oracle/Makefile)
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def refops():
+    import oracle_lib
+    r = oracle_lib.load_ref_ops()
+    if r is None:
+        pytest.skip("oracle/_ref/libref-ops.so not built (make -C oracle ref)")
+    return r
+
+
+def _mask(n_q, n_kv):
+    m = np.zeros((n_q, n_kv), np.float32)
+    for i in range(n_q):
+        m[i, n_kv - n_q + i + 1:] = -np.inf
+    return m.astype(np.float16).view(np.uint16)
+
+
+@pytest.mark.parametrize("kind", ["f16", "f32", "bf16", "q8_0", "q4_0"])
+@pytest.mark.parametrize("n_q,n_kv,H,Hkv,D,max_bias,softcap", [(1, 113, 8, 2, 64, 0.0, 0.0), (7, 96, 4, 4, 128, 0.0, 0.0),
+                                                               (3, 64, 4, 1, 64, 8.0, 0.0), (2, 70, 4, 2, 128, 0.0, 10.0)])
+def test_flash_attn_oracle_vs_reference(orc, refops, kind, n_q, n_kv, H, Hkv, D, max_bias, softcap):
+    """orc_flash_attn_t against ggml_flash_attn_ext on the reference CPU backend, every
+    cache type of the harness grid (tests/test-backend-ops.cpp:8232), mask, ALiBi, softcap"""
+    from qgen import KV_TYPES, kv_rows
+    rng = np.random.default_rng(n_kv * 7 + D)
+    q = rng.standard_normal((H, n_q, D)).astype(np.float32)
+    k = kv_rows(kind, Hkv, n_kv, D, rng, orc)
+    v = kv_rows(kind, Hkv, n_kv, D, rng, orc)
+    m = _mask(n_q, n_kv)
+    scale = 1.0 / np.sqrt(D)
+    mine = orc.flash_attn_t(q, k, v, m, scale, KV_TYPES[kind], max_bias, softcap)
+    ref = refops.flash_attn(q, k, v, m, scale, KV_TYPES[kind], max_bias, softcap)
+    # the reference accumulates f16 V rows in f16 (VKQ16, ops.cpp one_chunk); the oracle in double
+    assert nmse(mine, ref) < (2e-5 if kind == "f16" else 1e-9), nmse(mine, ref)
+
+
+@pytest.mark.parametrize("mode,n_dims,ext", [(0, 128, 0.0), (2, 128, 0.0), (0, 64, 0.0), (2, 128, 1.0)])
+def test_rope_oracle_vs_reference(orc, refops, mode, n_dims, ext):
+    rng = np.random.default_rng(11 + mode + n_dims)
+    x = rng.standard_normal((5, 4, 128)).astype(np.float32)
+    pos = np.array([0, 1, 17, 300, 4095], np.int32)
+    args = (pos, n_dims, mode, 8192, 500000.0, 0.5 if ext else 1.0, ext, 1.0, 32.0, 1.0)
+    mine = orc.rope(x, *args)
+    ref = refops.rope(x, *args)
+    assert nmse(mine, ref) < 1e-12, nmse(mine, ref)
+
+
+@pytest.mark.parametrize("masked,max_bias", [(False, 0.0), (True, 0.0), (True, 8.0)])
+def test_soft_max_oracle_vs_reference(orc, refops, masked, max_bias):
+    rng = np.random.default_rng(21)
+    x = rng.standard_normal((4, 6, 77)).astype(np.float32) * 3
+    m = None
+    if masked:
+        mm = np.where(rng.random((6, 77)) < 0.3, -np.inf, rng.standard_normal((6, 77))).astype(np.float16)
+        m = mm.view(np.uint16)
+    mine = orc.soft_max(x, m, 0.7, max_bias)
+    ref = refops.soft_max(x, m, 0.7, max_bias)
+    assert nmse(mine, ref) < 1e-12, nmse(mine, ref)
+
+
+def test_rms_norm_oracle_vs_reference(orc, refops):
+    rng = np.random.default_rng(31)
+    x = rng.standard_normal((5, 4096)).astype(np.float32) * 2
+    assert nmse(orc.rms_norm(x, 1e-5), refops.rms_norm(x, 1e-5)) < 1e-12
