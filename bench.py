@@ -191,8 +191,9 @@ def dropin_bench(args):
     (oracle/_ref/ref-llama-bench, llama-bench's test_prompt / test_gen loop,
     tools/llama-bench/llama-bench.cpp:1962-2010, warmup + -r repetitions) loads
     libggml-mi355x.so through GGML_BACKEND_PATH with every layer offloaded (-ngl 99), on
-    the same Llama-3-8B Q4_K_M GGUF. Reports tg128 and pp512 at -fa 1 and -fa 0 and the
-    executor's counters per llama_decode."""
+    the same Llama-3-8B Q4_K_M GGUF. Reports tg128 and pp512 at -fa 1 and -fa 0, at -fa 1
+    with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv) and the executor's counters per
+    llama_decode."""
     if not os.path.exists(REF_BENCH) or args.no_dropin:
         return None
     out = {"how": "reference libllama (oracle/_ref/ref-llama-bench) + GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, "
@@ -200,22 +201,24 @@ def dropin_bench(args):
     try:
         gguf = bench_gguf()
         env = dict(os.environ, GGML_BACKEND_PATH=LIB, GGML_MI355X_STATS="1")
-        for fa in (1, 0):
+        for fa, ctk in ((1, None), (0, None), (1, 8)):        # 8 = GGML_TYPE_Q8_0
             for test, pp, tg in (("tg128", 0, args.tg), ("pp512", args.pp, 0)):
                 if (pp or tg) == 0:
                     continue
+                key = f"{test}_fa{fa}" + ("_q8kv" if ctk else "")
                 r = subprocess.run([REF_BENCH, "-m", gguf, "-t", "8", "-ngl", "99", "-fa", str(fa), "-p", str(pp),
-                                    "-n", str(tg), "-r", str(args.dropin_reps), "-c", str(max(256, pp + tg))],
+                                    "-n", str(tg), "-r", str(args.dropin_reps), "-c", str(max(256, pp + tg))] +
+                                   (["-ctk", str(ctk)] if ctk else []),
                                    capture_output=True, text=True, timeout=900, env=env)
                 line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
                 if r.returncode != 0 or not line:
-                    out[f"{test}_fa{fa}"] = f"failed rc={r.returncode}: {r.stderr[-300:]}"
+                    out[key] = f"failed rc={r.returncode}: {r.stderr[-300:]}"
                     continue
                 res = json.loads(line[-1])
-                out[f"{test}_fa{fa}_tok_s"] = res["tg_tok_s"] if tg else res["pp_tok_s"]
+                out[f"{key}_tok_s"] = res["tg_tok_s"] if tg else res["pp_tok_s"]
                 st = [json.loads(s.split("stats ", 1)[1]) for s in r.stderr.splitlines() if "[mi355x] stats" in s]
                 if st and tg:
-                    out[f"{test}_fa{fa}_executor"] = st[0]
+                    out[f"{key}_executor"] = st[0]
     except Exception as e:  # noqa: BLE001
         out["error"] = str(e)
     return out

@@ -30,6 +30,7 @@ struct QkvArgs {
     float theta_scale, freq_scale, ext_factor, attn_factor, corr0, corr1;
     unsigned long long * trace;    // debug (MX_TRACE), workgroup 0
     unsigned long long * trace_blk;
+    float * kq8f; float * vq8f;    // q8_0 caches: roped K / V rows staged in f32 (k_kv_store_q8)
 };
 
 __device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i) {
@@ -86,6 +87,7 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     if (p.xs.dbg & 4) { if (m == 0) p.q_out[row] = v; return; }
     if ((p.xs.dbg & 8) && m > 0) return;
     if (m == 2) {
+        if (p.vq8f) { p.vq8f[row] = v; return; }
         const uint16_t h = f2h(v);
         if (p.v_trans) *(uint16_t *) (p.vc + kvrow * p.vc_nb1) = h;
         else *(uint16_t *) (p.vc + kvrow * p.vc_nb1 + row * 2) = h;
@@ -95,8 +97,30 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     const float x0 = odd ? pv : v, x1 = odd ? v : pv;
     const float r = odd ? x0 * sn + x1 * cs : x0 * cs - x1 * sn;
     if (m == 0) p.q_out[row] = r;
+    else if (p.kq8f) p.kq8f[row] = r;
     else *(uint16_t *) (p.kc + kvrow * p.kc_nb1 + row * 2) = f2h(r);
     MX_TRACE(tr, 4);
+}
+
+// q8_0 KV caches (-ctk/-ctv q8_0): the token's roped K row and V row, staged in f32 by
+// k_qkv_rope_store, quantised into their cache rows (SET_ROWS to a q8_0 tensor: from_float
+// = quantize_row_q8_0: quants.cuh quantize_block_q8_0's arithmetic), one lane per element,
+// a 32-lane half-wave per block (a thread per block serialised 32 loads: 12 us)
+__global__ __launch_bounds__(256) void k_kv_store_q8(QkvArgs p, int nk, int nv) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;   // element of K then V (nk, nv % 32 == 0)
+    const bool isk = e < nk;
+    const int i = isk ? e : e - nk;
+    const bool on = e < nk + nv;
+    const float x = on ? (isk ? p.kq8f[i] : p.vq8f[min(i, nv - 1)]) : 0.f;
+    const int lane = threadIdx.x & 63;
+    const float amax = __shfl(dpp_max_group<32>(fabsf(x)), (lane & 32) | 31, 64);
+    const float d = amax / 127.0f;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    if (!on) return;
+    const int64_t kvrow = ((const int64_t *) (isk ? p.kidx : p.vidx))[0];
+    char * blk = (isk ? p.kc + kvrow * p.kc_nb1 : p.vc + kvrow * p.vc_nb1) + 34 * (i >> 5);
+    blk[2 + (i & 31)] = (char) (int8_t) roundf(__fmul_rn(x, id));
+    if ((i & 31) == 0) *(uint16_t *) blk = f2h(d);
 }
 
 // (cos θ·m, sin θ·m) for every dimension pair of one position: rope_yarn
@@ -179,15 +203,18 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     // only the fused consumers may read the intermediate results
     if ((mq->flags | mk->flags | mv->flags | rk->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
     if (uses(mq) != 1 || uses(mk) != 1 || uses(mv) != 1 || uses(rk) != 1) return 0;
-    // KV stores: f16 caches, one token
+    // KV stores: f16 caches, or q8_0 caches (rows quantised by k_kv_store_q8), one token
     const ggml_tensor * kcache = sk, * vcache = sv;
-    if (kcache->type != GGML_TYPE_F16 || vcache->type != GGML_TYPE_F16) return 0;
+    const bool kq8 = kcache->type == GGML_TYPE_Q8_0 && vcache->type == GGML_TYPE_Q8_0;
+    if (!kq8 && (kcache->type != GGML_TYPE_F16 || vcache->type != GGML_TYPE_F16)) return 0;
+    const size_t esz = kq8 ? 34 : 2;
     const ggml_tensor * kix = sk->src[1], * vix = sv->src[1];
-    if (sk->src[0]->ne[0] != wk->ne[1] || sk->src[0]->ne[1] != 1 || kix->ne[0] != 1 || sk->nb[0] != 2) return 0;
+    if (sk->src[0]->ne[0] != wk->ne[1] || sk->src[0]->ne[1] != 1 || kix->ne[0] != 1 || sk->nb[0] != esz) return 0;
     int v_trans;
-    if (sv->src[0]->ne[0] == wv->ne[1] && sv->src[0]->ne[1] == 1 && vix->ne[0] == 1 && sv->nb[0] == 2) v_trans = 0;
-    else if (sv->src[0]->ne[0] == 1 && sv->src[0]->ne[1] == wv->ne[1] && vix->ne[0] == wv->ne[1] && sv->ne[0] == 1) v_trans = 1;
+    if (sv->src[0]->ne[0] == wv->ne[1] && sv->src[0]->ne[1] == 1 && vix->ne[0] == 1 && sv->nb[0] == esz) v_trans = 0;
+    else if (!kq8 && sv->src[0]->ne[0] == 1 && sv->src[0]->ne[1] == wv->ne[1] && vix->ne[0] == wv->ne[1] && sv->ne[0] == 1) v_trans = 1;
     else return 0;
+    if (kq8 && (wk->ne[1] % 32 || wv->ne[1] % 32 || c.scratch->avail() < (size_t) 4 * (wk->ne[1] + wv->ne[1]) + 512)) return 0;
     for (const ggml_tensor * ix : {kix, vix}) if (ix->type != GGML_TYPE_I64) return 0;   // llama's KV indices
 
     QkvArgs p{};
@@ -262,8 +289,15 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
 #undef GEOS
     if (mode != XS_NORM && cfg != 5) return 0;   // the other sources exist in the default geometry only
     const dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
-    MX_KLOG("qkv qta=%d qtv=%d mode=%d cfg=%d K=%d", ta, tv, mode, cfg, p.K);
+    if (kq8) {
+        p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
+        p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
+    }
+    MX_KLOG("qkv qta=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d", ta, tv, mode, cfg, p.K, (int) kq8);
     hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K, mode), c.st, p);
+    if (kq8) {
+        k_kv_store_q8<<<(unsigned) mx_ceil_div(wk->ne[1] + wv->ne[1], 256), 256, 0, c.st>>>(p, (int) wk->ne[1], (int) wv->ne[1]);
+    }
     return last - i + 1;
 }
 

@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$ROOTDIR"
 export GGML_BACKEND_PATH=$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so
 [ "${GRAPHS:-0}" = 0 ] && export GGML_MI355X_DISABLE_GRAPHS=1
 timeout -k 10 ${TMO:-300} rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- \
-  oracle/_ref/ref-llama-bench -m $G -t 8 -ngl 99 -fa ${FA:-1} -p 0 -n 128 -r 1 -c 256 > $OUT.log 2>&1
+  oracle/_ref/ref-llama-bench -m $G -t 8 -ngl 99 -fa ${FA:-1} -p 0 -n 128 -r 1 -c 256 ${CTK:+-ctk $CTK} > $OUT.log 2>&1
 rc=$?
 echo "prof_dropin rc=$rc"; head -30 $OUT/run_kernel_stats.csv
 exit $rc

@@ -42,16 +42,20 @@ def ggufs(tmp_path_factory):
     return out
 
 
-def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False):
+def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False, ctk=None, klog=None):
     tf = tmp_path / "toks.i32"
     of = tmp_path / f"logits_{ngl}_{fa}_{int(incremental)}.f32"
     np.asarray(toks, np.int32).tofile(tf)
     env = dict(os.environ)
     if ngl > 0:
         env["GGML_BACKEND_PATH"] = LIB
+        if klog:
+            env["GGML_MI355X_KLOG"] = str(klog)
     cmd = [REF, "-m", gguf, "-t", "8", "-ngl", str(ngl), "-fa", str(fa), "--logits", str(tf), str(of)]
     if incremental:
         cmd.append("--incremental")
+    if ctk is not None:
+        cmd += ["-ctk", str(ctk)]        # K and V cache type (ggml type id)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     n_vocab = int(r.stdout.strip().splitlines()[-1].split('"n_vocab": ')[1].split(",")[0].rstrip("}"))
@@ -82,6 +86,25 @@ def test_dropin_incremental_decode(ggufs, tmp_path, shape, recipe, fa):
     gpu, log = run_ref(tmp_path, ggufs[(shape, recipe)], toks, 99, fa, incremental=True)
     assert "MI355X" in log
     assert nmse(gpu, cpu) < TOL
+
+
+@pytest.mark.parametrize("incremental", [False, True])
+def test_dropin_q8_0_kv_cache(ggufs, tmp_path, incremental):
+    """-ctk q8_0 -ctv q8_0 (the fork's preferred setting): SET_ROWS into q8_0 caches and
+    FLASH_ATTN_EXT on them, against the reference CPU backend with the same caches; the
+    decode steps must take the fused QKV (q8_0 rows) and the q8_0 decode attention kernel"""
+    _need_ref()
+    toks = np.random.default_rng(9).integers(0, 1000, 24 if incremental else 40)
+    g = ggufs[("small", "q4_k_m")]
+    klog = tmp_path / "klog.txt"
+    cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental, ctk=8)
+    gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, ctk=8, klog=klog)
+    assert "MI355X" in log
+    assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+    if incremental:
+        kl = klog.read_text()
+        assert "kq8=1" in kl and any(ln.startswith("qkv ") and "kq8=1" in ln for ln in kl.splitlines()), kl[-2000:]
+        assert any(ln.startswith("fattn_dec2") and "kq8=1" in ln for ln in kl.splitlines()), kl[-2000:]
 
 
 @pytest.mark.parametrize("shape,recipe", [("small", "q4_k_m"), ("tiny_moe", "q4_k_m")])
