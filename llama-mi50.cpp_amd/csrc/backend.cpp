@@ -29,6 +29,61 @@ static const uint8_t kGuid[16] = {0x6d, 0x69, 0x33, 0x35, 0x35, 0x78, 0x2d, 0x67
 static Device * dev_ctx(ggml_backend_dev_t d) { return (Device *) d->context; }
 
 // ---------------------------------------------------------------------------
+// staged small writes. libllama writes each graph input through the buffer interface
+// (set_input: token ids, positions, KQ mask, KV-cache row indices, output ids —
+// src/llama-graph.cpp), about six per decoded token; a synchronous hipMemcpy each left
+// the GPU idle between tokens. Writes up to 64 KB are copied into a pinned ring and
+// sent asynchronously on the device's compute stream (the stream of the first backend
+// created on it), so they are ordered before that backend's next graph; `ev` marks the
+// latest one for every other path that touches device memory (buffer reads, memsets,
+// copies, another stream's graph), which waits for it first.
+// ---------------------------------------------------------------------------
+struct Staging {
+    std::mutex mu;
+    Stream * s = nullptr;          // compute stream the writes go to (null: synchronous writes)
+    char * host = nullptr;         // pinned ring
+    size_t cap = 0, off = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    uint64_t n = 0;                // staged writes (GGML_MI355X_STATS)
+};
+static Staging g_stage[MX_MAX_DEVICES];
+static constexpr size_t kStageMax = 64 << 10, kStageRing = 4 << 20;
+
+static bool stage_write(int dev, void * dst, const void * data, size_t size) {
+    if (dev < 0 || dev >= MX_MAX_DEVICES || size > kStageMax) return false;
+    Staging & st = g_stage[dev];
+    std::lock_guard<std::mutex> lk(st.mu);
+    if (!st.s) return false;
+    if (!st.host) {
+        if (hipHostMalloc((void **) &st.host, kStageRing, hipHostMallocDefault) != hipSuccess) { (void) hipGetLastError(); st.host = nullptr; return false; }
+        HIP_CHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
+        st.cap = kStageRing;
+    }
+    size_t a = (st.off + 255) & ~(size_t) 255;
+    if (a + size > st.cap) {       // wrap: every earlier staged copy has to be done reading
+        HIP_CHECK(hipStreamSynchronize(st.s->stream));
+        a = 0;
+    }
+    memcpy(st.host + a, data, size);
+    HIP_CHECK(hipMemcpyAsync(dst, st.host + a, size, hipMemcpyHostToDevice, st.s->stream));
+    HIP_CHECK(hipEventRecord(st.ev, st.s->stream));
+    st.off = a + size;
+    st.pending = true;
+    st.n++;
+    return true;
+}
+
+// make `stream` wait for the device's staged writes (no-op when none or on their stream)
+void staged_writes_wait(int dev, hipStream_t stream) {
+    if (dev < 0 || dev >= MX_MAX_DEVICES) return;
+    Staging & st = g_stage[dev];
+    std::lock_guard<std::mutex> lk(st.mu);
+    if (!st.pending || (st.s && st.s->stream == stream)) return;
+    HIP_CHECK(hipStreamWaitEvent(stream, st.ev, 0));
+}
+
+// ---------------------------------------------------------------------------
 // device buffers
 // ---------------------------------------------------------------------------
 static void buf_free(ggml_backend_buffer_t b) {
@@ -42,18 +97,22 @@ static ggml_status buf_init_tensor(ggml_backend_buffer_t, ggml_tensor *) { retur
 static void buf_memset(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size_t off, size_t size) {
     BufferCtx * c = (BufferCtx *) b->context;
     HIP_CHECK(hipSetDevice(c->device));
+    staged_writes_wait(c->device, hipStreamPerThread);
     HIP_CHECK(hipMemsetAsync((char *) t->data + off, v, size, hipStreamPerThread));
     HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
 static void buf_set(ggml_backend_buffer_t b, ggml_tensor * t, const void * data, size_t off, size_t size) {
     BufferCtx * c = (BufferCtx *) b->context;
     HIP_CHECK(hipSetDevice(c->device));
+    if (stage_write(c->device, (char *) t->data + off, data, size)) return;
+    staged_writes_wait(c->device, hipStreamPerThread);
     HIP_CHECK(hipMemcpyAsync((char *) t->data + off, data, size, hipMemcpyHostToDevice, hipStreamPerThread));
     HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
 static void buf_get(ggml_backend_buffer_t b, const ggml_tensor * t, void * data, size_t off, size_t size) {
     BufferCtx * c = (BufferCtx *) b->context;
     HIP_CHECK(hipSetDevice(c->device));
+    staged_writes_wait(c->device, hipStreamPerThread);
     HIP_CHECK(hipMemcpyAsync(data, (const char *) t->data + off, size, hipMemcpyDeviceToHost, hipStreamPerThread));
     HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
@@ -64,6 +123,8 @@ static bool buf_cpy(ggml_backend_buffer_t b, const ggml_tensor * src, ggml_tenso
     BufferCtx * dc = (BufferCtx *) b->context;
     const size_t n = mx_nbytes(src);
     HIP_CHECK(hipSetDevice(dc->device));
+    staged_writes_wait(dc->device, hipStreamPerThread);
+    staged_writes_wait(sc->device, hipStreamPerThread);
     if (sc->device == dc->device) {
         HIP_CHECK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, hipStreamPerThread));
     } else {
@@ -75,6 +136,7 @@ static bool buf_cpy(ggml_backend_buffer_t b, const ggml_tensor * src, ggml_tenso
 static void buf_clear(ggml_backend_buffer_t b, uint8_t v) {
     BufferCtx * c = (BufferCtx *) b->context;
     HIP_CHECK(hipSetDevice(c->device));
+    staged_writes_wait(c->device, hipStreamPerThread);
     HIP_CHECK(hipMemsetAsync(c->base, v, c->size, hipStreamPerThread));
     HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
@@ -160,16 +222,22 @@ static void be_free(ggml_backend_t b) {
     Stream * s = stream_of(b);
     hipSetDevice(s->device);
     hipStreamSynchronize(s->stream);
+    if (s->device >= 0 && s->device < MX_MAX_DEVICES) {   // later small writes go synchronous again
+        Staging & st = g_stage[s->device];
+        std::lock_guard<std::mutex> lk(st.mu);
+        if (st.s == s) { st.s = nullptr; st.pending = false; }
+    }
     // GGML_MI355X_STATS=1: executor counters of this backend on stderr when libllama frees
     // it (drop-in runs: shows the fusions fired on the reference's own node order)
     if (getenv("GGML_MI355X_STATS"))
         fprintf(stderr, "[mi355x] stats {\"backend\": \"%s\", \"graph_compute\": %llu, \"graph_replay\": %llu, "
                 "\"nodes_run\": %llu, \"nodes_fused\": %llu, \"host_us\": {\"graph_compute\": %.0f, \"set_async\": %.0f, "
                 "\"get_async\": %.0f, \"synchronize\": %.0f}, \"n_set\": %llu, \"bytes_set\": %llu, \"n_get\": %llu, "
-                "\"bytes_get\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
+                "\"bytes_get\": %llu, \"n_staged\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
                 (unsigned long long) s->n_graph_replay, (unsigned long long) s->n_nodes_run, (unsigned long long) s->n_fused,
                 s->us_compute, s->us_set, s->us_get, s->us_sync, (unsigned long long) s->n_set, (unsigned long long) s->b_set,
-                (unsigned long long) s->n_get, (unsigned long long) s->b_get);
+                (unsigned long long) s->n_get, (unsigned long long) s->b_get,
+                (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n : 0));
     if (const char * kp = getenv("GGML_MI355X_KLOG")) klog_dump(kp);
     if (s->gcache.exec) hipGraphExecDestroy(s->gcache.exec);
     if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
@@ -271,6 +339,11 @@ static ggml_backend_t make_backend(Device * d) {
     s->backend.iface = kBackendIface;
     s->backend.device = &d->dev;
     s->backend.context = s;
+    if (d->id >= 0 && d->id < MX_MAX_DEVICES && !env_flag("GGML_MI355X_SYNC_SET")) {
+        Staging & st = g_stage[d->id];
+        std::lock_guard<std::mutex> lk(st.mu);
+        if (!st.s) st.s = s;
+    }
     return &s->backend;
 }
 

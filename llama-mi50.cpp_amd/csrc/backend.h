@@ -9,6 +9,10 @@
 
 namespace mx {
 
+constexpr int MX_MAX_DEVICES = 16;
+// order `stream` after the device's staged small buffer writes (backend.cpp)
+void staged_writes_wait(int dev, hipStream_t stream);
+
 struct Device {
     int id = 0;
     std::string name, description, pci_bus_id;

@@ -420,6 +420,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
 
 void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     HIP_CHECK(hipSetDevice(s->device));
+    staged_writes_wait(s->device, s->stream);
     s->n_graph_compute++;
     if (s->abort_cb && s->abort_cb(s->abort_data)) { *status = GGML_STATUS_ABORTED; return; }
 
