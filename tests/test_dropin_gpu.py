@@ -121,3 +121,16 @@ def test_runner_matches_reference_cpu(pkg, backend, ggufs, tmp_path, shape, reci
     s.free(); m.free()
     assert nmse(pre, cpu) < TOL
     assert nmse(inc, cpu) < TOL
+
+
+def test_layer_split_handoff_cpy_tensor_async(tmp_path):
+    """The layer-split hand-off as libllama's scheduler performs it, through the reference's
+    own ggml-backend (oracle/cpy_async_probe.cpp over libggml-ref.so): two MI355X backends,
+    ggml_backend_tensor_copy_async into the second one's buffer, then a graph on it that
+    reads the copy without a host synchronisation (be_cpy_async's event orders them)."""
+    probe = os.path.join(ROOT, "oracle", "_ref", "cpy-async-probe")
+    if not os.path.exists(probe):
+        pytest.skip("oracle/_ref/cpy-async-probe not built")
+    r = subprocess.run([probe, LIB], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert '"mismatches": 0' in r.stdout and "MI355X" in r.stdout, r.stdout
