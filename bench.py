@@ -122,7 +122,9 @@ def roofline_glu(pkg, be, model, iters=256):
     ctx.free()
     achieved = bytes_per_launch / (us * 1e-6) / 1e9
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01", "pmc_glu.json")   # scripts/pmc_roofline.sh
+    pmc = os.path.join(ROOT, "profiles", "r02", "pmc_glu.json")   # scripts/pmc_roofline.sh
+    if not os.path.exists(pmc):
+        pmc = os.path.join(ROOT, "profiles", "r01", "pmc_glu.json")
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libggml-mi355x.so")
+LIB_PATH = os.environ.get("GGML_MI355X_LIB") or os.path.join(HERE, "lib", "libggml-mi355x.so")   # override: A/B builds
 
 # ggml_type ids (ggml.h:389-431)
 GGML_TYPE = {"f32": 0, "f16": 1, "q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7, "q8_0": 8, "q8_1": 9,

@@ -192,6 +192,11 @@ static bool try_defer_norm(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
         for (int k = 0; k < GGML_MAX_SRC; ++k) {
             if (m->src[k] != mul) continue;
             if (m->op != GGML_OP_MUL_MAT || k != 1 || !gemv2_ok(m->src[0], mul, m)) return false;
+            // the lm_head (128256 rows = 8016 workgroups): each workgroup would stage 32 KB
+            // (x and the norm weight) and normalise / quantise 4096 values again; one
+            // RMS_NORM+MUL+q8 launch and q8 staging measured 76.5 + 5.7 us against 86.8
+            // (decode profiles, r02). g_tune[22] = 1 keeps the deferral (A/B)
+            if (m->src[0]->ne[1] > 65536 && g_tune[22] != 1) return false;
             ++found;
         }
     }

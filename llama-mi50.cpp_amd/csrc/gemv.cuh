@@ -79,6 +79,10 @@ __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
 // instead of under their latency. Each read and its lgkmcnt(0) wait are one asm
 // statement (outputs exist only once the data has landed); writes are waited for by the
 // next lds_barrier.
+#ifndef MX_PROLOGUE_ASM
+#define MX_PROLOGUE_ASM 1
+#endif
+#if MX_PROLOGUE_ASM
 __device__ __forceinline__ uint32_t lds_off(const void * p) {
     return (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) p;
 }
@@ -91,6 +95,51 @@ __device__ __forceinline__ void lds_rd16(const float * p, float (&d)[16]) {
                  : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(e) : "v"(lds_off(p)));
 #pragma unroll
     for (int j = 0; j < 4; ++j) { d[j] = a[j]; d[4 + j] = b[j]; d[8 + j] = c[j]; d[12 + j] = e[j]; }
+}
+// x and the norm weight of one 16-value half in one round trip
+__device__ __forceinline__ void lds_rd16x2(const float * p, const float * q, float (&d)[16], float (&e)[16]) {
+    v4f_t a, b, c, f, g, h, i, j;
+    asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:16\n\tds_read_b128 %2, %8 offset:32\n\t"
+                 "ds_read_b128 %3, %8 offset:48\n\tds_read_b128 %4, %9\n\tds_read_b128 %5, %9 offset:16\n\t"
+                 "ds_read_b128 %6, %9 offset:32\n\tds_read_b128 %7, %9 offset:48\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(f), "=&v"(g), "=&v"(h), "=&v"(i), "=&v"(j)
+                 : "v"(lds_off(p)), "v"(lds_off(q)));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        d[k] = a[k]; d[4 + k] = b[k]; d[8 + k] = c[k]; d[12 + k] = f[k];
+        e[k] = g[k]; e[4 + k] = h[k]; e[8 + k] = i[k]; e[12 + k] = j[k];
+    }
+}
+// sum of N (4, 8 or 16) consecutive floats, one round trip
+template <int N>
+__device__ __forceinline__ float lds_sum(const float * p) {
+    static_assert(N == 4 || N == 8 || N == 16, "lds_sum");
+    v4f_t a, b, c, d;
+    if constexpr (N == 4) {
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(a) : "v"(lds_off(p)));
+        return (a[0] + a[1]) + (a[2] + a[3]);
+    } else if constexpr (N == 8) {
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)" : "=&v"(a), "=&v"(b) : "v"(lds_off(p)));
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += a[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += b[k];
+        return s;
+    } else {
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\tds_read_b128 %2, %4 offset:32\n\t"
+                     "ds_read_b128 %3, %4 offset:48\n\ts_waitcnt lgkmcnt(0)" : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(lds_off(p)));
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += a[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += b[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += c[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += d[k];
+        return s;
+    }
 }
 __device__ __forceinline__ float4 lds_rd4(const float * p) {
     v4f_t a;
@@ -109,6 +158,20 @@ __device__ __forceinline__ void lds_wr4i(void * p, int4 v) {
     v4i_t w = {v.x, v.y, v.z, v.w};
     asm volatile("ds_write_b128 %0, %1" :: "v"(lds_off(p)), "v"(w) : "memory");
 }
+
+#else   // A/B build (EXTRA=-DMX_PROLOGUE_ASM=0): ordinary LDS accesses
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_rd16(const float * p, float (&d)[16]) { for (int j = 0; j < 16; ++j) d[j] = p[j]; }
+__device__ __forceinline__ void lds_rd16x2(const float * p, const float * q, float (&d)[16], float (&e)[16]) {
+    for (int j = 0; j < 16; ++j) { d[j] = p[j]; e[j] = q[j]; }
+}
+template <int N> __device__ __forceinline__ float lds_sum(const float * p) { float s = 0.f; for (int j = 0; j < N; ++j) s += p[j]; return s; }
+__device__ __forceinline__ float4 lds_rd4(const float * p) { return *(const float4 *) p; }
+__device__ __forceinline__ float lds_rd1(const float * p) { return *p; }
+__device__ __forceinline__ void lds_wr1(float * p, float v) { *p = v; }
+__device__ __forceinline__ void lds_wr4i(void * p, int4 v) { *(int4 *) p = v; }
+#endif
 
 // quantise 16 values held by this thread; the partner thread (tid ^ 1) holds the other
 // half of the 32-block (k_quantize_act semantics up to the rounding noted below).
@@ -239,22 +302,43 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
         if (xs.drain) wait_vmcnt<0>();       // A/B (g_tune[14]): prologue after the whole stream
         else wait_vmcnt<NW>();
         lds_barrier();                        // staged x (and norm weight) visible
+        // K <= 16 NT (every SwiGLU / lm_head grid): each thread reads its one 16-value half
+        // (and norm weight) once, in one round trip, and keeps it for Σx² and quantisation
+        const bool one = nhg <= NT;
+        float v1[16], w1[16];
+        if (one && t < nhg) {
+            if constexpr (MODE == XS_NORM_LDS) lds_rd16x2(xf + 16 * t, xf + K + 16 * t, v1, w1);
+            else lds_rd16(xf + 16 * t, v1);
+        }
         float scale = 1.0f;
         if constexpr (MODE == XS_NORM_LDS) {
             float ss = 0.f;
-            for (int i = 4 * t; i < K; i += 4 * NT) {
-                const float4 f = lds_rd4(xf + i);
-                ss += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+            if (one) {
+                if (t < nhg) {
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) ss += v1[j] * v1[j];
+                }
+            } else {
+                for (int i = 4 * t; i < K; i += 4 * NT) {
+                    const float4 f = lds_rd4(xf + i);
+                    ss += f.x * f.x + f.y * f.y + f.z * f.z + f.w * f.w;
+                }
             }
             ss = wave_sum(ss);
             if ((t & 63) == 0) lds_wr1(red + (t >> 6), ss);
             lds_barrier();
-            ss = 0.f;
-#pragma unroll
-            for (int wv = 0; wv < NT / 64; ++wv) ss += lds_rd1(red + wv);
+            ss = lds_sum<NT / 64>(red);
             scale = __builtin_amdgcn_rsqf(ss / (float) K + xs.eps);
         }
-        for (int hg = t; hg < nhg; hg += NT) {   // nhg is even: partner lanes stay paired
+        if (one) {
+            if (t < nhg) {                           // nhg is even: partner lanes stay paired
+                if constexpr (MODE == XS_NORM_LDS) {
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) v1[j] = (v1[j] * scale) * w1[j];
+                }
+                q8_half<true>(v1, t, a);
+            }
+        } else for (int hg = t; hg < nhg; hg += NT) {   // nhg is even: partner lanes stay paired
             float v2[16];
             lds_rd16(xf + 16 * hg, v2);
             if constexpr (MODE == XS_NORM_LDS) {
