@@ -371,8 +371,21 @@ static void dv_props(ggml_backend_dev_t d, ggml_backend_dev_props * p) {
 static ggml_backend_t dv_init(ggml_backend_dev_t d, const char *) { return make_backend(dev_ctx(d)); }
 static ggml_backend_buffer_type_t dv_buft(ggml_backend_dev_t d) { return &dev_ctx(d)->buft; }
 static ggml_backend_buffer_type_t dv_host_buft(ggml_backend_dev_t d) { return &dev_ctx(d)->host_buft; }
-static bool dv_supports_op(ggml_backend_dev_t, const ggml_tensor * op) { return supports_op(op); }
+// Row-split weights (split.cpp) serve one op only: MUL_MAT's src0, a 2D matrix, run from
+// the split's main device with an f32 activation (the reference's CUDA rule,
+// ggml_backend_cuda_device_supports_op).
+static bool dv_supports_op(ggml_backend_dev_t d, const ggml_tensor * op) {
+    for (int i = 0; i < GGML_MAX_SRC; ++i) {
+        const ggml_tensor * s = op->src[i];
+        if (!s || !s->buffer || !buft_is_split(s->buffer->buft)) continue;
+        if (op->op != GGML_OP_MUL_MAT || i != 0 || s->ne[2] != 1 || s->ne[3] != 1) return false;
+        if (split_main_device(s->buffer->buft) != dev_ctx(d)->index) return false;
+        if (op->src[1]->type != GGML_TYPE_F32 || op->type != GGML_TYPE_F32) return false;
+    }
+    return supports_op(op);
+}
 static bool dv_supports_buft(ggml_backend_dev_t d, ggml_backend_buffer_type_t t) {
+    if (buft_is_split(t)) return split_main_device(t) == dev_ctx(d)->index;
     return t->iface.alloc_buffer == buft_alloc && t->device == d;
 }
 static int64_t op_batch(const ggml_tensor * op) {
@@ -425,27 +438,47 @@ static void rg_set_abort(ggml_backend_t b, ggml_abort_callback cb, void * data) 
 static void * rg_proc(ggml_backend_reg_t, const char * name) {
     if (strcmp(name, "ggml_backend_get_features") == 0) return (void *) rg_features;
     if (strcmp(name, "ggml_backend_set_abort_callback") == 0) return (void *) rg_set_abort;
+    if (strcmp(name, "ggml_backend_split_buffer_type") == 0) return (void *) split_buffer_type;
     return nullptr;
 }
 
 static const ggml_backend_reg_i kRegIface = { rg_name, rg_count, rg_get, rg_proc };
 
+// logical devices for the row split (split.cpp)
+int mx_dev_count() { return (int) g_devices.size(); }
+int mx_dev_hip(int logical) { return g_devices[logical]->id; }
+ggml_backend_dev_t mx_dev_handle(int logical) { return &g_devices[logical]->dev; }
+// one auxiliary stream per logical device runs that device's row slices
+Stream * mx_aux_stream(int logical) {
+    static std::mutex mu;
+    static Stream * aux[MX_MAX_DEVICES] = {};
+    std::lock_guard<std::mutex> lk(mu);
+    if (!aux[logical]) aux[logical] = stream_of(make_backend(g_devices[logical].get()));
+    return aux[logical];
+}
+
 void klog_env_init();
 static void init_registry() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) { (void) hipGetLastError(); n = 0; }
-    for (int i = 0; i < n; ++i) {
+    // GGML_MI355X_VIRTUAL_DEVICES=V (tests): V logical devices over the n GPUs, round robin
+    int nl = n;
+    if (const char * v = getenv("GGML_MI355X_VIRTUAL_DEVICES")) if (n > 0 && atoi(v) > 0) nl = std::min(atoi(v), MX_MAX_DEVICES);
+    for (int li = 0; li < nl; ++li) {
+        const int i = li % std::max(n, 1);
         hipDeviceProp_t p;
         if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
         auto d = std::make_unique<Device>();
         d->id = i;
-        d->name = "MI355X" + std::to_string(i);
+        d->index = (int) g_devices.size();
+        d->name = "MI355X" + std::to_string(d->index);
         d->description = std::string(p.name[0] ? p.name : "AMD Instinct MI355X") + " (" + p.gcnArchName + ")";
         d->total_mem = p.totalGlobalMem;
         d->n_cu = p.multiProcessorCount;
         char pci[32] = {0};
         if (hipDeviceGetPCIBusId(pci, sizeof(pci), i) == hipSuccess) d->pci_bus_id = pci;
         for (auto & ch : d->pci_bus_id) ch = (char) tolower(ch);
+        if (li >= n) d->pci_bus_id += "-v" + std::to_string(li);   // libllama skips devices with equal ids
         d->dev = ggml_backend_device{kDevIface, &g_reg, d.get()};
         d->buft = ggml_backend_buffer_type{kBuftIface, &d->dev, d.get()};
         d->host_buft = ggml_backend_buffer_type{kHostBuftIface, &d->dev, d.get()};

@@ -10,11 +10,17 @@
 namespace mx {
 
 constexpr int MX_MAX_DEVICES = 16;
+// row split (split.cpp)
+bool buft_is_split(ggml_backend_buffer_type_t t);
+int split_main_device(ggml_backend_buffer_type_t t);
+bool tensor_is_split(const ggml_tensor * t);
+ggml_backend_buffer_type_t split_buffer_type(int main_device, const float * tensor_split);
 // order `stream` after the device's staged small buffer writes (backend.cpp)
 void staged_writes_wait(int dev, hipStream_t stream);
 
 struct Device {
-    int id = 0;
+    int id = 0;                      // HIP device (GGML_MI355X_VIRTUAL_DEVICES may map several here)
+    int index = 0;                   // logical device index in the registry
     std::string name, description, pci_bus_id;
     size_t total_mem = 0;
     int n_cu = 0;
@@ -156,6 +162,7 @@ void op_soft_max(OpCtx & c, ggml_tensor * dst);
 void op_sum_rows(OpCtx & c, ggml_tensor * dst);
 void op_argsort(OpCtx & c, ggml_tensor * dst);
 void op_mul_mat(OpCtx & c, ggml_tensor * dst);
+void op_mul_mat_split(OpCtx & c, ggml_tensor * dst);
 void op_mul_mat_id(OpCtx & c, ggml_tensor * dst);
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst);
 

@@ -324,7 +324,7 @@ static void run_node(OpCtx & c, ggml_tensor * n) {
         case GGML_OP_SOFT_MAX:   op_soft_max(c, n); break;
         case GGML_OP_SUM_ROWS:   op_sum_rows(c, n); break;
         case GGML_OP_ARGSORT:    op_argsort(c, n); break;
-        case GGML_OP_MUL_MAT:    op_mul_mat(c, n); break;
+        case GGML_OP_MUL_MAT:    if (tensor_is_split(n->src[0])) op_mul_mat_split(c, n); else op_mul_mat(c, n); break;
         case GGML_OP_MUL_MAT_ID: op_mul_mat_id(c, n); break;
         case GGML_OP_FLASH_ATTN_EXT: op_flash_attn_ext(c, n); break;
         default: MX_ABORT("unsupported op %d on node %s", (int) n->op, n->name);
@@ -423,22 +423,9 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
     HIP_CHECK(hipGetLastError());
 }
 
-void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
-    HIP_CHECK(hipSetDevice(s->device));
-    staged_writes_wait(s->device, s->stream);
-    s->n_graph_compute++;
-    if (s->abort_cb && s->abort_cb(s->abort_data)) { *status = GGML_STATUS_ABORTED; return; }
-
-    size_t need = 0, slot = 0, f16need = 0;
-    for (int i = 0; i < g->n_nodes; ++i) {
-        need = std::max(need, scratch_bytes(g->nodes[i]));
-        if (g->nodes[i]->op == GGML_OP_MUL_MAT) f16need = std::max(f16need, mmq_act_bytes(g->nodes[i]));
-        if (g->nodes[i]->op == GGML_OP_MUL_MAT && mmvq_small_batch_ok(g->nodes[i])) slot = std::max(slot, act_slot_bytes(g->nodes[i]->src[1]));
-        if (g->nodes[i]->op == GGML_OP_MUL && mx_nrows(g->nodes[i]) <= 8) slot = std::max(slot, act_slot_bytes(g->nodes[i]));
-        // MoE decode: the q8 copy of the gate/up SwiGLU output (= this node's shape) and of src1
-        if (g->nodes[i]->op == GGML_OP_MUL_MAT_ID && g->nodes[i]->src[2]->ne[1] <= 8)
-            slot = std::max({slot, act_slot_bytes(g->nodes[i]), act_slot_bytes(g->nodes[i]->src[1])});
-    }
+// grow a stream's scratch arena, activation ring and f16 slots to the given sizes
+// (never inside a capture)
+static void stream_reserve(Stream * s, size_t need, size_t slot, size_t f16need) {
     if (slot > s->act_slot) {
         HIP_CHECK(hipStreamSynchronize(s->stream));
         if (s->act.base) HIP_CHECK(hipFree(s->act.base));
@@ -463,7 +450,44 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         s->scratch.cap = cap;
         s->gcache.key.clear();  // captured kernels point at the old arena
     }
+}
 
+// the buffers one MUL_MAT node needs on stream s (the row split's per-device slices)
+void stream_reserve_node(Stream * s, const ggml_tensor * n) {
+    size_t slot = 0;
+    if (mmvq_small_batch_ok(n)) slot = act_slot_bytes(n->src[1]);
+    stream_reserve(s, scratch_bytes(n), slot, mmq_act_bytes(n));
+}
+
+void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
+    HIP_CHECK(hipSetDevice(s->device));
+    staged_writes_wait(s->device, s->stream);
+    s->n_graph_compute++;
+    if (s->abort_cb && s->abort_cb(s->abort_data)) { *status = GGML_STATUS_ABORTED; return; }
+
+    size_t need = 0, slot = 0, f16need = 0;
+    for (int i = 0; i < g->n_nodes; ++i) {
+        need = std::max(need, scratch_bytes(g->nodes[i]));
+        if (g->nodes[i]->op == GGML_OP_MUL_MAT) f16need = std::max(f16need, mmq_act_bytes(g->nodes[i]));
+        if (g->nodes[i]->op == GGML_OP_MUL_MAT && mmvq_small_batch_ok(g->nodes[i])) slot = std::max(slot, act_slot_bytes(g->nodes[i]->src[1]));
+        if (g->nodes[i]->op == GGML_OP_MUL && mx_nrows(g->nodes[i]) <= 8) slot = std::max(slot, act_slot_bytes(g->nodes[i]));
+        // MoE decode: the q8 copy of the gate/up SwiGLU output (= this node's shape) and of src1
+        if (g->nodes[i]->op == GGML_OP_MUL_MAT_ID && g->nodes[i]->src[2]->ne[1] <= 8)
+            slot = std::max({slot, act_slot_bytes(g->nodes[i]), act_slot_bytes(g->nodes[i]->src[1])});
+    }
+    stream_reserve(s, need, slot, f16need);
+
+    // row-split weights (split.cpp): every device works on the node, which no single-stream
+    // capture can hold, and the fusions assume one device — eager and unfused
+    bool split = false;
+    for (int i = 0; i < g->n_nodes && !split; ++i) split = g->nodes[i]->op == GGML_OP_MUL_MAT && tensor_is_split(g->nodes[i]->src[0]);
+    if (split) {
+        const bool f = s->use_fusion;
+        s->use_fusion = false;
+        run_nodes(s, g);
+        s->use_fusion = f;
+        return;
+    }
     if (!s->use_graphs || g_sync_debug) { run_nodes(s, g); return; }
 
     GraphCache & gc = s->gcache;

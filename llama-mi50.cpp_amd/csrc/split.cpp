@@ -1,0 +1,237 @@
+// split.cpp — row-split tensor parallelism (`llama -sm row`): the weight rows of every 2D
+// matrix are partitioned over the devices, each device multiplies its rows with the
+// activation, the row slices of the result are gathered on the main device.
+//
+// Reference behaviour replaced (not ported): llama asks the backend registry for the
+// optional proc "ggml_backend_split_buffer_type" (src/llama-model.cpp:391-409) and puts
+// the matrices in that buffer type when the device's supports_op accepts the MUL_MAT;
+// the CUDA backend's split buffer (ggml-cuda.cu:778-1067) keeps per-device row slices in
+// tensor->extra, and ggml_cuda_op_mul_mat (:1452-1770) broadcasts src1, runs every
+// device's slice and copies the partial dst back (:1432).
+//
+// MI355X form: one process drives all devices (as the reference does for -sm row); each
+// device runs its slice with the same kernels as an unsplit MUL_MAT (decode GEMV, prefill
+// GEMM) on an auxiliary stream of its own; src1 goes to the devices by peer copy over
+// xGMI (peer access is enabled between all pairs at registry init), the slices come back
+// by 2D peer copies, events order everything against the main stream. Split graphs run
+// eagerly and unfused (a capture cannot span devices).
+// GGML_MI355X_VIRTUAL_DEVICES=N exposes the GPUs N times over (tests: a row split over
+// two logical devices of one MI355X exercises every path but the xGMI link itself).
+#include "backend.h"
+
+#include <array>
+#include <map>
+#include <mutex>
+
+namespace mx {
+
+int mx_dev_count();
+int mx_dev_hip(int logical);
+ggml_backend_dev_t mx_dev_handle(int logical);
+Stream * mx_aux_stream(int logical);
+void stream_reserve_node(Stream * s, const ggml_tensor * n);
+
+constexpr int64_t SPLIT_ROUND = 256;   // rows per slice are a multiple (GEMM row tiles, q8 groups)
+
+struct SplitBuftCtx {
+    int main = 0;
+    std::array<float, MX_MAX_DEVICES> split{};   // cumulative start fractions
+    std::string name;
+};
+struct SplitExtra {
+    void * data[MX_MAX_DEVICES] = {};
+    int64_t lo[MX_MAX_DEVICES] = {}, hi[MX_MAX_DEVICES] = {};
+};
+struct SplitBufCtx {
+    const SplitBuftCtx * t = nullptr;
+    std::vector<SplitExtra *> extras;
+};
+
+static void row_split(const SplitBuftCtx * c, int64_t nrows, int d, int64_t * lo, int64_t * hi) {
+    const int n = mx_dev_count();
+    auto at = [&](int i) { int64_t r = (int64_t) ((double) nrows * c->split[i]); return r - r % SPLIT_ROUND; };
+    *lo = d == 0 ? 0 : at(d);
+    *hi = d == n - 1 ? nrows : at(d + 1);
+    if (*hi < *lo) *hi = *lo;
+}
+
+static void free_extra(SplitExtra * e) {
+    for (int d = 0; d < MX_MAX_DEVICES; ++d)
+        if (e->data[d]) { hipSetDevice(mx_dev_hip(d)); hipFree(e->data[d]); }
+    delete e;
+}
+
+// ---- buffer
+static void sbuf_free(ggml_backend_buffer_t b) {
+    SplitBufCtx * c = (SplitBufCtx *) b->context;
+    for (SplitExtra * e : c->extras) free_extra(e);
+    delete c;
+}
+// tensors of a split buffer have no single address: data points into a dummy range
+static void * sbuf_base(ggml_backend_buffer_t) { return (void *) 0x1000; }
+static ggml_status sbuf_init_tensor(ggml_backend_buffer_t b, ggml_tensor * t) {
+    if (t->view_src) return GGML_STATUS_SUCCESS;
+    SplitBufCtx * c = (SplitBufCtx *) b->context;
+    MX_ASSERT(mx_is_contiguous(t) && t->ne[2] == 1 && t->ne[3] == 1);
+    SplitExtra * e = new SplitExtra();
+    const size_t rs = mx_row_size(t->type, t->ne[0]);
+    for (int d = 0; d < mx_dev_count(); ++d) {
+        row_split(c->t, t->ne[1], d, &e->lo[d], &e->hi[d]);
+        const int64_t n = e->hi[d] - e->lo[d];
+        if (n == 0) continue;
+        HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
+        // + 16 bytes: the kernels' vector loads may run past the last block of the last row
+        HIP_CHECK(hipMalloc(&e->data[d], (size_t) n * rs + 256));
+        HIP_CHECK(hipMemset(e->data[d], 0, (size_t) n * rs + 256));
+    }
+    t->extra = e;
+    c->extras.push_back(e);
+    return GGML_STATUS_SUCCESS;
+}
+static void sbuf_set(ggml_backend_buffer_t, ggml_tensor * t, const void * data, size_t off, size_t size) {
+    MX_ASSERT(off == 0 && size == mx_nbytes(t) && t->extra);   // whole tensors, as the reference
+    const SplitExtra * e = (const SplitExtra *) t->extra;
+    const size_t rs = mx_row_size(t->type, t->ne[0]);
+    for (int d = 0; d < mx_dev_count(); ++d) {
+        const int64_t n = e->hi[d] - e->lo[d];
+        if (n == 0) continue;
+        HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
+        HIP_CHECK(hipMemcpy(e->data[d], (const char *) data + e->lo[d] * rs, n * rs, hipMemcpyHostToDevice));
+    }
+}
+static void sbuf_get(ggml_backend_buffer_t, const ggml_tensor * t, void * data, size_t off, size_t size) {
+    MX_ASSERT(off == 0 && size == mx_nbytes(t) && t->extra);
+    const SplitExtra * e = (const SplitExtra *) t->extra;
+    const size_t rs = mx_row_size(t->type, t->ne[0]);
+    for (int d = 0; d < mx_dev_count(); ++d) {
+        const int64_t n = e->hi[d] - e->lo[d];
+        if (n == 0) continue;
+        HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
+        HIP_CHECK(hipMemcpy((char *) data + e->lo[d] * rs, e->data[d], n * rs, hipMemcpyDeviceToHost));
+    }
+}
+static void sbuf_clear(ggml_backend_buffer_t b, uint8_t v) {
+    SplitBufCtx * c = (SplitBufCtx *) b->context;
+    (void) c; (void) v;   // weights are always set whole; nothing reads a cleared split buffer
+}
+static const ggml_backend_buffer_i kSplitBufIface = {
+    sbuf_free, sbuf_base, sbuf_init_tensor, nullptr, sbuf_set, sbuf_get, nullptr, sbuf_clear, nullptr,
+};
+
+// ---- buffer type
+static const char * sbuft_name(ggml_backend_buffer_type_t t) { return ((SplitBuftCtx *) t->context)->name.c_str(); }
+static ggml_backend_buffer_t sbuft_alloc(ggml_backend_buffer_type_t t, size_t size) {
+    SplitBufCtx * c = new SplitBufCtx();
+    c->t = (const SplitBuftCtx *) t->context;
+    return new ggml_backend_buffer{kSplitBufIface, t, c, size, GGML_BACKEND_BUFFER_USAGE_WEIGHTS};
+}
+static size_t sbuft_align(ggml_backend_buffer_type_t) { return 128; }
+static size_t sbuft_alloc_size(ggml_backend_buffer_type_t, const ggml_tensor * t) { return mx_nbytes(t); }
+static bool sbuft_is_host(ggml_backend_buffer_type_t) { return false; }
+static const ggml_backend_buffer_type_i kSplitBuftIface = {
+    sbuft_name, sbuft_alloc, sbuft_align, nullptr, sbuft_alloc_size, sbuft_is_host,
+};
+
+bool buft_is_split(ggml_backend_buffer_type_t t) { return t && t->iface.alloc_buffer == sbuft_alloc; }
+int split_main_device(ggml_backend_buffer_type_t t) { return ((const SplitBuftCtx *) t->context)->main; }
+bool tensor_is_split(const ggml_tensor * t) { return t && t->buffer && buft_is_split(t->buffer->buft); }
+
+// the proc "ggml_backend_split_buffer_type": (main device, tensor_split fractions)
+ggml_backend_buffer_type_t split_buffer_type(int main_device, const float * tensor_split) {
+    static std::mutex mu;
+    static std::map<std::pair<int, std::array<float, MX_MAX_DEVICES>>, ggml_backend_buffer_type> types;
+    std::lock_guard<std::mutex> lk(mu);
+    const int n = mx_dev_count();
+    if (main_device < 0 || main_device >= n) return nullptr;
+    std::array<float, MX_MAX_DEVICES> cum{};
+    bool zero = true;
+    for (int i = 0; i < n && tensor_split; ++i) zero = zero && tensor_split[i] == 0.0f;
+    float sum = 0.0f;
+    for (int i = 0; i < n; ++i) {       // default: equal shares (the devices are identical)
+        cum[i] = sum;
+        sum += zero ? 1.0f : tensor_split[i];
+    }
+    for (int i = 0; i < n; ++i) cum[i] /= sum;
+    auto it = types.find({main_device, cum});
+    if (it != types.end()) return &it->second;
+    SplitBuftCtx * c = new SplitBuftCtx();
+    c->main = main_device;
+    c->split = cum;
+    c->name = "MI355X" + std::to_string(main_device) + "_Split";
+    ggml_backend_buffer_type bt{kSplitBuftIface, mx_dev_handle(main_device), c};
+    return &types.emplace(std::make_pair(main_device, cum), bt).first->second;
+}
+
+// ---- MUL_MAT with a split src0
+struct DevStage { void * p = nullptr; size_t cap = 0; };
+static DevStage g_x[MX_MAX_DEVICES], g_y[MX_MAX_DEVICES];
+static hipEvent_t g_ev_main[MX_MAX_DEVICES], g_ev_done[MX_MAX_DEVICES];
+
+static void * stage_buf(DevStage & s, int hip, size_t bytes) {
+    if (bytes > s.cap) {
+        HIP_CHECK(hipSetDevice(hip));
+        if (s.p) HIP_CHECK(hipFree(s.p));
+        HIP_CHECK(hipMalloc(&s.p, bytes));
+        s.cap = bytes;
+    }
+    return s.p;
+}
+
+void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    const SplitExtra * e = (const SplitExtra *) w->extra;
+    MX_ASSERT(e && x->type == GGML_TYPE_F32 && mx_is_contiguous(x) && mx_is_contiguous(dst) && dst->type == GGML_TYPE_F32);
+    MX_ASSERT(x->ne[2] * x->ne[3] == dst->ne[2] * dst->ne[3]);
+    const int64_t N = x->ne[1] * x->ne[2] * x->ne[3];
+    const size_t xb = mx_nbytes(x);
+    const int main_hip = c.s->device;
+    // src1 is ready on the main stream at this point
+    static bool ev_init = false;
+    if (!ev_init) {
+        for (int d = 0; d < mx_dev_count(); ++d) {
+            HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
+            HIP_CHECK(hipEventCreateWithFlags(&g_ev_done[d], hipEventDisableTiming));
+            HIP_CHECK(hipSetDevice(main_hip));
+            HIP_CHECK(hipEventCreateWithFlags(&g_ev_main[d], hipEventDisableTiming));
+        }
+        ev_init = true;
+    }
+    MX_KLOG("mm_split M=%d K=%d N=%d devices=%d", (int) w->ne[1], (int) w->ne[0], (int) N, mx_dev_count());
+    for (int d = 0; d < mx_dev_count(); ++d) {
+        const int64_t rows = e->hi[d] - e->lo[d];
+        if (rows == 0) continue;
+        Stream * ds = mx_aux_stream(d);
+        const int hip = ds->device;
+        HIP_CHECK(hipSetDevice(main_hip));
+        HIP_CHECK(hipEventRecord(g_ev_main[d], c.st));
+        HIP_CHECK(hipSetDevice(hip));
+        HIP_CHECK(hipStreamWaitEvent(ds->stream, g_ev_main[d], 0));
+        // the slice's operands on device d: src1 by peer copy, the partial dst
+        void * xd = stage_buf(g_x[d], hip, xb);
+        void * yd = stage_buf(g_y[d], hip, (size_t) rows * N * 4);
+        if (hip == main_hip) HIP_CHECK(hipMemcpyAsync(xd, x->data, xb, hipMemcpyDeviceToDevice, ds->stream));
+        else HIP_CHECK(hipMemcpyPeerAsync(xd, hip, x->data, main_hip, xb, ds->stream));
+        ggml_tensor ws = *w, xs = *x, ys = *dst;
+        ws.ne[1] = rows; ws.nb[2] = ws.nb[3] = ws.nb[1] * rows; ws.data = e->data[d]; ws.buffer = nullptr; ws.extra = nullptr;
+        ws.view_src = nullptr;
+        xs.data = xd; xs.buffer = nullptr; xs.view_src = nullptr;
+        ys.ne[0] = rows; ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[1] * ys.ne[1]; ys.nb[3] = ys.nb[2] * ys.ne[2];
+        ys.data = yd; ys.buffer = nullptr; ys.view_src = nullptr;
+        ys.src[0] = &ws; ys.src[1] = &xs;
+        stream_reserve_node(ds, &ys);
+        OpCtx dc{ds, ds->stream, &ds->scratch};
+        ds->scratch.reset();
+        act_cache_reset(ds);
+        op_mul_mat(dc, &ys);
+        // the slice's rows of every column back into dst on the main device
+        HIP_CHECK(hipMemcpy2DAsync((char *) dst->data + e->lo[d] * 4, dst->nb[1], yd, (size_t) rows * 4, (size_t) rows * 4, N,
+                                   hipMemcpyDeviceToDevice, ds->stream));
+        HIP_CHECK(hipEventRecord(g_ev_done[d], ds->stream));
+        HIP_CHECK(hipSetDevice(main_hip));
+        HIP_CHECK(hipStreamWaitEvent(c.st, g_ev_done[d], 0));
+    }
+    HIP_CHECK(hipSetDevice(main_hip));
+}
+
+}  // namespace mx

@@ -66,6 +66,9 @@ int main(int argc, char ** argv) {
     std::string model, tok_in, logits_out;
     int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0, incremental = 0, last = 0, n_batch = 0, n_ubatch = 0, reps = 1;
     int ctk = -1;   // K/V cache type (ggml_type id), -1: default f16
+    std::string sm = "layer";          // -sm none|layer|row
+    std::vector<float> ts;             // -ts a,b,...
+    int mg = 0;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() { return std::string(argv[++i]); };
@@ -83,6 +86,17 @@ int main(int argc, char ** argv) {
         else if (a == "-ub") n_ubatch = std::stoi(next());
         else if (a == "-r") reps = std::max(1, std::stoi(next()));
         else if (a == "-ctk") ctk = std::stoi(next());
+        else if (a == "-sm") sm = next();
+        else if (a == "-mg") mg = std::stoi(next());
+        else if (a == "-ts") {
+            std::string v = next();
+            for (size_t p = 0; p <= v.size();) {
+                size_t q = v.find_first_of(",/", p);
+                if (q == std::string::npos) q = v.size();
+                ts.push_back(std::stof(v.substr(p, q - p)));
+                p = q + 1;
+            }
+        }
         else if (a == "--dump") g_dump = fopen(next().c_str(), "w");
         else if (a == "--dump-dir") g_dump_dir = next();
         else if (a == "--dump-filter") g_dump_filter = next();
@@ -95,6 +109,10 @@ int main(int argc, char ** argv) {
                 ggml_backend_dev_description(ggml_backend_dev_get(i)));
     llama_model_params mp = llama_model_default_params();
     mp.n_gpu_layers = ngl;
+    mp.split_mode = sm == "row" ? LLAMA_SPLIT_MODE_ROW : sm == "none" ? LLAMA_SPLIT_MODE_NONE : LLAMA_SPLIT_MODE_LAYER;
+    mp.main_gpu = mg;
+    static float tsplit[128] = {};
+    if (!ts.empty()) { for (size_t i = 0; i < ts.size() && i < 128; ++i) tsplit[i] = ts[i]; mp.tensor_split = tsplit; }
     llama_model * m = llama_model_load_from_file(model.c_str(), mp);
     if (!m) { fprintf(stderr, "load failed\n"); return 1; }
     const int n_vocab = llama_vocab_n_tokens(llama_model_get_vocab(m));

@@ -42,7 +42,7 @@ def ggufs(tmp_path_factory):
     return out
 
 
-def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False, ctk=None, klog=None):
+def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False, ctk=None, klog=None, extra=(), env_extra=None):
     tf = tmp_path / "toks.i32"
     of = tmp_path / f"logits_{ngl}_{fa}_{int(incremental)}.f32"
     np.asarray(toks, np.int32).tofile(tf)
@@ -56,6 +56,9 @@ def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False, ctk=None, klog=Non
         cmd.append("--incremental")
     if ctk is not None:
         cmd += ["-ctk", str(ctk)]        # K and V cache type (ggml type id)
+    cmd += list(extra)
+    if env_extra and ngl > 0:
+        env.update(env_extra)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     n_vocab = int(r.stdout.strip().splitlines()[-1].split('"n_vocab": ')[1].split(",")[0].rstrip("}"))
@@ -134,3 +137,22 @@ def test_layer_split_handoff_cpy_tensor_async(tmp_path):
     r = subprocess.run([probe, LIB], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     assert '"mismatches": 0' in r.stdout and "MI355X" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("incremental", [False, True])
+def test_dropin_row_split(ggufs, tmp_path, incremental):
+    """llama -sm row -ts 1,1: libllama puts every matrix in the backend's split buffer type
+    (proc ggml_backend_split_buffer_type), rows halved over two devices — here two logical
+    devices of the one MI355X (GGML_MI355X_VIRTUAL_DEVICES=2) — and every MUL_MAT runs its
+    slices on both and gathers them (split.cpp). Logits against the reference CPU backend."""
+    _need_ref()
+    toks = np.random.default_rng(10).integers(0, 1000, 24 if incremental else 40)
+    g = ggufs[("small", "q4_k_m")]
+    klog = tmp_path / "klog.txt"
+    cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental)
+    gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, klog=klog, extra=["-sm", "row", "-ts", "1,1"],
+                       env_extra={"GGML_MI355X_VIRTUAL_DEVICES": "2"})
+    assert "MI355X" in log
+    assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+    kl = klog.read_text()
+    assert "mm_split" in kl and "devices=2" in kl, kl[-2000:]
