@@ -232,10 +232,10 @@ static void be_free(ggml_backend_t b) {
     if (getenv("GGML_MI355X_STATS"))
         fprintf(stderr, "[mi355x] stats {\"backend\": \"%s\", \"graph_compute\": %llu, \"graph_replay\": %llu, "
                 "\"nodes_run\": %llu, \"nodes_fused\": %llu, \"host_us\": {\"graph_compute\": %.0f, \"set_async\": %.0f, "
-                "\"get_async\": %.0f, \"synchronize\": %.0f}, \"n_set\": %llu, \"bytes_set\": %llu, \"n_get\": %llu, "
+                "\"get_async\": %.0f, \"synchronize\": %.0f, \"signature\": %.0f, \"graph_launch\": %.0f}, \"n_set\": %llu, \"bytes_set\": %llu, \"n_get\": %llu, "
                 "\"bytes_get\": %llu, \"n_staged\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
                 (unsigned long long) s->n_graph_replay, (unsigned long long) s->n_nodes_run, (unsigned long long) s->n_fused,
-                s->us_compute, s->us_set, s->us_get, s->us_sync, (unsigned long long) s->n_set, (unsigned long long) s->b_set,
+                s->us_compute, s->us_set, s->us_get, s->us_sync, s->us_sig, s->us_launch, (unsigned long long) s->n_set, (unsigned long long) s->b_set,
                 (unsigned long long) s->n_get, (unsigned long long) s->b_get,
                 (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n : 0));
     if (const char * kp = getenv("GGML_MI355X_KLOG")) klog_dump(kp);

@@ -128,6 +128,7 @@ struct Stream {
     // microseconds spent inside graph_compute / set_async / get_async / synchronize, and
     // the calls and bytes of the copies
     double us_compute = 0, us_set = 0, us_get = 0, us_sync = 0;
+    double us_sig = 0, us_launch = 0;   // inside graph_compute: signature compare, hipGraphLaunch
     uint64_t n_set = 0, n_get = 0, b_set = 0, b_get = 0;
 };
 
