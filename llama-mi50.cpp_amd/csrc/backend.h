@@ -203,6 +203,8 @@ using UseCount = std::unordered_map<const ggml_tensor *, int>;
 int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 // MoE router chain / expert combine in one launch each (ops_moe.hip); nodes consumed
 int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i);
+// -fa 0 decode attention chain (ops_fattn_dec.hip)
+int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 // the executor's guard for a node about to run (deferred norms it reads or overwrites)
 void deferred_guard_node_ext(OpCtx & c, const ggml_tensor * n);

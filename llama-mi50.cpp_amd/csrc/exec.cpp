@@ -85,6 +85,7 @@ static bool g_no_qkv = getenv("GGML_MI355X_NO_QKV_FUSION") != nullptr;
 static bool g_no_moe_fusion = getenv("GGML_MI355X_NO_MOE_FUSION") != nullptr;   // A/B
 static bool g_no_topk = getenv("GGML_MI355X_NO_TOPK_FUSION") != nullptr;
 static bool g_no_combine = getenv("GGML_MI355X_NO_COMBINE_FUSION") != nullptr;
+static bool g_no_attn_nofa = getenv("GGML_MI355X_NO_ATTN_FUSION") != nullptr;   // -fa 0 decode chain
 
 // ---- deferred RMS norm --------------------------------------------------------
 // An attn_norm / ffn_norm pair whose every consumer is a single-token GEMV is not
@@ -395,6 +396,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             if (n->op == GGML_OP_MUL_MAT && !g_no_qkv) {
                 const int k = fuse_qkv_rope_store(c, g, i, uses);
                 if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; deferred_retire(s, g, i0, i); continue; }
+            }
+            if (n->op == GGML_OP_MUL_MAT && !g_no_attn_nofa) {
+                const int k = fuse_attn_nofa(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 3; s->n_nodes_run += 4; deferred_retire(s, g, i0, i); continue; }
             }
             if (n->op == GGML_OP_MUL_MAT_ID && try_fuse_moe_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
             if (n->op == GGML_OP_SOFT_MAX && !g_no_moe_fusion && !g_no_topk) {

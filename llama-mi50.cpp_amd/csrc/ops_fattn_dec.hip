@@ -406,4 +406,187 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     MX_ABORT("fattn dec2 D=%d G=%d NW=%d", D, f.G, f.NW);
 }
 
+// ---------------------------------------------------------------------------
+// Non-flash-attention decode (llama-bench's default -fa 0): build_attn_mha's chain
+// MUL_MAT(k, q) -> SOFT_MAX(mask, scale) -> MUL_MAT(v, kq) -> PERMUTE -> CONT
+// (src/llama-graph.cpp:1740-1796) for one query token in ONE launch instead of four
+// (2 dense GEMVs of 7.5 us, the softmax and the copy: 24.8 us per layer in the -fa 0
+// drop-in profile). One workgroup per query head. Semantics per node: kq = f16(q)·k (the
+// first mul_mat converts q to K's vec_dot_type f16), softmax over the row in f32
+// (x·scale + mask, exp(x - max), times 1/sum), kqv = f16(p)·v (the second mul_mat
+// converts p to f16), f32 accumulation. V is the transposed cache view: one contiguous
+// row of n_kv values per dimension.
+struct NfArgs {
+    const char * q; size_t q2;          // q [D, 1, H] f32: head stride (bytes)
+    const char * k; size_t k1, k2;      // k [D, n_kv, Hkv] f16: key stride, head stride
+    const char * v; size_t v1, v2;      // v [n_kv, D, Hkv] f16: dimension stride, head stride
+    const char * mask; int mask_f16;    // the token's mask row [n_kv] (f16 or f32), nullable
+    float * dst;                        // [H * D]
+    int n_kv, H, Hkv;
+    float scale;
+};
+
+constexpr int NF_NI = 8;                // key rows per lane in flight
+
+template <int D>
+__global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
+    extern __shared__ __align__(16) float sc[];   // [n_kv]: scores, then f16-rounded probabilities
+    __shared__ float red[4];
+    __shared__ float opart[256 / D][D];
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    constexpr int LPK = D / 8, KPI = 64 / LPK, PER = 4 * NF_NI * KPI;   // keys per workgroup pass
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = blockIdx.x, hk = h / (p.H / p.Hkv);
+    const int c = lane % LPK, kq = lane / LPK;
+    h2v qh[4];
+    {
+        const float * qp = (const float *) (p.q + (size_t) h * p.q2) + 8 * c;
+        const float4 a = *(const float4 *) qp, b = *(const float4 *) (qp + 4);
+        qh[0] = h2v{(_Float16) a.x, (_Float16) a.y}; qh[1] = h2v{(_Float16) a.z, (_Float16) a.w};
+        qh[2] = h2v{(_Float16) b.x, (_Float16) b.y}; qh[3] = h2v{(_Float16) b.z, (_Float16) b.w};
+    }
+    const char * kb = p.k + (size_t) hk * p.k2 + c * 16;
+    for (int base = 0; base < p.n_kv; base += PER) {
+        uint4 kr[NF_NI];
+        int key[NF_NI];
+#pragma unroll
+        for (int t = 0; t < NF_NI; ++t) {
+            key[t] = base + (wave * NF_NI + t) * KPI + kq;
+            kr[t] = *(const uint4 *) (kb + (size_t) min(key[t], p.n_kv - 1) * p.k1);
+        }
+#pragma unroll
+        for (int t = 0; t < NF_NI; ++t) {
+            float acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[0], 0.f, false);
+            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[1], acc, false);
+            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[2], acc, false);
+            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[3], acc, false);
+            acc = dpp_sum_group<LPK>(acc);
+            if (c == LPK - 1 && key[t] < p.n_kv) {
+                float m = 0.f;
+                if (p.mask) m = p.mask_f16 ? h2f(((const uint16_t *) p.mask)[key[t]]) : ((const float *) p.mask)[key[t]];
+                sc[key[t]] = acc * p.scale + m;
+            }
+        }
+    }
+    __syncthreads();
+    // softmax (ggml_vec_soft_max_f32: exp(x - max), Σ, times 1/Σ)
+    float mx = -INFINITY;
+    for (int k = tid; k < p.n_kv; k += 256) mx = fmaxf(mx, sc[k]);
+    mx = wave_max(mx);
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float sum = 0.f;
+    for (int k = tid; k < p.n_kv; k += 256) {
+        const float e = sc[k] == -INFINITY ? 0.f : expf(sc[k] - mx);
+        sc[k] = e;
+        sum += e;
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) red[wave] = sum;
+    __syncthreads();
+    const float inv = 1.0f / ((red[0] + red[1]) + (red[2] + red[3]));
+    for (int k = tid; k < p.n_kv; k += 256) sc[k] = (float) (_Float16) (sc[k] * inv);
+    __syncthreads();
+    // P·V over the transposed rows: 256/D threads per dimension, each a contiguous key range
+    constexpr int SPLIT = 256 / D;
+    const int d = tid % D, part = tid / D;
+    const int nk = p.n_kv / SPLIT;                           // host: n_kv % (8 SPLIT) == 0
+    const char * vr = p.v + (size_t) hk * p.v2 + (size_t) d * p.v1 + (size_t) part * nk * 2;
+    const float * pp = sc + part * nk;
+    float o = 0.f;
+    for (int k = 0; k < nk; k += 8) {
+        const uint4 w = *(const uint4 *) (vr + 2 * k);
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            o += pp[k + 2 * j] * h2f((uint16_t) (ww[j] & 0xFFFF));
+            o += pp[k + 2 * j + 1] * h2f((uint16_t) (ww[j] >> 16));
+        }
+    }
+    opart[part][d] = o;
+    __syncthreads();
+    if (tid < D) {
+        float r = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < SPLIT; ++s2) r += opart[s2][tid];
+        p.dst[(size_t) h * D + tid] = r;
+    }
+}
+
+static bool nf_view(const ggml_tensor * t) {
+    return t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW || t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE;
+}
+static const ggml_tensor * nf_base(const ggml_tensor * t) {
+    while (t && nf_view(t)) t = t->src[0];
+    return t;
+}
+
+// returns the number of graph nodes consumed from i (0: no match)
+int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
+    auto use = [&](const ggml_tensor * t) { auto it = uses.find(t); return it == uses.end() ? 0 : it->second; };
+    ggml_tensor * kq = g->nodes[i];
+    if (kq->op != GGML_OP_MUL_MAT) return 0;
+    const ggml_tensor * k = kq->src[0], * q = kq->src[1];
+    if (k->type != GGML_TYPE_F16 || q->type != GGML_TYPE_F32 || kq->type != GGML_TYPE_F32) return 0;
+    const int D = (int) k->ne[0];
+    if ((D != 64 && D != 128) || q->ne[0] != D || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1) return 0;
+    const int n_kv = (int) k->ne[1], H = (int) q->ne[2], Hkv = (int) k->ne[2];
+    if (H % Hkv || n_kv % 16 || n_kv > 16384 || k->nb[0] != 2 || k->nb[1] % 16 || k->nb[2] % 16 || (uintptr_t) k->data % 16) return 0;
+    if (q->nb[0] != 4 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return 0;
+    ggml_tensor * sm = nullptr, * kqv = nullptr, * out = nullptr;
+    int last = i;
+    for (int j = i + 1; j < g->n_nodes && j < i + 12; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (nf_view(n)) continue;
+        if (!sm && n->op == GGML_OP_SOFT_MAX && n->src[0] == kq) { sm = n; last = j; continue; }
+        if (sm && !kqv && n->op == GGML_OP_MUL_MAT && n->src[1] == sm) { kqv = n; last = j; continue; }
+        if (kqv && !out && (n->op == GGML_OP_CONT || n->op == GGML_OP_CPY || n->op == GGML_OP_DUP) && nf_base(n->src[0]) == kqv &&
+            n->src[0]->op == GGML_OP_PERMUTE) { out = n; last = j; break; }
+        break;
+    }
+    if (!sm || !kqv || !out) return 0;
+    // the softmax: plain scale + mask, no ALiBi / sinks
+    if (sm->src[2] || mx_op_param<float>(sm, 1) != 0.0f || sm->type != GGML_TYPE_F32 || !mx_is_contiguous(sm)) return 0;
+    const ggml_tensor * m = sm->src[1];
+    if (m && ((m->type != GGML_TYPE_F16 && m->type != GGML_TYPE_F32) || m->ne[0] < n_kv || !mx_is_contiguous(m))) return 0;
+    // v: the transposed cache view [n_kv, D, Hkv], contiguous keys per dimension
+    const ggml_tensor * v = kqv->src[0];
+    if (v->type != GGML_TYPE_F16 || v->ne[0] != n_kv || v->ne[1] != D || v->ne[2] != Hkv || v->ne[3] != 1 || v->nb[0] != 2) return 0;
+    if (v->nb[1] % 16 || v->nb[2] % 16 || (uintptr_t) v->data % 16) return 0;
+    if (kqv->ne[0] != D || kqv->ne[1] != 1 || kqv->ne[2] != H || kqv->type != GGML_TYPE_F32) return 0;
+    if (out->type != GGML_TYPE_F32 || !mx_is_contiguous(out) || mx_nelements(out) != (int64_t) D * H) return 0;
+    const ggml_tensor * pm = out->src[0];   // permute(kqv, 0, 2, 1, 3): element (d, h) -> out[h * D + d]
+    if (pm->ne[0] != D || pm->ne[1] != H || pm->nb[1] != kqv->nb[2]) return 0;
+    // intermediates read only inside the chain, nothing else in between
+    if (use(kq) != 1 || use(sm) != 1 || ((kq->flags | sm->flags | kqv->flags) & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    for (int j = i + 1; j <= last; ++j) {
+        const ggml_tensor * n = g->nodes[j];
+        if (n != sm && n != kqv && n != out && !nf_view(n)) return 0;
+        if (nf_view(n) && nf_base(n) == kqv && n != pm) return 0;   // another reader of kqv
+    }
+    for (const ggml_tensor * t : {(const ggml_tensor *) kq, (const ggml_tensor *) sm, (const ggml_tensor *) kqv})
+        for (int j = last + 1; j < g->n_nodes; ++j)
+            for (int s2 = 0; s2 < GGML_MAX_SRC; ++s2)
+                if (g->nodes[j]->src[s2] && nf_base(g->nodes[j]->src[s2]) == t) return 0;
+    NfArgs a{};
+    a.q = (const char *) q->data; a.q2 = q->nb[2];
+    a.k = (const char *) k->data; a.k1 = k->nb[1]; a.k2 = k->nb[2];
+    a.v = (const char *) v->data; a.v1 = v->nb[1]; a.v2 = v->nb[2];
+    a.mask = m ? (const char *) m->data : nullptr; a.mask_f16 = m && m->type == GGML_TYPE_F16;
+    a.dst = (float *) out->data;
+    a.n_kv = n_kv; a.H = H; a.Hkv = Hkv;
+    a.scale = mx_op_param<float>(sm, 0);
+    for (int j = i; j <= last; ++j) {
+        deferred_guard_node_ext(c, g->nodes[j]);
+        act_cache_invalidate(c.s, g->nodes[j]);
+    }
+    MX_KLOG("attn_nofa D=%d n_kv=%d H=%d Hkv=%d mask=%d", D, n_kv, H, Hkv, m ? (int) m->type : -1);
+    const size_t lds = (size_t) n_kv * 4;
+    if (D == 128) k_attn_nofa_dec<128><<<(unsigned) H, 256, lds, c.st>>>(a);
+    else k_attn_nofa_dec<64><<<(unsigned) H, 256, lds, c.st>>>(a);
+    return last - i + 1;
+}
+
 }  // namespace mx

@@ -481,3 +481,49 @@ def test_moe_router_fusion(pkg, backend, n_tok, n_exp, producer):
     assert nmse(w.reshape(n_tok, k), ref_w) < 1e-6
     assert nmse(wn.reshape(n_tok, k), ref_w / ref_w.sum(1, keepdims=True)) < 1e-6
     assert any(ln.startswith("topk_moe") for ln in log), log
+
+
+@pytest.mark.parametrize("n_kv,H,Hkv,D,mask_t", [(256, 32, 8, 128, "f32"), (512, 8, 8, 128, "f16"), (96, 4, 2, 64, "f32"),
+                                                 (256, 32, 8, 128, None)])
+def test_attn_nofa_decode_chain(pkg, backend, n_kv, H, Hkv, D, mask_t):
+    """-fa 0 decode attention (llama-bench's default): MUL_MAT(k, q) -> SOFT_MAX(mask, scale)
+    -> MUL_MAT(v^T, kq) -> PERMUTE -> CONT (src/llama-graph.cpp:1740-1796) as one launch
+    (k_attn_nofa_dec), against the node-by-node semantics in float64: q and p rounded to
+    f16 as the two mul_mats' vec_dot_type conversions do"""
+    rng = np.random.default_rng(n_kv + H + D)
+    q = rng.standard_normal((H, 1, D)).astype(np.float32)
+    k = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16)
+    vt = rng.standard_normal((Hkv, D, n_kv)).astype(np.float16)     # transposed V cache view
+    mask = np.zeros((1, n_kv), np.float32)
+    mask[0, n_kv - 5:] = -np.inf
+    scale = 1.0 / np.sqrt(D)
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, 1, H)
+        tk = ctx.new_tensor("f16", D, n_kv, Hkv)
+        tv = ctx.new_tensor("f16", n_kv, D, Hkv)
+        tm = ctx.new_tensor(mask_t, n_kv, 1) if mask_t else None
+        kq = ctx.mul_mat(tk, tq)
+        sm = ctx.soft_max_ext(kq, tm, scale)
+        kqv = ctx.mul_mat(tv, sm)
+        out = ctx.cont(ctx.permute(kqv, 0, 2, 1, 3))
+        feed = [(tq, q), (tk, k.view(np.uint16)), (tv, vt.view(np.uint16))]
+        if mask_t:
+            feed.append((tm, mask if mask_t == "f32" else mask.astype(np.float16).view(np.uint16)))
+        return [out], feed
+
+    backend.klog(True)
+    y = run(pkg, backend, build)[0].reshape(H, D)
+    log = backend.klog_read()
+    backend.klog(False)
+    assert any(ln.startswith("attn_nofa") for ln in log), log
+    G = H // Hkv
+    ref = np.empty((H, D))
+    for h in range(H):
+        s = (q[h, 0].astype(np.float16).astype(np.float64) @ k[h // G].astype(np.float64).T) * scale
+        if mask_t:
+            s = s + mask[0]
+        e = np.exp(s - s.max())
+        pr = (e / e.sum()).astype(np.float16).astype(np.float64)
+        ref[h] = vt[h // G].astype(np.float64) @ pr
+    assert nmse(y, ref) < 1e-6, nmse(y, ref)
