@@ -13,7 +13,9 @@
  *
  * Only the members the backend touches are given meaningful names; every offset
  * is pinned by static_assert below and re-checked against the real headers by
- * tests/test_abi_layout.py (compiles a probe against /root/reference when present).
+ * tests/test_abi_cpu.py (test_abi_layout_matches_reference: ggml_tensor and enums;
+ * test_vtable_layout_matches_reference: every backend vtable and the structs embedding
+ * them, ggml-backend-impl.h:17-210 — probes compiled against /root/reference when present).
  */
 #pragma once
 

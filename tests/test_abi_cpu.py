@@ -81,3 +81,54 @@ def test_abi_layout_matches_reference(tmp_path):
         subprocess.run(["gcc", "-std=gnu11", "-I", inc, str(c), "-o", str(exe)], check=True)
         outs.append(subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout)
     assert outs[0] == outs[1]
+
+
+# the backend vtables and the structs that embed them (ggml/src/ggml-backend-impl.h:17-210,
+# ggml/include/ggml-backend.h:140-170 for the device props/caps): member order, offsets
+# and sizes of include/ggml_abi.h against the reference headers
+VTABLE_STRUCTS = ["ggml_backend_buffer_type_i", "ggml_backend_buffer_type", "ggml_backend_buffer_i",
+                  "ggml_backend_buffer", "ggml_backend_i", "ggml_backend", "ggml_backend_event",
+                  "ggml_backend_device_i", "ggml_backend_device", "ggml_backend_reg_i", "ggml_backend_reg",
+                  "ggml_backend_dev_caps", "ggml_backend_dev_props", "ggml_backend_feature"]
+
+
+def struct_members(src, name):
+    m = re.search(r"struct\s+" + name + r"\s*\{(.*?)\n\s*\};", src, flags=re.S)
+    assert m, f"struct {name} not found in include/ggml_abi.h"
+    body = re.sub(r"//[^\n]*", "", m.group(1))
+    members = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        fp = re.search(r"\(\s*\*\s*(\w+)\s*\)", decl)
+        members.append(fp.group(1) if fp else re.findall(r"(\w+)\s*(?:\[[^\]]*\])?\s*$", decl)[0])
+    return members
+
+
+def test_vtable_layout_matches_reference(tmp_path):
+    """sizeof / offsetof of every backend vtable member: a reordered or missing function
+    pointer would make libllama call the wrong entry point. Skipped on the GPU box."""
+    ref_root = "/root/reference/ggml"
+    if not os.path.isdir(ref_root):
+        pytest.skip("reference headers not present")
+    src = open(os.path.join(ROOT, "include", "ggml_abi.h")).read()
+    lines = []
+    for s in VTABLE_STRUCTS:
+        mem = struct_members(src, s)
+        assert mem, s
+        lines.append(f'fprintf(f,"{s} %zu\\n",sizeof(struct {s}));')
+        lines += [f'fprintf(f,"{s}.{x} %zu\\n",offsetof(struct {s},{x}));' for x in mem]
+    probe = lambda hdr: "\n".join([f'#include "{hdr}"', "#include <stddef.h>", "#include <stdio.h>",
+                                   "void dump(FILE*f){", *lines, "}", "int main(){dump(stdout);return 0;}"])
+    outs = []
+    for incs, hdr in [([f"{ref_root}/include", f"{ref_root}/src"], "ggml-backend-impl.h"),
+                      ([os.path.join(ROOT, "include")], "ggml_abi.h")]:
+        c = tmp_path / f"v_{hdr}.c"
+        c.write_text(probe(hdr))
+        exe = tmp_path / f"v_{hdr}"
+        args = ["gcc", "-std=gnu11"] + [a for i in incs for a in ("-I", i)] + [str(c), "-o", str(exe)]
+        subprocess.run(args, check=True)
+        outs.append(subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout)
+    assert outs[0].count("\n") > 80
+    assert outs[0] == outs[1]
