@@ -113,6 +113,16 @@ struct Stream {
     // pass by the first fused QKV block, read by all layers' (same position, same params)
     float * rope_tab = nullptr;        // device, float2 [MX_ROPE_TAB]
     unsigned int * fa_cnt = nullptr;   // device, zeroed; each decode FA launch leaves it zero
+    // weight ranges the next decode attention launch touches while HBM is otherwise idle
+    // (fa_prefetch_plan in exec.cpp; consumed by fa_dec2_run)
+    const char * pf_ptr[4] = {};
+    size_t pf_len[4] = {}, pf_take[4] = {};   // bytes; bytes taken from the head of each eighth
+    int pf_n = 0;
+    // second stage: the GEMV right after the attention (output projection, ~2 TB/s) warms
+    // the next part of each eighth (gpf_off .. + gpf_take) while its own stream runs
+    const ggml_tensor * gpf_node = nullptr;   // the MUL_MAT that carries it
+    bool gpf_armed = false;                   // set while that node runs
+    size_t gpf_off = 0, gpf_take = 0;
     bool rope_valid = false;
     const void * rope_pos = nullptr, * rope_ff = nullptr;
     int32_t rope_params[11] = {};

@@ -370,6 +370,55 @@ static bool try_group_mm(OpCtx & c, ggml_cgraph * g, int i, std::unordered_map<c
     return true;
 }
 
+// Decode attention is latency-bound (one K/V round trip over 32 CUs, ~6 us per layer) and
+// leaves HBM idle. Its launch carries extra workgroups that touch one dword per 128-B line
+// of the weights the next streaming GEMV reads (gate/up: the first MUL_MATs after the
+// attention whose weights are >= 16 MB, sharing one activation), from the XCD whose
+// blocks will read them (gemv.cuh xcd_block gives XCD x the x-th eighth of a matrix's
+// rows, starting at its head), so that GEMV starts on L2 / Infinity-Cache hits.
+// Measured on the Llama-3-8B decode (tg128 603 -> 617 tok/s, same box): 16 MB over gate
+// and up took 1.3 us off the SwiGLU launch per 6.6 MB; the 9.4 MB output projection
+// (latency-bound at ~2 TB/s) gained nothing, and budgets past ~24 MB outlast the
+// attention itself. Budget: g_tune[23] MB (> 0), else GGML_MI355X_FA_PREFETCH_MB
+// (default 16; 0 = off); minimum matrix size g_tune[24] MB (-1 = none).
+extern int g_tune[32];
+static int g_pf_mb_env = getenv("GGML_MI355X_FA_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_FA_PREFETCH_MB")) : 16;
+static int g_gpf_mb_env = getenv("GGML_MI355X_GEMV_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_GEMV_PREFETCH_MB")) : 0;
+static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i) {
+    s->pf_n = 0;
+    const int mb = g_tune[23] ? g_tune[23] : g_pf_mb_env;
+    if (mb <= 0 || g->nodes[i]->src[0]->ne[1] > 4) return;   // decode rows only
+    const size_t min_len = (size_t) (g_tune[24] ? std::max(0, g_tune[24]) : 16) << 20;
+    const ggml_tensor * x = nullptr;
+    for (int j = i + 1; j < g->n_nodes && j < i + 64 && s->pf_n < 4; ++j) {
+        const ggml_tensor * n = g->nodes[j];
+        if (n->op == GGML_OP_FLASH_ATTN_EXT || n->op == GGML_OP_MUL_MAT_ID) break;
+        if (n->op != GGML_OP_MUL_MAT || !n->src[0]->data || tensor_is_split(n->src[0]) || n->src[1]->ne[1] > 4) continue;
+        if (mx_nbytes(n->src[0]) < min_len) continue;
+        if (x && n->src[1] != x) break;       // the next GEMV only
+        x = n->src[1];
+        s->pf_ptr[s->pf_n] = (const char *) n->src[0]->data;
+        s->pf_len[s->pf_n++] = mx_nbytes(n->src[0]);
+    }
+    const size_t per = ((size_t) mb << 20) / std::max(1, s->pf_n);   // even split: one kernel reads them together
+    for (int r = 0; r < s->pf_n; ++r) s->pf_take[r] = std::min(s->pf_len[r], per) / 8;
+    // second stage (g_tune[25] MB, else GGML_MI355X_GEMV_PREFETCH_MB): carried by the first
+    // MUL_MAT after the attention when it is a small latency-bound GEMV (under min_len)
+    s->gpf_node = nullptr;
+    const int mb2 = g_tune[25] ? g_tune[25] : g_gpf_mb_env;
+    if (mb2 <= 0 || !s->pf_n) return;
+    for (int j = i + 1; j < g->n_nodes && j < i + 16; ++j) {
+        const ggml_tensor * n = g->nodes[j];
+        if (n->op != GGML_OP_MUL_MAT) continue;
+        if (mx_nbytes(n->src[0]) < min_len && n->src[1]->ne[1] == 1) s->gpf_node = n;
+        break;
+    }
+    s->gpf_off = s->pf_take[0];
+    const size_t per2 = ((size_t) mb2 << 20) / s->pf_n;
+    s->gpf_take = std::min(s->pf_len[0] / 8 - std::min(s->pf_len[0] / 8, s->gpf_off), per2 / 8);
+    for (int r = 1; r < s->pf_n; ++r) if (s->pf_take[r] != s->gpf_off) s->gpf_node = nullptr;   // one offset for all
+}
+
 static void run_nodes(Stream * s, ggml_cgraph * g) {
     OpCtx c{s, s->stream, &s->scratch};
     static thread_local UseMap uses;
@@ -389,6 +438,8 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         if (is_view_op(n->op) || mx_is_empty(n)) continue;
         if (!done.empty() && done.count(n)) continue;
         s->scratch.reset();
+        if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i);   // (pf_n read by that node and gpf_node)
+        s->gpf_armed = s->gpf_node && n == s->gpf_node;
         if (s->use_fusion) {
             const int i0 = i;
             if (n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }

@@ -38,6 +38,9 @@ struct FaDecArgs {
     float scale;
     unsigned long long * trace;    // debug (MX_TRACE), workgroup 0
     unsigned long long * trace_blk;
+    // weight prefetch (grid rows y >= nsplit, see fa_prefetch_plan in exec.cpp): one dword
+    // per 128-B line of each range, so the next GEMV launches hit the Infinity Cache
+    const char * pf[4]; size_t pf_eighth[4]; unsigned pf_lines[4]; int pf_n;   // lines per eighth
 };
 
 constexpr int FD_NI = 4;          // key-row load instructions per wave per chunk
@@ -69,6 +72,22 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     __shared__ int s_last;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if ((int) blockIdx.y >= p.nsplit) {       // prefetch rows (workgroup-uniform: no barrier below)
+        // linear workgroup id L runs on XCD L % 8 (fa_dec2_run keeps the first prefetch id
+        // and their count multiples of 8); XCD x touches the head of the x-th eighth of
+        // every range, the rows its GEMV blocks will read first
+        const unsigned L = blockIdx.x + gridDim.x * blockIdx.y, P0 = gridDim.x * p.nsplit;
+        const unsigned xcd = L & 7, T = (gridDim.x * (gridDim.y - p.nsplit) >> 3) * NT;
+        const unsigned t0 = ((L - P0) >> 3) * NT + tid;
+        unsigned acc = 0;
+        for (int r = 0; r < p.pf_n; ++r) {
+            const unsigned * w = (const unsigned *) (p.pf[r] + (size_t) xcd * p.pf_eighth[r]);
+#pragma unroll 4
+            for (unsigned l = t0; l < p.pf_lines[r]; l += T) acc ^= w[(size_t) l * 32];
+        }
+        if (acc == 0x9E3779B9u && p.n_kv < 0) p.part[0] = 0.f;   // never (n_kv > 0): keeps the loads
+        return;
+    }
     const int c = lane % LPK, kq = lane / LPK;
     const int Gt = p.H / p.Hkv, NGB = Gt / G;
     const int hk = blockIdx.x % p.Hkv;
@@ -393,9 +412,20 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     a.cnt = c.s->fa_cnt;
     a.trace = mx_trace_slot(0);
     a.trace_blk = mx_trace_blocks();
-    const dim3 grid((unsigned) (a.Hkv * (Gt / f.G) * a.n_q * q->ne[3]), (unsigned) a.nsplit);
+    const unsigned gx = (unsigned) (a.Hkv * (Gt / f.G) * a.n_q * q->ne[3]);
+    unsigned pf_rows = 0;
+    a.pf_n = c.s->pf_n;
+    for (int r = 0; r < a.pf_n; ++r) {
+        a.pf[r] = c.s->pf_ptr[r]; a.pf_eighth[r] = c.s->pf_len[r] / 8; a.pf_lines[r] = (unsigned) (c.s->pf_take[r] / 128);
+    }
+    // ~160 otherwise idle workgroups, first id and count multiples of 8 (XCD = id % 8)
+    if (a.pf_n && (gx * a.nsplit) % 8 == 0) {
+        pf_rows = (unsigned) mx_ceil_div(160, gx);
+        while ((gx * pf_rows) % 8) ++pf_rows;
+    } else a.pf_n = 0;
+    const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
     const bool kq = k->type == GGML_TYPE_Q8_0;
-    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv, (int) kq);
+    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv, (int) kq, pf_rows);
 #define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { \
         if (kq) k_fattn_dec2<DD, GG, NWW, true><<<grid, 64 * NWW, 0, c.st>>>(a); \
         else k_fattn_dec2<DD, GG, NWW><<<grid, 64 * NWW, 0, c.st>>>(a); \

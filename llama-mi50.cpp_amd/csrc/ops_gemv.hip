@@ -26,6 +26,9 @@ struct G2Args {
     size_t w_exp;                                // weight expert stride (bytes)
     int64_t x_col;                               // f32 source: floats per activation column
     size_t d_slot, d_tok;                        // dst strides (floats)
+    // weight prefetch rows (grid.y > 0, dense only; exec.cpp fa_prefetch_plan's second
+    // stage): lines [off, off + lines) of the XCD's eighth of each range
+    const char * pf[4]; size_t pf_eighth[4], pf_off; unsigned pf_lines; int pf_n;
 };
 
 // per-item bases of a MUL_MAT_ID GEMV workgroup; false: no valid expert (block-uniform)
@@ -53,6 +56,18 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     constexpr int NM = EPI == 1 ? 2 : 1;
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (!p.ids && blockIdx.y > 0) {            // prefetch rows: workgroup-uniform, before any barrier
+        const unsigned L = blockIdx.x + gridDim.x * blockIdx.y, xcd = L & 7;
+        const unsigned T = (gridDim.x * (gridDim.y - 1) >> 3) * (64 * W), t0 = ((L - gridDim.x) >> 3) * (64 * W) + threadIdx.x;
+        unsigned acc = 0;
+        for (int r = 0; r < p.pf_n; ++r) {
+            const unsigned * w = (const unsigned *) (p.pf[r] + (size_t) xcd * p.pf_eighth[r] + p.pf_off);
+#pragma unroll 4
+            for (unsigned l = t0; l < p.pf_lines; l += T) acc ^= w[(size_t) l * 32];
+        }
+        if (acc == 0x9E3779B9u && p.nrows < 0) p.dst[0] = 0.f;   // never (nrows > 0): keeps the loads
+        return;
+    }
     const int sub = lane % LPR;
     const int blk = xcd_block((int) blockIdx.x, (int) gridDim.x, p.xs.xcd);
     const int row = (blk * W + wave) * RPW + lane / LPR;
@@ -109,13 +124,17 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
 }
 
 template <int QT, int LPR, int UPL, int EPI, int W = 4>
-static void launch_cfg(hipStream_t st, const G2Args & p, bool regs = false) {
+static void launch_cfg(hipStream_t st, const G2Args & p0, bool regs = false) {
+    G2Args p = p0;
     constexpr int RPB = W * (64 / LPR);
-    const dim3 grid((unsigned) ((p.nrows + RPB - 1) / RPB), p.ids ? (unsigned) p.n_items : 1u);
+    const dim3 grid0((unsigned) ((p.nrows + RPB - 1) / RPB), p.ids ? (unsigned) p.n_items : 1u);
     // regs: register staging of x even on a large grid (the q8-emitting SwiGLU)
-    const int mode = gemv_mode(p.xs, p.K, regs && g_tune[9] == 0 ? 0 : (int64_t) grid.x * grid.y * W, 64 * W);
+    const int mode = gemv_mode(p.xs, p.K, regs && g_tune[9] == 0 ? 0 : (int64_t) grid0.x * grid0.y * W, 64 * W);
+    if (p.pf_n && grid0.x % 8) p.pf_n = 0;          // prefetch ids must start on XCD 0
     const size_t lds = gemv_lds_bytes(p.K, mode);
-    MX_KLOG("gemv2 qt=%d lpr=%d upl=%d epi=%d w=%d mode=%d K=%d M=%d q8o=%d", QT, LPR, UPL, EPI, W, mode, p.K, p.nrows, p.q8o != nullptr);
+    MX_KLOG("gemv2 qt=%d lpr=%d upl=%d epi=%d w=%d mode=%d K=%d M=%d q8o=%d pf=%d", QT, LPR, UPL, EPI, W, mode, p.K, p.nrows, p.q8o != nullptr, p.pf_n);
+    dim3 grid = grid0;
+    if (p.pf_n && !p.ids) grid.y = 2;           // one row of prefetch workgroups (grid0.x % 8 == 0)
     switch (mode) {
         case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8><<<grid, 64 * W, lds, st>>>(p); break;
         case XS_NORM_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_LDS><<<grid, 64 * W, lds, st>>>(p); break;
@@ -215,6 +234,13 @@ void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, cons
         p.q8o = (int8_t *) q8out->q; p.q8od = (float *) q8out->d; p.q8os = (float *) q8out->s;
     }
     MX_ASSERT(!(glu && res));
+    if (c.s->gpf_armed && !glu) {               // the executor's second prefetch stage
+        c.s->gpf_armed = false;
+        p.pf_n = c.s->pf_n;
+        for (int r = 0; r < p.pf_n; ++r) { p.pf[r] = c.s->pf_ptr[r]; p.pf_eighth[r] = c.s->pf_len[r] / 8; }
+        p.pf_off = c.s->gpf_off & ~(size_t) 127;
+        p.pf_lines = (unsigned) (c.s->gpf_take / 128);
+    }
     gemv2_launch_p(c, p, w->type, glu, res != nullptr);
 }
 

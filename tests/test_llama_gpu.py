@@ -172,3 +172,37 @@ def test_bench_pipeline_two_ranks_one_gpu(tmp_path):
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0 and "layer split" in out["config"]["parallelism"]
     assert out["pp512_tok_s"] > 0
+
+
+def test_weight_prefetch_leaves_logits_unchanged(pkg):
+    """The decode attention's (and, second stage, the output projection's) extra
+    workgroups only read the next GEMV's weights (exec.cpp fa_prefetch_plan): logits are
+    bit-identical with the prefetch off, and the launches did carry the prefetch rows.
+    TINY's matrices are under the 16 MB default floor, so the floor is lifted (tune 24).
+    A fresh backend per setting: captured decode graphs are cached per backend."""
+    lib = pkg._lib.load()
+    rng = np.random.default_rng(11)
+    toks = rng.integers(0, TINY["n_vocab"], 8).astype(np.int32)
+
+    def run(knobs):
+        for k, v in knobs.items():
+            lib.ggml_backend_mi355x_set_tune(k, v)
+        try:
+            be = pkg.Backend(0)
+            m = pkg.Model.random(be, TINY, "q4_k_m", seed=3)
+            s = pkg.Session(m, n_ctx=256, flash_attn=True)
+            be.klog(True)
+            out = np.stack([s.decode(toks[i:i + 1]) for i in range(len(toks))])
+            log = be.klog_read()
+            be.klog(False)
+            s.free(); m.free(); be.free()
+        finally:
+            for k in knobs:
+                lib.ggml_backend_mi355x_set_tune(k, 0)
+        return out, log
+
+    off, _ = run({23: -1})
+    on, log = run({23: 2, 24: -1, 25: 1})
+    assert any(ln.startswith("fattn_dec2") and "pf_rows=0" not in ln for ln in log), log[-20:]
+    assert any(ln.startswith("gemv2") and "epi=2" in ln and "pf=0" not in ln for ln in log), log[-20:]
+    assert np.array_equal(off, on)
