@@ -384,10 +384,10 @@ static bool try_group_mm(OpCtx & c, ggml_cgraph * g, int i, std::unordered_map<c
 extern int g_tune[32];
 static int g_pf_mb_env = getenv("GGML_MI355X_FA_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_FA_PREFETCH_MB")) : 16;
 static int g_gpf_mb_env = getenv("GGML_MI355X_GEMV_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_GEMV_PREFETCH_MB")) : 0;
-static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i) {
+static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q) {
     s->pf_n = 0;
     const int mb = g_tune[23] ? g_tune[23] : g_pf_mb_env;
-    if (mb <= 0 || g->nodes[i]->src[0]->ne[1] > 4) return;   // decode rows only
+    if (mb <= 0 || n_q > 4) return;                            // decode rows only
     const size_t min_len = (size_t) (g_tune[24] ? std::max(0, g_tune[24]) : 16) << 20;
     const ggml_tensor * x = nullptr;
     for (int j = i + 1; j < g->n_nodes && j < i + 64 && s->pf_n < 4; ++j) {
@@ -438,7 +438,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         if (is_view_op(n->op) || mx_is_empty(n)) continue;
         if (!done.empty() && done.count(n)) continue;
         s->scratch.reset();
-        if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i);   // (pf_n read by that node and gpf_node)
+        // (pf_n read by the attention launch and gpf_node; the non-FA chain starts at
+        // MUL_MAT(k, q) and is matched by fuse_attn_nofa below)
+        if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i, n->src[0]->ne[1]);
+        else if (n->op == GGML_OP_MUL_MAT && n->src[0]->type == GGML_TYPE_F16 && n->src[1]->ne[1] == 1) fa_prefetch_plan(s, g, i, 1);
         s->gpf_armed = s->gpf_node && n == s->gpf_node;
         if (s->use_fusion) {
             const int i0 = i;

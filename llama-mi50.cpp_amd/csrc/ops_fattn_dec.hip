@@ -454,6 +454,7 @@ struct NfArgs {
     float * dst;                        // [H * D]
     int n_kv, H, Hkv;
     float scale;
+    const char * pf[4]; size_t pf_eighth[4]; unsigned pf_lines[4]; int pf_n;   // as FaDecArgs
 };
 
 constexpr int NF_NI = 8;                // key rows per lane in flight
@@ -466,6 +467,18 @@ __global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
     typedef _Float16 h2v __attribute__((ext_vector_type(2)));
     constexpr int LPK = D / 8, KPI = 64 / LPK, PER = 4 * NF_NI * KPI;   // keys per workgroup pass
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.y > 0) {                      // weight prefetch rows, as in k_fattn_dec2
+        const unsigned L = blockIdx.x + gridDim.x * blockIdx.y, xcd = L & 7;
+        const unsigned T = (gridDim.x * (gridDim.y - 1) >> 3) * 256, t0 = ((L - gridDim.x) >> 3) * 256 + tid;
+        unsigned acc = 0;
+        for (int r = 0; r < p.pf_n; ++r) {
+            const unsigned * w = (const unsigned *) (p.pf[r] + (size_t) xcd * p.pf_eighth[r]);
+#pragma unroll 4
+            for (unsigned l = t0; l < p.pf_lines[r]; l += T) acc ^= w[(size_t) l * 32];
+        }
+        if (acc == 0x9E3779B9u && p.n_kv < 0) p.dst[0] = 0.f;   // never (n_kv > 0): keeps the loads
+        return;
+    }
     const int h = blockIdx.x, hk = h / (p.H / p.Hkv);
     const int c = lane % LPK, kq = lane / LPK;
     h2v qh[4];
@@ -612,10 +625,16 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         deferred_guard_node_ext(c, g->nodes[j]);
         act_cache_invalidate(c.s, g->nodes[j]);
     }
-    MX_KLOG("attn_nofa D=%d n_kv=%d H=%d Hkv=%d mask=%d", D, n_kv, H, Hkv, m ? (int) m->type : -1);
+    MX_KLOG("attn_nofa D=%d n_kv=%d H=%d Hkv=%d mask=%d pf=%d", D, n_kv, H, Hkv, m ? (int) m->type : -1, H % 8 == 0 ? c.s->pf_n : 0);
     const size_t lds = (size_t) n_kv * 4;
-    if (D == 128) k_attn_nofa_dec<128><<<(unsigned) H, 256, lds, c.st>>>(a);
-    else k_attn_nofa_dec<64><<<(unsigned) H, 256, lds, c.st>>>(a);
+    dim3 grid((unsigned) H, 1);
+    a.pf_n = H % 8 == 0 ? c.s->pf_n : 0;       // prefetch ids must start on XCD 0
+    for (int r = 0; r < a.pf_n; ++r) {
+        a.pf[r] = c.s->pf_ptr[r]; a.pf_eighth[r] = c.s->pf_len[r] / 8; a.pf_lines[r] = (unsigned) (c.s->pf_take[r] / 128);
+    }
+    if (a.pf_n) grid.y = 1 + (unsigned) mx_ceil_div(640, H);   // ~640 prefetch workgroups of 4 waves
+    if (D == 128) k_attn_nofa_dec<128><<<grid, 256, lds, c.st>>>(a);
+    else k_attn_nofa_dec<64><<<grid, 256, lds, c.st>>>(a);
     return last - i + 1;
 }
 

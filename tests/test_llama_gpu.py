@@ -174,12 +174,15 @@ def test_bench_pipeline_two_ranks_one_gpu(tmp_path):
     assert out["pp512_tok_s"] > 0
 
 
-def test_weight_prefetch_leaves_logits_unchanged(pkg):
+@pytest.mark.parametrize("fa", [True, False])
+def test_weight_prefetch_leaves_logits_unchanged(pkg, fa):
     """The decode attention's (and, second stage, the output projection's) extra
     workgroups only read the next GEMV's weights (exec.cpp fa_prefetch_plan): logits are
     bit-identical with the prefetch off, and the launches did carry the prefetch rows.
-    TINY's matrices are under the 16 MB default floor, so the floor is lifted (tune 24).
-    A fresh backend per setting: captured decode graphs are cached per backend."""
+    TINY's matrices are under the 16 MB default floor, so the floor is lifted (tune 24); its
+    head size is widened to 64 (the decode attention kernels take D 64/128). A fresh
+    backend per setting: captured decode graphs are cached per backend."""
+    shape = dict(TINY, n_embd=512)
     lib = pkg._lib.load()
     rng = np.random.default_rng(11)
     toks = rng.integers(0, TINY["n_vocab"], 8).astype(np.int32)
@@ -189,8 +192,8 @@ def test_weight_prefetch_leaves_logits_unchanged(pkg):
             lib.ggml_backend_mi355x_set_tune(k, v)
         try:
             be = pkg.Backend(0)
-            m = pkg.Model.random(be, TINY, "q4_k_m", seed=3)
-            s = pkg.Session(m, n_ctx=256, flash_attn=True)
+            m = pkg.Model.random(be, shape, "q4_k_m", seed=3)
+            s = pkg.Session(m, n_ctx=256, flash_attn=fa)
             be.klog(True)
             out = np.stack([s.decode(toks[i:i + 1]) for i in range(len(toks))])
             log = be.klog_read()
@@ -203,6 +206,9 @@ def test_weight_prefetch_leaves_logits_unchanged(pkg):
 
     off, _ = run({23: -1})
     on, log = run({23: 2, 24: -1, 25: 1})
-    assert any(ln.startswith("fattn_dec2") and "pf_rows=0" not in ln for ln in log), log[-20:]
+    if fa:
+        assert any(ln.startswith("fattn_dec2") and "pf_rows=0" not in ln for ln in log), log[-20:]
+    else:
+        assert any(ln.startswith("attn_nofa") and "pf=0" not in ln for ln in log), log[-20:]
     assert any(ln.startswith("gemv2") and "epi=2" in ln and "pf=0" not in ln for ln in log), log[-20:]
     assert np.array_equal(off, on)
