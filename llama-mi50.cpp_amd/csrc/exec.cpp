@@ -380,15 +380,17 @@ static bool try_group_mm(OpCtx & c, ggml_cgraph * g, int i, std::unordered_map<c
 // and up took 1.3 us off the SwiGLU launch per 6.6 MB; the 9.4 MB output projection
 // (latency-bound at ~2 TB/s) gained nothing, and budgets past ~24 MB outlast the
 // attention itself. Budget: g_tune[23] MB (> 0), else GGML_MI355X_FA_PREFETCH_MB
-// (default 16; 0 = off); minimum matrix size g_tune[24] MB (-1 = none).
+// (default 16; 0 = off); minimum matrix size g_tune[24] KB (-1 = none).
 extern int g_tune[32];
 static int g_pf_mb_env = getenv("GGML_MI355X_FA_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_FA_PREFETCH_MB")) : 16;
 static int g_gpf_mb_env = getenv("GGML_MI355X_GEMV_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_GEMV_PREFETCH_MB")) : 0;
-static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q) {
+static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q, bool nofa) {
     s->pf_n = 0;
-    const int mb = g_tune[23] ? g_tune[23] : g_pf_mb_env;
+    // the non-FA chain's kernel is shorter than the 16 MB stream: measured 554 -> 546 tok/s
+    // with it (bench tg128 --no-fa, same box), so there it is opt-in (g_tune[26] MB)
+    const int mb = nofa ? g_tune[26] : (g_tune[23] ? g_tune[23] : g_pf_mb_env);
     if (mb <= 0 || n_q > 4) return;                            // decode rows only
-    const size_t min_len = (size_t) (g_tune[24] ? std::max(0, g_tune[24]) : 16) << 20;
+    const size_t min_len = g_tune[24] ? (size_t) std::max(0, g_tune[24]) << 10 : (size_t) 16 << 20;   // tune 24 in KB
     const ggml_tensor * x = nullptr;
     for (int j = i + 1; j < g->n_nodes && j < i + 64 && s->pf_n < 4; ++j) {
         const ggml_tensor * n = g->nodes[j];
@@ -440,8 +442,8 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         s->scratch.reset();
         // (pf_n read by the attention launch and gpf_node; the non-FA chain starts at
         // MUL_MAT(k, q) and is matched by fuse_attn_nofa below)
-        if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i, n->src[0]->ne[1]);
-        else if (n->op == GGML_OP_MUL_MAT && n->src[0]->type == GGML_TYPE_F16 && n->src[1]->ne[1] == 1) fa_prefetch_plan(s, g, i, 1);
+        if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i, n->src[0]->ne[1], false);
+        else if (n->op == GGML_OP_MUL_MAT && n->src[0]->type == GGML_TYPE_F16 && n->src[1]->ne[1] == 1) fa_prefetch_plan(s, g, i, 1, true);
         s->gpf_armed = s->gpf_node && n == s->gpf_node;
         if (s->use_fusion) {
             const int i0 = i;
