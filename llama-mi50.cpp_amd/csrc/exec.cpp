@@ -411,7 +411,7 @@ static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q, bo
     if (mb2 <= 0 || !s->pf_n) return;
     for (int j = i + 1; j < g->n_nodes && j < i + 16; ++j) {
         const ggml_tensor * n = g->nodes[j];
-        if (n->op != GGML_OP_MUL_MAT) continue;
+        if (n->op != GGML_OP_MUL_MAT || n->src[0]->type == GGML_TYPE_F16 || n->src[0]->type == GGML_TYPE_F32) continue;   // attention mul_mats
         if (mx_nbytes(n->src[0]) < min_len && n->src[1]->ne[1] == 1) s->gpf_node = n;
         break;
     }
