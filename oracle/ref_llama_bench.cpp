@@ -69,6 +69,7 @@ int main(int argc, char ** argv) {
     std::string sm = "layer";          // -sm none|layer|row
     std::vector<float> ts;             // -ts a,b,...
     int mg = 0;
+    int use_mmap = 1;                  // -mmp 0: libllama's async upload through pinned host buffers
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() { return std::string(argv[++i]); };
@@ -88,6 +89,7 @@ int main(int argc, char ** argv) {
         else if (a == "-ctk") ctk = std::stoi(next());
         else if (a == "-sm") sm = next();
         else if (a == "-mg") mg = std::stoi(next());
+        else if (a == "-mmp") use_mmap = std::stoi(next());
         else if (a == "-ts") {
             std::string v = next();
             for (size_t p = 0; p <= v.size();) {
@@ -111,6 +113,7 @@ int main(int argc, char ** argv) {
     mp.n_gpu_layers = ngl;
     mp.split_mode = sm == "row" ? LLAMA_SPLIT_MODE_ROW : sm == "none" ? LLAMA_SPLIT_MODE_NONE : LLAMA_SPLIT_MODE_LAYER;
     mp.main_gpu = mg;
+    mp.use_mmap = use_mmap != 0;
     static float tsplit[128] = {};
     if (!ts.empty()) { for (size_t i = 0; i < ts.size() && i < 128; ++i) tsplit[i] = ts[i]; mp.tensor_split = tsplit; }
     llama_model * m = llama_model_load_from_file(model.c_str(), mp);

@@ -8,6 +8,7 @@ Tolerance: NMSE 2e-3 on whole-model logits (the reference's test-backend-ops bou
 full graphs); prefill (one ubatch, MFMA GEMM path) and incremental decode
 (one token per llama_decode: GEMV / decode-FA / fused QKV path) are both checked.
 Synthetic GGUFs come from tools/gguf_synth.py (random weights, seeded)."""
+import json
 import os
 import subprocess
 import sys
@@ -156,6 +157,22 @@ def test_dropin_row_split(ggufs, tmp_path, incremental):
     assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
     kl = klog.read_text()
     assert "mm_split" in kl and "devices=2" in kl, kl[-2000:]
+
+
+def test_dropin_async_upload_no_mmap(ggufs, tmp_path):
+    """llama -mmp 0: the model loader uploads the weights through this backend's pinned
+    host buffers, set_tensor_async and events (src/llama-model-loader.cpp:999-1180, the
+    path taken when the device reports async + host_buffer + events) instead of mmap +
+    set_tensor. The weights must land identically: logits bit-equal to the mmap load, and
+    the upload backend's counters show the file's bytes went through set_tensor_async."""
+    _need_ref()
+    toks = np.random.default_rng(13).integers(0, 1000, 24)
+    g = ggufs[("small", "q4_k_m")]
+    a, _ = run_ref(tmp_path, g, toks, 99, 1)
+    b, err = run_ref(tmp_path, g, toks, 99, 1, extra=["-mmp", "0"], env_extra={"GGML_MI355X_STATS": "1"})
+    assert np.array_equal(a, b)
+    st = [json.loads(ln.split("stats ", 1)[1]) for ln in err.splitlines() if "[mi355x] stats" in ln]
+    assert st and max(x["bytes_set"] for x in st) > 0.5 * os.path.getsize(g), st
 
 
 def _kld_stats(p_logits, q_logits):
