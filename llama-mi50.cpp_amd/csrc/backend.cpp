@@ -15,6 +15,13 @@
 #include <mutex>
 #include <memory>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <ucontext.h>
+#include <unistd.h>
+
 namespace mx {
 
 void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status);  // exec.cpp
@@ -254,6 +261,7 @@ static void be_set_async(ggml_backend_t b, ggml_tensor * t, const void * data, s
     Stream * s = stream_of(b);
     const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));
+    staged_writes_wait(s->device, s->stream);   // no-op on the staging stream itself
     HIP_CHECK(hipMemcpyAsync((char *) t->data + off, data, size, hipMemcpyHostToDevice, s->stream));
     s->us_set += now_us() - t0; s->n_set++; s->b_set += size;
 }
@@ -261,6 +269,7 @@ static void be_get_async(ggml_backend_t b, const ggml_tensor * t, void * data, s
     Stream * s = stream_of(b);
     const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));
+    staged_writes_wait(s->device, s->stream);
     HIP_CHECK(hipMemcpyAsync(data, (const char *) t->data + off, size, hipMemcpyDeviceToHost, s->stream));
     s->us_get += now_us() - t0; s->n_get++; s->b_get += size;
 }
@@ -274,7 +283,11 @@ static bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const ggml_te
     Stream * ds = stream_of(bdst);
     const size_t n = mx_nbytes(dst);
     HIP_CHECK(hipSetDevice(ss->device));
-    if (ss->device == ds->device) {
+    staged_writes_wait(ss->device, ss->stream);   // a staged write to src (or to dst) lands first
+    if (ds->device != ss->device) staged_writes_wait(ds->device, ss->stream);
+    MX_KLOG("cpy_async %s -> %s bytes=%zu peer=%d", ss->name.c_str(), ds->name.c_str(), n,
+            (int) (ss->device != ds->device || mx_force_peer()));
+    if (ss->device == ds->device && !mx_force_peer()) {
         HIP_CHECK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, ss->stream));
     } else {
         HIP_CHECK(hipMemcpyPeerAsync(dst->data, ds->device, src->data, ss->device, n, ss->stream));
@@ -445,6 +458,14 @@ static void * rg_proc(ggml_backend_reg_t, const char * name) {
 static const ggml_backend_reg_i kRegIface = { rg_name, rg_count, rg_get, rg_proc };
 
 // logical devices for the row split (split.cpp)
+static bool g_peer[MX_MAX_DEVICES][MX_MAX_DEVICES];   // peer access enabled a -> b (HIP ids)
+// (GGML_MI355X_NO_PEER: never, also between logical devices of one GPU, so the row split's
+// staged gather runs in one-GPU tests)
+bool mx_peer_enabled(int a, int b) {
+    static const bool no_peer = env_flag("GGML_MI355X_NO_PEER");
+    if (no_peer) return false;
+    return a == b || (a >= 0 && b >= 0 && a < MX_MAX_DEVICES && b < MX_MAX_DEVICES && g_peer[a][b] && g_peer[b][a]);
+}
 int mx_dev_count() { return (int) g_devices.size(); }
 int mx_dev_hip(int logical) { return g_devices[logical]->id; }
 ggml_backend_dev_t mx_dev_handle(int logical) { return &g_devices[logical]->dev; }
@@ -457,8 +478,57 @@ Stream * mx_aux_stream(int logical) {
     return aux[logical];
 }
 
+// GGML_MI355X_SEGV_TRACE=<file>|1: on SIGSEGV/SIGBUS write the faulting PC and address, every
+// frame as module+offset (dladdr: stripped ROCm libraries still resolve to a module and an
+// offset that addr2line / llvm-symbolizer can turn into a symbol offline) and the
+// /proc/self/maps lines, then re-raise. Diagnostics only (the handler is not strictly
+// async-signal-safe); installed after a profiler's own handler, so it runs first.
+static int g_segv_fd = 2;
+static void segv_write(const char * s) { if (write(g_segv_fd, s, strlen(s)) < 0) {} }
+static void segv_handler(int sig, siginfo_t * si, void * uc) {
+    char line[512];
+    const ucontext_t * u = (const ucontext_t *) uc;
+    const void * pc = (const void *) u->uc_mcontext.gregs[REG_RIP];
+    snprintf(line, sizeof line, "[mi355x] signal %d addr %p pc %p\n", sig, si->si_addr, pc);
+    segv_write(line);
+    void * fr[64];
+    const int nf = backtrace(fr, 64);
+    for (int i = 0; i < nf + 1; ++i) {
+        const void * a = i == 0 ? pc : fr[i - 1];
+        Dl_info di{};
+        if (dladdr(a, &di) && di.dli_fname)
+            snprintf(line, sizeof line, "  #%02d %p %s+0x%lx %s+0x%lx\n", i, a, di.dli_fname,
+                     (unsigned long) ((const char *) a - (const char *) di.dli_fbase), di.dli_sname ? di.dli_sname : "?",
+                     di.dli_saddr ? (unsigned long) ((const char *) a - (const char *) di.dli_saddr) : 0ul);
+        else snprintf(line, sizeof line, "  #%02d %p ?\n", i, a);
+        segv_write(line);
+    }
+    segv_write("[mi355x] maps:\n");
+    const int mf = open("/proc/self/maps", O_RDONLY);
+    if (mf >= 0) {
+        char buf[4096];
+        ssize_t k;
+        while ((k = read(mf, buf, sizeof buf)) > 0) if (write(g_segv_fd, buf, (size_t) k) < 0) break;
+        close(mf);
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+static void segv_trace_install() {
+    const char * v = getenv("GGML_MI355X_SEGV_TRACE");
+    if (!v || !*v || strcmp(v, "0") == 0) return;
+    if (strcmp(v, "1") != 0) { const int fd = open(v, O_WRONLY | O_CREAT | O_TRUNC, 0644); if (fd >= 0) g_segv_fd = fd; }
+    struct sigaction sa{};
+    sa.sa_sigaction = segv_handler;
+    sa.sa_flags = SA_SIGINFO;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+}
+
 void klog_env_init();
 static void init_registry() {
+    segv_trace_install();
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) { (void) hipGetLastError(); n = 0; }
     // GGML_MI355X_VIRTUAL_DEVICES=V (tests): V logical devices over the n GPUs, round robin
@@ -495,6 +565,7 @@ static void init_registry() {
                 hipSetDevice(i);
                 const hipError_t e = hipDeviceEnablePeerAccess(j, 0);
                 if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void) hipGetLastError();
+                else if (i < MX_MAX_DEVICES && j < MX_MAX_DEVICES) g_peer[i][j] = true;
             }
         hipSetDevice(0);
     }

@@ -14,6 +14,7 @@ constexpr int MX_MAX_DEVICES = 16;
 bool buft_is_split(ggml_backend_buffer_type_t t);
 int split_main_device(ggml_backend_buffer_type_t t);
 bool tensor_is_split(const ggml_tensor * t);
+bool mx_force_peer();   // GGML_MI355X_FORCE_PEER: cross-device copy branches on one GPU (split.cpp)
 ggml_backend_buffer_type_t split_buffer_type(int main_device, const float * tensor_split);
 // order `stream` after the device's staged small buffer writes (backend.cpp)
 void staged_writes_wait(int dev, hipStream_t stream);

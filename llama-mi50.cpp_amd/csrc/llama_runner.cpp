@@ -167,7 +167,13 @@ static ggml_tensor * wt(mxr_model * m, const char * name, ggml_type t, int64_t n
 static void create_weights(mxr_model * m, const char * recipe) {
     const mxr_hparams & h = m->hp;
     const std::string r = recipe ? recipe : "q4_k_m";
-    ggml_type tmain = GGML_TYPE_Q4_K, tv = GGML_TYPE_Q4_K, tdown = GGML_TYPE_Q4_K, tout = GGML_TYPE_Q6_K, temb = GGML_TYPE_Q4_K;
+    ggml_type tmain = GGML_TYPE_Q4_K, tk = GGML_TYPE_Q4_K, tv = GGML_TYPE_Q4_K, tdown = GGML_TYPE_Q4_K, tout = GGML_TYPE_Q6_K,
+              temb = GGML_TYPE_Q4_K;
+    // llama_tensor_get_type's per-model rules (src/llama-quant.cpp:305-321): the 70B model
+    // (LLM_TYPE_70B: 80 layers) takes attn_v Q4_K -> Q5_K; 8-expert models attn_k and
+    // attn_v Q8_0
+    const bool is70b = h.n_layer == 80 && h.n_expert == 0;
+    const bool exp8 = h.n_expert == 8;
     const int hd = h.n_embd / h.n_head;
     const int nkv = hd * h.n_head_kv;
     m->tok_embd = nullptr;
@@ -181,9 +187,12 @@ static void create_weights(mxr_model * m, const char * recipe) {
         else if (r == "q8_0") { tmain = tv = tdown = tout = temb = GGML_TYPE_Q8_0; }
         else if (r == "f16") { tmain = tv = tdown = tout = temb = GGML_TYPE_F16; }
         else MX_ABORT("unknown recipe %s", r.c_str());
+        tk = tmain;
+        if (r == "q4_k_m" && is70b && tv == GGML_TYPE_Q4_K) tv = GGML_TYPE_Q5_K;
+        if ((r == "q4_k_m" || r == "q5_k_m") && exp8) tk = tv = GGML_TYPE_Q8_0;
         snprintf(nm, sizeof nm, "blk.%d.attn_norm.weight", i); L.attn_norm = wt(m, nm, GGML_TYPE_F32, h.n_embd, 1);
         snprintf(nm, sizeof nm, "blk.%d.attn_q.weight", i); L.wq = wt(m, nm, tmain, h.n_embd, h.n_embd);
-        snprintf(nm, sizeof nm, "blk.%d.attn_k.weight", i); L.wk = wt(m, nm, tmain, h.n_embd, nkv);
+        snprintf(nm, sizeof nm, "blk.%d.attn_k.weight", i); L.wk = wt(m, nm, tk, h.n_embd, nkv);
         snprintf(nm, sizeof nm, "blk.%d.attn_v.weight", i); L.wv = wt(m, nm, tv, h.n_embd, nkv);
         snprintf(nm, sizeof nm, "blk.%d.attn_output.weight", i); L.wo = wt(m, nm, tmain, h.n_embd, h.n_embd);
         snprintf(nm, sizeof nm, "blk.%d.ffn_norm.weight", i); L.ffn_norm = wt(m, nm, GGML_TYPE_F32, h.n_embd, 1);

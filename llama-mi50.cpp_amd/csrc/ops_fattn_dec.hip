@@ -458,6 +458,7 @@ struct NfArgs {
 };
 
 constexpr int NF_NI = 8;                // key rows per lane in flight
+constexpr int NF_MAX_KV = 16384;        // scores in LDS: 64 KB dynamic + ~1 KB static (> the 64 KB default)
 
 template <int D>
 __global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
@@ -576,7 +577,9 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
     const int D = (int) k->ne[0];
     if ((D != 64 && D != 128) || q->ne[0] != D || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1) return 0;
     const int n_kv = (int) k->ne[1], H = (int) q->ne[2], Hkv = (int) k->ne[2];
-    if (H % Hkv || n_kv % 16 || n_kv > 16384 || k->nb[0] != 2 || k->nb[1] % 16 || k->nb[2] % 16 || (uintptr_t) k->data % 16) return 0;
+    // P·V: 256/D threads per dimension, each a contiguous key range stepped by 8 keys
+    // (16-byte V loads), so n_kv must split into 256/D parts of a multiple of 8 keys
+    if (H % Hkv || n_kv % (8 * (256 / D)) || n_kv > NF_MAX_KV || k->nb[0] != 2 || k->nb[1] % 16 || k->nb[2] % 16 || (uintptr_t) k->data % 16) return 0;
     if (q->nb[0] != 4 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return 0;
     ggml_tensor * sm = nullptr, * kqv = nullptr, * out = nullptr;
     int last = i;
@@ -633,6 +636,12 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         a.pf[r] = c.s->pf_ptr[r]; a.pf_eighth[r] = c.s->pf_len[r] / 8; a.pf_lines[r] = (unsigned) (c.s->pf_take[r] / 128);
     }
     if (a.pf_n) grid.y = 1 + (unsigned) mx_ceil_div(640, H);   // ~640 prefetch workgroups of 4 waves
+    static const bool attr = [] {
+        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<128>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
+        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<64>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
+        return true;
+    }();
+    (void) attr;
     if (D == 128) k_attn_nofa_dec<128><<<grid, 256, lds, c.st>>>(a);
     else k_attn_nofa_dec<64><<<grid, 256, lds, c.st>>>(a);
     return last - i + 1;

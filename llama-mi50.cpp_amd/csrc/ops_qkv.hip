@@ -19,7 +19,7 @@ struct QkvArgs {
     size_t w_row[3];
     int rows[3];
     int nblk_q, nblk_k;            // block ranges: [0,nq) q, [nq,nq+nk) k, rest v
-    int units_a, units_v, K;
+    int units_a, units_k, units_v, K;
     XStage xs;
     float * q_out;                 // roped q, f32 [n_embd]
     char * kc; size_t kc_nb1; const char * kidx; int kidx64;
@@ -39,8 +39,10 @@ __device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i)
 
 // Geometry: LA lanes x UA units per row for Q/K (LA <= 32: the RoPE pair, rows 2i and
 // 2i+1, sits LA lanes apart in one wave), LV x UV for V (no pairing). Rows per block =
-// 4 waves x 64/L.
-template <int QTA, int QTV, int MODE, int LA = 16, int UA = 4, int LV = 16, int UV = 4>
+// 4 waves x 64/L. Weight types per matrix: QTA (q), QTK (k), QTV (v) — the recipes mix
+// them (Q4_K_M: v Q6_K on the use_more_bits layers, Q5_K on the others at 70B; 8-expert
+// Q4_K_M/Q5_K_M: k and v Q8_0, src/llama-quant.cpp:302-321).
+template <int QTA, int QTK, int QTV, int MODE, int LA = 16, int UA = 4, int LV = 16, int UV = 4>
 __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     static_assert(LA <= 32, "RoPE pairs must share a wave");
     extern __shared__ __align__(16) char smem[];
@@ -78,6 +80,7 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     StageRegs<256, MODE> sr;
     stage_issue<256, MODE>(p.xs, p.K, a, sr);
     if (m == 2) gemv_rows_staged<QTV, LV, UV, 1, 256, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, sr, acc, fence);   // block-uniform branch
+    else if (QTK != QTA && m == 1) gemv_rows_staged<QTK, LA, UA, 1, 256, MODE>(rows, p.units_k, sub, a, p.xs, p.K, red, sr, acc, fence);
     else gemv_rows_staged<QTA, LA, UA, 1, 256, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, sr, acc, fence);
     MX_TRACE(tr, 3);
     MX_TRACE_BLK(p.trace_blk, 1);
@@ -192,7 +195,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     if (x->ne[1] != 1 || x->ne[2] != 1 || x->ne[3] != 1) return 0;
     if (!g_gemv2 || !gemv2_ok(mq->src[0], x, mq) || !gemv2_ok(mk->src[0], x, mk) || !gemv2_ok(mv->src[0], x, mv)) return 0;
     const ggml_tensor * wq = mq->src[0], * wk = mk->src[0], * wv = mv->src[0];
-    if (wq->type != wk->type || wq->ne[0] != wk->ne[0] || wq->ne[0] != wv->ne[0]) return 0;
+    if (wq->ne[0] != wk->ne[0] || wq->ne[0] != wv->ne[0]) return 0;
     for (const ggml_tensor * r : {rq, rk}) {
         if (mx_op_param<int32_t>(r, 2) != GGML_ROPE_TYPE_NORMAL || r->type != GGML_TYPE_F32 || !mx_is_contiguous(r)) return 0;
         if (r->src[1]->type != GGML_TYPE_I32 || r->src[1]->ne[0] != 1) return 0;
@@ -230,8 +233,8 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     const int rba = 4 * (64 / GEO[cfg][0]), rbv = 4 * (64 / GEO[cfg][2]);
     p.nblk_q = (int) mx_ceil_div(wq->ne[1], rba);
     p.K = (int) wq->ne[0];
-    p.units_a = (int) (wq->ne[0] / ((wq->type == GGML_TYPE_Q4_0 || wq->type == GGML_TYPE_Q8_0) ? 32 : 64));
-    p.units_v = (int) (wv->ne[0] / ((wv->type == GGML_TYPE_Q4_0 || wv->type == GGML_TYPE_Q8_0) ? 32 : 64));
+    auto units = [](const ggml_tensor * w) { return (int) (w->ne[0] / ((w->type == GGML_TYPE_Q4_0 || w->type == GGML_TYPE_Q8_0) ? 32 : 64)); };
+    p.units_a = units(wq); p.units_k = units(wk); p.units_v = units(wv);
     p.nblk_k = (int) mx_ceil_div(wk->ne[1], rba);
     const int nblk_v = (int) mx_ceil_div(wv->ne[1], rbv);
     p.q_out = (float *) rq->data;
@@ -252,30 +255,35 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     p.corr0 = std::max(0.0f, floorf(yarn_corr(n_dims, n_ctx_orig, mx_op_param<float>(rq, 9), base)));
     p.corr1 = std::min((float) (n_dims - 1), ceilf(yarn_corr(n_dims, n_ctx_orig, mx_op_param<float>(rq, 10), base)));
 
-    const int ta = wq->type, tv = wv->type;
+    const int ta = wq->type, tk = wk->type, tv = wv->type;
     void (*kern)(QkvArgs) = nullptr;
-    // the Llama K-quant mixes get every geometry; the other type pairs the default one
-#define GEOS(TA, TV, M) if (ta == TA && tv == TV) kern = cfg == 0 ? k_qkv_rope_store<TA, TV, M, 16, 4, 16, 4> : \
-        cfg == 1 ? k_qkv_rope_store<TA, TV, M, 16, 4, 64, 1> : cfg == 2 ? k_qkv_rope_store<TA, TV, M, 32, 2, 64, 1> : \
-        cfg == 3 ? k_qkv_rope_store<TA, TV, M, 32, 2, 32, 2> : cfg == 4 ? k_qkv_rope_store<TA, TV, M, 32, 1, 32, 1> : \
-        k_qkv_rope_store<TA, TV, M, 16, 2, 32, 2>;
-#define QKV(TA, TV) if (ta == TA && tv == TV) kern = k_qkv_rope_store<TA, TV, XS_NORM, 16, 2, 32, 2>;
-    QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
-    QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
-    QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
+    // the (q, k, v) weight-type triples of the recipes: Q4_K_M / Q5_K_M (v Q6_K on the
+    // use_more_bits layers; v Q5_K at 70B; k and v Q8_0 for 8 experts), Q4_0, Q8_0, Q6_K.
+    // The Llama-3-8B Q4_K_M mixes get every geometry; the others the default one.
+#define QKV_TYPES(X) X(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) X(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) \
+    X(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, GGML_TYPE_Q5_K) X(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, GGML_TYPE_Q8_0) \
+    X(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0, GGML_TYPE_Q8_0) X(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) \
+    X(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) X(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K, GGML_TYPE_Q8_0) \
+    X(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0, GGML_TYPE_Q8_0) X(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) \
+    X(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) X(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
+#define GEOS(TA, TV, M) if (ta == TA && tk == TA && tv == TV) kern = cfg == 0 ? k_qkv_rope_store<TA, TA, TV, M, 16, 4, 16, 4> : \
+        cfg == 1 ? k_qkv_rope_store<TA, TA, TV, M, 16, 4, 64, 1> : cfg == 2 ? k_qkv_rope_store<TA, TA, TV, M, 32, 2, 64, 1> : \
+        cfg == 3 ? k_qkv_rope_store<TA, TA, TV, M, 32, 2, 32, 2> : cfg == 4 ? k_qkv_rope_store<TA, TA, TV, M, 32, 1, 32, 1> : \
+        k_qkv_rope_store<TA, TA, TV, M, 16, 2, 32, 2>;
+#define QKV(TA, TK, TV) if (ta == TA && tk == TK && tv == TV) kern = k_qkv_rope_store<TA, TK, TV, XS_NORM, 16, 2, 32, 2>;
+    QKV_TYPES(QKV)
 #undef QKV
     GEOS(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, XS_NORM) GEOS(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K, XS_NORM)
     if (!kern) return 0;
     if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs)) return 0;
     const int mode = gemv_mode(p.xs, p.K, 0);
     if (mode != XS_NORM) {   // the fused block normally follows attn_norm; other sources
-#define QKV(TA, TV) if (ta == TA && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TV, XS_Q8, 16, 2, 32, 2> : \
-        mode == XS_NORM_H2 ? k_qkv_rope_store<TA, TV, XS_NORM_H2, 16, 2, 32, 2> : k_qkv_rope_store<TA, TV, XS_F32_H2, 16, 2, 32, 2>;
-            QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0)
-        QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q5_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0)
-        QKV(GGML_TYPE_Q6_K, GGML_TYPE_Q6_K) QKV(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKV(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
+#define QKV(TA, TK, TV) if (ta == TA && tk == TK && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TK, TV, XS_Q8, 16, 2, 32, 2> : \
+        mode == XS_NORM_H2 ? k_qkv_rope_store<TA, TK, TV, XS_NORM_H2, 16, 2, 32, 2> : k_qkv_rope_store<TA, TK, TV, XS_F32_H2, 16, 2, 32, 2>;
+        QKV_TYPES(QKV)
 #undef QKV
     }
+#undef QKV_TYPES
     // the per-token RoPE table: once per graph pass for a (position, params, factors) key
     Stream * S = c.s;
     if (!S->rope_valid || S->rope_pos != (const void *) p.pos || S->rope_ff != (const void *) p.ff ||
@@ -293,7 +301,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
         p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
         p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
     }
-    MX_KLOG("qkv qta=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d", ta, tv, mode, cfg, p.K, (int) kq8);
+    MX_KLOG("qkv qta=%d qtk=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d", ta, tk, tv, mode, cfg, p.K, (int) kq8);
     hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K, mode), c.st, p);
     if (kq8) {
         k_kv_store_q8<<<(unsigned) mx_ceil_div(wk->ne[1] + wv->ne[1], 256), 256, 0, c.st>>>(p, (int) wk->ne[1], (int) wv->ne[1]);

@@ -29,6 +29,7 @@ int mx_dev_count();
 int mx_dev_hip(int logical);
 ggml_backend_dev_t mx_dev_handle(int logical);
 Stream * mx_aux_stream(int logical);
+bool mx_peer_enabled(int hip_a, int hip_b);
 void stream_reserve_node(Stream * s, const ggml_tensor * n);
 
 constexpr int64_t SPLIT_ROUND = 256;   // rows per slice are a multiple (GEMM row tiles, q8 groups)
@@ -163,18 +164,45 @@ ggml_backend_buffer_type_t split_buffer_type(int main_device, const float * tens
 }
 
 // ---- MUL_MAT with a split src0
-struct DevStage { void * p = nullptr; size_t cap = 0; };
-static DevStage g_x[MX_MAX_DEVICES], g_y[MX_MAX_DEVICES];
-static hipEvent_t g_ev_main[MX_MAX_DEVICES], g_ev_done[MX_MAX_DEVICES];
+// Staging buffers and events per (main device, slice device): a split buffer type with
+// another main device, or a second context, gets state created on its own devices.
+struct SliceState {
+    void * x = nullptr; size_t xcap = 0;        // src1 copy on the slice device
+    void * y = nullptr; size_t ycap = 0;        // the slice's partial dst on the slice device
+    void * g = nullptr; size_t gcap = 0;        // no-peer gather: the partial dst staged on main
+    hipEvent_t ev_main = nullptr;               // main stream -> slice stream (created on main)
+    hipEvent_t ev_done = nullptr;               // slice stream -> main stream (created on slice)
+};
+static std::mutex g_split_mu;
+static std::map<std::pair<int, int>, SliceState> g_slices;   // (main logical, slice logical)
 
-static void * stage_buf(DevStage & s, int hip, size_t bytes) {
-    if (bytes > s.cap) {
+static void * grow(void *& p, size_t & cap, int hip, size_t bytes) {
+    if (bytes > cap) {
         HIP_CHECK(hipSetDevice(hip));
-        if (s.p) HIP_CHECK(hipFree(s.p));
-        HIP_CHECK(hipMalloc(&s.p, bytes));
-        s.cap = bytes;
+        if (p) HIP_CHECK(hipFree(p));
+        HIP_CHECK(hipMalloc(&p, bytes));
+        cap = bytes;
     }
-    return s.p;
+    return p;
+}
+
+static SliceState & slice_state(int main_l, int d) {
+    SliceState & st = g_slices[{main_l, d}];
+    if (!st.ev_main) {
+        HIP_CHECK(hipSetDevice(mx_dev_hip(main_l)));
+        HIP_CHECK(hipEventCreateWithFlags(&st.ev_main, hipEventDisableTiming));
+        HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
+        HIP_CHECK(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
+    }
+    return st;
+}
+
+// GGML_MI355X_FORCE_PEER=1 (tests): take the cross-device copy branches even when two
+// logical devices are the same GPU (hipMemcpyPeerAsync between a device and itself is
+// legal), so virtual-device runs execute the code real multi-GPU runs take.
+bool mx_force_peer() {
+    static const bool f = [] { const char * v = getenv("GGML_MI355X_FORCE_PEER"); return v && *v && strcmp(v, "0") != 0; }();
+    return f;
 }
 
 void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) {
@@ -186,31 +214,30 @@ void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) {
     const int64_t N = x->ne[1] * x->ne[2] * x->ne[3];
     const size_t xb = mx_nbytes(x);
     const int main_hip = c.s->device;
+    const int main_l = split_main_device(w->buffer->buft);
+    MX_ASSERT(mx_dev_hip(main_l) == main_hip);
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    const bool force = mx_force_peer();
+    MX_KLOG("mm_split M=%d K=%d N=%d devices=%d peer=%d direct=%d", (int) w->ne[1], (int) w->ne[0], (int) N, mx_dev_count(), (int) force,
+            (int) mx_peer_enabled(main_hip, main_hip));
     // src1 is ready on the main stream at this point
-    static bool ev_init = false;
-    if (!ev_init) {
-        for (int d = 0; d < mx_dev_count(); ++d) {
-            HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
-            HIP_CHECK(hipEventCreateWithFlags(&g_ev_done[d], hipEventDisableTiming));
-            HIP_CHECK(hipSetDevice(main_hip));
-            HIP_CHECK(hipEventCreateWithFlags(&g_ev_main[d], hipEventDisableTiming));
-        }
-        ev_init = true;
-    }
-    MX_KLOG("mm_split M=%d K=%d N=%d devices=%d", (int) w->ne[1], (int) w->ne[0], (int) N, mx_dev_count());
     for (int d = 0; d < mx_dev_count(); ++d) {
         const int64_t rows = e->hi[d] - e->lo[d];
         if (rows == 0) continue;
+        SliceState & st = slice_state(main_l, d);
         Stream * ds = mx_aux_stream(d);
         const int hip = ds->device;
+        const bool cross = hip != main_hip || force;
+        const bool direct = !cross || mx_peer_enabled(hip, main_hip);   // slice device writes main's dst itself
         HIP_CHECK(hipSetDevice(main_hip));
-        HIP_CHECK(hipEventRecord(g_ev_main[d], c.st));
+        HIP_CHECK(hipEventRecord(st.ev_main, c.st));
         HIP_CHECK(hipSetDevice(hip));
-        HIP_CHECK(hipStreamWaitEvent(ds->stream, g_ev_main[d], 0));
+        HIP_CHECK(hipStreamWaitEvent(ds->stream, st.ev_main, 0));
         // the slice's operands on device d: src1 by peer copy, the partial dst
-        void * xd = stage_buf(g_x[d], hip, xb);
-        void * yd = stage_buf(g_y[d], hip, (size_t) rows * N * 4);
-        if (hip == main_hip) HIP_CHECK(hipMemcpyAsync(xd, x->data, xb, hipMemcpyDeviceToDevice, ds->stream));
+        void * xd = grow(st.x, st.xcap, hip, xb);
+        void * yd = grow(st.y, st.ycap, hip, (size_t) rows * N * 4);
+        HIP_CHECK(hipSetDevice(hip));
+        if (!cross) HIP_CHECK(hipMemcpyAsync(xd, x->data, xb, hipMemcpyDeviceToDevice, ds->stream));
         else HIP_CHECK(hipMemcpyPeerAsync(xd, hip, x->data, main_hip, xb, ds->stream));
         ggml_tensor ws = *w, xs = *x, ys = *dst;
         ws.ne[1] = rows; ws.nb[2] = ws.nb[3] = ws.nb[1] * rows; ws.data = e->data[d]; ws.buffer = nullptr; ws.extra = nullptr;
@@ -224,12 +251,26 @@ void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) {
         ds->scratch.reset();
         act_cache_reset(ds);
         op_mul_mat(dc, &ys);
-        // the slice's rows of every column back into dst on the main device
-        HIP_CHECK(hipMemcpy2DAsync((char *) dst->data + e->lo[d] * 4, dst->nb[1], yd, (size_t) rows * 4, (size_t) rows * 4, N,
-                                   hipMemcpyDeviceToDevice, ds->stream));
-        HIP_CHECK(hipEventRecord(g_ev_done[d], ds->stream));
-        HIP_CHECK(hipSetDevice(main_hip));
-        HIP_CHECK(hipStreamWaitEvent(c.st, g_ev_done[d], 0));
+        if (direct) {
+            // the slice's rows of every column straight into dst on the main device (a 2D
+            // copy over xGMI when the devices differ: peer access is on between them)
+            HIP_CHECK(hipMemcpy2DAsync((char *) dst->data + e->lo[d] * 4, dst->nb[1], yd, (size_t) rows * 4, (size_t) rows * 4, N,
+                                       hipMemcpyDeviceToDevice, ds->stream));
+            HIP_CHECK(hipEventRecord(st.ev_done, ds->stream));
+            HIP_CHECK(hipSetDevice(main_hip));
+            HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));
+        } else {
+            // no peer access (GGML_MI355X_NO_PEER or no link): one contiguous peer copy of
+            // the partial dst into a staging buffer on main, scattered into dst there
+            void * gm = grow(st.g, st.gcap, main_hip, (size_t) rows * N * 4);
+            HIP_CHECK(hipSetDevice(hip));
+            HIP_CHECK(hipMemcpyPeerAsync(gm, main_hip, yd, hip, (size_t) rows * N * 4, ds->stream));
+            HIP_CHECK(hipEventRecord(st.ev_done, ds->stream));
+            HIP_CHECK(hipSetDevice(main_hip));
+            HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));
+            HIP_CHECK(hipMemcpy2DAsync((char *) dst->data + e->lo[d] * 4, dst->nb[1], gm, (size_t) rows * 4, (size_t) rows * 4, N,
+                                       hipMemcpyDeviceToDevice, c.st));
+        }
     }
     HIP_CHECK(hipSetDevice(main_hip));
 }

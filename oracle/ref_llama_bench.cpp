@@ -10,6 +10,9 @@
 //                pp2048 as 4 ubatches with -b 2048 -ub 512);
 //   -r R       : bench mode repeats pp / tg R times and reports the mean and the
 //                per-repetition rates, llama-bench's avg_ts / samples_ts.
+//   -d D       : llama-bench's depth (tools/llama-bench/llama-bench.cpp:2191-2226): before
+//                every timed pp / tg repetition the cleared cache is filled with a
+//                D-token prompt (untimed), so tg runs against D + i keys.
 // -ngl > 0 with GGML_BACKEND_PATH=libggml-mi355x.so runs the reference libllama on the
 // MI355X backend unmodified (the drop-in check).
 #include "llama.h"
@@ -66,6 +69,7 @@ int main(int argc, char ** argv) {
     std::string model, tok_in, logits_out;
     int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0, incremental = 0, last = 0, n_batch = 0, n_ubatch = 0, reps = 1;
     int ctk = -1;   // K/V cache type (ggml_type id), -1: default f16
+    int depth = 0;
     std::string sm = "layer";          // -sm none|layer|row
     std::vector<float> ts;             // -ts a,b,...
     int mg = 0;
@@ -86,6 +90,7 @@ int main(int argc, char ** argv) {
         else if (a == "-b") n_batch = std::stoi(next());
         else if (a == "-ub") n_ubatch = std::stoi(next());
         else if (a == "-r") reps = std::max(1, std::stoi(next()));
+        else if (a == "-d") depth = std::stoi(next());
         else if (a == "-ctk") ctk = std::stoi(next());
         else if (a == "-sm") sm = next();
         else if (a == "-mg") mg = std::stoi(next());
@@ -128,8 +133,8 @@ int main(int argc, char ** argv) {
         fclose(f);
     }
     llama_context_params cp = llama_context_default_params();
-    cp.n_ctx = n_ctx > 0 ? n_ctx : std::max(512, (int) (pp + tg + toks.size() + 64));
-    cp.n_batch = n_batch > 0 ? n_batch : std::max<int>({pp, (int) toks.size(), 1});
+    cp.n_ctx = n_ctx > 0 ? n_ctx : std::max(512, (int) (pp + tg + depth + toks.size() + 64));
+    cp.n_batch = n_batch > 0 ? n_batch : std::max<int>({pp, (int) toks.size(), 1, std::min(depth, 2048)});
     cp.n_ubatch = n_ubatch > 0 ? n_ubatch : std::min<int>(512, cp.n_batch);
     if (ctk >= 0) { cp.type_k = (ggml_type) ctk; cp.type_v = (ggml_type) ctk; }
     cp.n_threads = threads;
@@ -189,12 +194,14 @@ int main(int argc, char ** argv) {
         for (int r = -1; r < reps; ++r) {   // r = -1: warmup
             if (pp > 0) {
                 llama_memory_clear(llama_get_memory(ctx), false);
+                if (depth > 0 && r >= 0) run_pp(depth);
                 const double t0 = now_s();
                 run_pp(pp);
                 if (r >= 0) pp_ts.push_back(pp / (now_s() - t0));
             }
             if (tg > 0) {
                 llama_memory_clear(llama_get_memory(ctx), false);
+                if (depth > 0 && r >= 0) run_pp(depth);
                 const double t1 = now_s();
                 run_tg(r < 0 ? 1 : tg);
                 if (r >= 0) tg_ts.push_back(tg / (now_s() - t1));
@@ -206,9 +213,9 @@ int main(int argc, char ** argv) {
             for (size_t i = 0; i < v.size(); ++i) { char b[32]; snprintf(b, sizeof(b), "%s%.3f", i ? ", " : "", v[i]); s += b; }
             return s + "]";
         };
-        printf("{\"pp\": %d, \"tg\": %d, \"threads\": %d, \"reps\": %d, \"n_batch\": %d, \"n_ubatch\": %d, \"fa\": %d, "
+        printf("{\"pp\": %d, \"tg\": %d, \"depth\": %d, \"threads\": %d, \"reps\": %d, \"n_batch\": %d, \"n_ubatch\": %d, \"fa\": %d, "
                "\"pp_tok_s\": %.3f, \"tg_tok_s\": %.3f, \"pp_samples\": %s, \"tg_samples\": %s}\n",
-               pp, tg, threads, reps, (int) cp.n_batch, (int) cp.n_ubatch, fa, mean(pp_ts), mean(tg_ts),
+               pp, tg, depth, threads, reps, (int) cp.n_batch, (int) cp.n_ubatch, fa, mean(pp_ts), mean(tg_ts),
                list(pp_ts).c_str(), list(tg_ts).c_str());
     }
     llama_free(ctx);

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 export GGML_BACKEND_PATH=$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so
 OUT=${OUT:-gpurun_out/refops}
 mkdir -p $OUT
-OPS=${OPS:-"ADD MUL SCALE RMS_NORM ROPE SOFT_MAX SET_ROWS GET_ROWS CPY CONT GLU MUL_MAT FLASH_ATTN_EXT MUL_MAT_ID ARGSORT SUM_ROWS"}
+OPS=${OPS:-"ADD MUL SCALE RMS_NORM ROPE SOFT_MAX SET_ROWS GET_ROWS CPY CONT SWIGLU,GEGLU,REGLU,GEGLU_ERF,GEGLU_QUICK MUL_MAT FLASH_ATTN_EXT MUL_MAT_ID ARGSORT SUM_ROWS"}
 for op in $OPS; do
   timeout -k 10 ${TMO:-240} oracle/_ref/test-backend-ops -b MI355X0 -o $op > $OUT/$op.log 2>&1
   rc=$?

@@ -140,8 +140,8 @@ def test_layer_split_handoff_cpy_tensor_async(tmp_path):
     assert '"mismatches": 0' in r.stdout and "MI355X" in r.stdout, r.stdout
 
 
-@pytest.mark.parametrize("incremental", [False, True])
-def test_dropin_row_split(ggufs, tmp_path, incremental):
+@pytest.mark.parametrize("incremental,no_peer", [(False, False), (True, False), (True, True)])
+def test_dropin_row_split(ggufs, tmp_path, incremental, no_peer):
     """llama -sm row -ts 1,1: libllama puts every matrix in the backend's split buffer type
     (proc ggml_backend_split_buffer_type), rows halved over two devices — here two logical
     devices of the one MI355X (GGML_MI355X_VIRTUAL_DEVICES=2) — and every MUL_MAT runs its
@@ -152,11 +152,78 @@ def test_dropin_row_split(ggufs, tmp_path, incremental):
     klog = tmp_path / "klog.txt"
     cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental)
     gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, klog=klog, extra=["-sm", "row", "-ts", "1,1"],
-                       env_extra={"GGML_MI355X_VIRTUAL_DEVICES": "2"})
+                       env_extra={"GGML_MI355X_VIRTUAL_DEVICES": "2", "GGML_MI355X_FORCE_PEER": "1",
+                                  **({"GGML_MI355X_NO_PEER": "1"} if no_peer else {})})
     assert "MI355X" in log
     assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
     kl = klog.read_text()
     assert "mm_split" in kl and "devices=2" in kl, kl[-2000:]
+    # GGML_MI355X_FORCE_PEER: the cross-device broadcast / gather branches of split.cpp ran
+    # (no_peer: the slices come back by one contiguous peer copy and a 2D copy on main)
+    assert all("peer=1" in ln and f"direct={int(not no_peer)}" in ln for ln in kl.splitlines() if ln.startswith("mm_split")), kl[-2000:]
+
+
+@pytest.mark.parametrize("ts", ["1,1", "1,1,1,1"])
+@pytest.mark.parametrize("incremental", [False, True])
+def test_dropin_layer_split(ggufs, tmp_path, ts, incremental):
+    """llama -sm layer -ts 1,1 / 1,1,1,1 (llama-bench's default split mode) over 2 or 4
+    logical devices of the one MI355X (GGML_MI355X_VIRTUAL_DEVICES): libllama gives each
+    device a contiguous layer range (src/llama-model.cpp:2599-2609) and, with every layer
+    offloaded, turns on pipeline parallelism (src/llama-context.cpp:307-334: the
+    scheduler's n_copies = 4 input copies ordered by this backend's events,
+    ggml/src/ggml-backend.cpp:1445-1629). Each boundary activation crosses through
+    be_cpy_async, forced onto its peer-copy branch (GGML_MI355X_FORCE_PEER=1) so the code a
+    real multi-GPU run takes executes here. Logits against the reference CPU backend,
+    prefill (one ubatch) and incremental decode."""
+    _need_ref()
+    n_dev = len(ts.split(","))
+    toks = np.random.default_rng(14).integers(0, 1000, 24 if incremental else 40)
+    g = ggufs[("small", "q4_k_m")]          # 4 layers: one per device at -ts 1,1,1,1
+    klog = tmp_path / "klog.txt"
+    cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental)
+    gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, klog=klog, extra=["-sm", "layer", "-ts", ts],
+                       env_extra={"GGML_MI355X_VIRTUAL_DEVICES": str(n_dev), "GGML_MI355X_FORCE_PEER": "1"})
+    assert "MI355X" in log
+    assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+    cp = [ln for ln in klog.read_text().splitlines() if ln.startswith("cpy_async")]
+    assert cp and all("peer=1" in ln for ln in cp), cp[:8]
+    for i in range(n_dev - 1):     # every layer boundary handed its activation over
+        assert any(f"MI355X{i} -> MI355X{i + 1} " in ln for ln in cp), (i, cp[:8])
+
+
+@pytest.fixture(scope="module")
+def tinyllama(tmp_path_factory):
+    path = str(tmp_path_factory.mktemp("gguf_tl") / "tinyllama_q4_0.gguf")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gguf_synth.py"), "--shape", "tinyllama",
+                    "--recipe", "q4_0", "--out", path], check=True, timeout=600)
+    return path
+
+
+def test_tinyllama_q4_0_dropin(tinyllama, tmp_path):
+    """BASELINE configs[0]: the TinyLlama-1.1B shape (2048 / 22 layers / 32 heads / 4 KV /
+    5632 / 32000) in Q4_0, the reference's CPU-runnable plumbing config (llama-bench pp64 /
+    tg32). The same libllama on the reference CPU backend (-ngl 0) and on this backend
+    (-ngl 99): logits of a 64-token prefill and of 32 incremental decode steps within the
+    whole-graph bound, then both run llama-bench's pp64 / tg32 loop."""
+    _need_ref()
+    toks = np.random.default_rng(15).integers(0, 32000, 64)
+    cpu, _ = run_ref(tmp_path, tinyllama, toks, 0, 1)
+    gpu, log = run_ref(tmp_path, tinyllama, toks, 99, 1)
+    assert "MI355X" in log
+    assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+    cpu_i, _ = run_ref(tmp_path, tinyllama, toks[:32], 0, 1, incremental=True)
+    gpu_i, _ = run_ref(tmp_path, tinyllama, toks[:32], 99, 1, incremental=True)
+    assert nmse(gpu_i, cpu_i) < TOL, nmse(gpu_i, cpu_i)
+    res = {}
+    for ngl in (0, 99):
+        env = dict(os.environ, GGML_BACKEND_PATH=LIB) if ngl else dict(os.environ)
+        r = subprocess.run([REF, "-m", tinyllama, "-t", str(min(16, os.cpu_count() or 8)), "-ngl", str(ngl), "-p", "64",
+                            "-n", "32", "-r", "2"], capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[ngl] = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        assert res[ngl]["pp_tok_s"] > 0 and res[ngl]["tg_tok_s"] > 0, res[ngl]
+    print(f"tinyllama q4_0 pp64/tg32: cpu {res[0]['pp_tok_s']:.0f}/{res[0]['tg_tok_s']:.1f}  "
+          f"mi355x {res[99]['pp_tok_s']:.0f}/{res[99]['tg_tok_s']:.1f} tok/s")
 
 
 def test_dropin_async_upload_no_mmap(ggufs, tmp_path):

@@ -9,7 +9,11 @@ Covered configs (BASELINE.json):
     LDS-DMA norm prologue, down Q4_K (layer 0) and Q6_K (layer 1), lm_head 128256);
   * Llama-3-8B pp512 (one ubatch) and pp2048 (-b 2048 -ub 512: four ubatches, the KV
     cache growing to 2048 cells; config 3) — the MFMA GEMMs and prefill attention;
-  * Mixtral-8x7B Q5_K_M (config 5): MUL_MAT_ID prefill and decode with FA.
+  * Mixtral-8x7B Q5_K_M (config 5): MUL_MAT_ID prefill and decode with FA, the fused QKV
+    on its (q Q5_K, k Q8_0, v Q8_0) recipe;
+  * Llama-3-70B Q4_K_M widths (config 4, `llama3_70b_2l`: 8192 / 64 heads / 8 KV / 28672,
+    attn_v Q5_K by the 70B rule on layer 0, Q6_K on layer 1): decode at fa 1 / fa 0 and
+    pp512, asserting the K = 8192 / 28672 instantiations.
 Besides logits, the kernel-choice log (GGML_MI355X_KLOG) shows which kernels libllama's
 graph reached, and the executor's per-token launch mix under libllama must equal the
 package runner's on the same GGUF (the fusions fire on the reference's node order).
@@ -52,6 +56,11 @@ def make_gguf(d, shape, recipe):
 @pytest.fixture(scope="module")
 def l8b(gguf_dir):
     return make_gguf(gguf_dir, "llama3_8b_2l", "q4_k_m")
+
+
+@pytest.fixture(scope="module")
+def l70b(gguf_dir):
+    return make_gguf(gguf_dir, "llama3_70b_2l", "q4_k_m")
 
 
 @pytest.fixture(scope="module")
@@ -157,6 +166,62 @@ def test_llama3_8b_width_pp512(l8b, tmp_path, fa):
         assert k["fa_mma2"] == 2, k
 
 
+def gemv_fields(klog):
+    return [dict(re.findall(r"(\w+)=(-?\d+)", ln)) for ln in klog if ln.startswith("gemv2 qt")]
+
+
+@pytest.mark.parametrize("fa", [1, 0])
+def test_llama3_70b_width_decode(l70b, tmp_path, fa):
+    """Llama-3-70B Q4_K_M widths, incremental decode through libllama. Every launch of the
+    70B decode at its shape: the fused QKV with (Q4_K, Q4_K, Q5_K) on layer 0 (the 70B
+    attn_v rule, src/llama-quant.cpp:305-310) and (Q4_K, Q4_K, Q6_K) on layer 1 at K = 8192,
+    the SwiGLU GEMV over 2 x 28672 rows (K = 8192: the LDS-DMA norm prologue would need
+    75,840 B, so x and the norm weight are staged in registers, one 16-value half per thread
+    of the 512-thread workgroup: XS_NORM = 1), the down projection at
+    K = 28672 from the SwiGLU's q8 copy (Q4_K layer 0, Q6_K layer 1), the 128256-row lm_head."""
+    toks = np.random.default_rng(31).integers(0, 128000, 8)
+    cpu, _, _ = run_ref(tmp_path, l70b, toks, 0, fa, incremental=True)
+    gpu, log, klog = run_ref(tmp_path, l70b, toks, 99, fa, incremental=True,
+                             env_extra={"GGML_MI355X_DISABLE_GRAPHS": "1"})
+    assert "MI355X" in log, log[-2000:]
+    assert np.all(np.isfinite(gpu))
+    err = nmse(gpu, cpu)
+    assert err < TOL, err
+    n, L = len(toks), 2
+    qkv = [ln for ln in klog if ln.startswith("qkv ")]
+    assert len(qkv) == n * L and all("K=8192" in ln for ln in qkv), qkv[:4]
+    assert sum("qta=12 qtk=12 qtv=13" in ln for ln in qkv) == n, qkv[:4]
+    assert sum("qta=12 qtk=12 qtv=14" in ln for ln in qkv) == n, qkv[:4]
+    g = gemv_fields(klog)
+    glu = [f for f in g if f["epi"] == "1" and f["M"] == "28672"]
+    assert len(glu) == n * L and all(f["K"] == "8192" and f["q8o"] == "1" and f["mode"] == "1" for f in glu), glu[:2]
+    down = [f for f in g if f["K"] == "28672" and f["M"] == "8192"]
+    assert len(down) == n * L and sorted({f["qt"] for f in down}) == ["12", "14"] and all(f["mode"] == "2" for f in down), down[:2]
+    lm = [f for f in g if f["M"] == "128256"]
+    assert len(lm) == n and all(f["K"] == "8192" and f["qt"] == "14" for f in lm), lm[:2]
+    k = kinds(klog)
+    assert k["mmvq1"] == 0, k
+    if fa:
+        assert k["fattn_dec2"] + k["fattn_dec"] == n * L, k
+    else:
+        assert k["attn_nofa"] == n * L, k
+
+
+@pytest.mark.parametrize("fa", [1, 0])
+def test_llama3_70b_width_pp512(l70b, tmp_path, fa):
+    """70B widths, one 512-token ubatch: the MFMA GEMMs at K = 8192 / 28672, M = 28672"""
+    toks = np.random.default_rng(32).integers(0, 128000, 512)
+    cpu, _, _ = run_ref(tmp_path, l70b, toks, 0, fa, last=16)
+    gpu, _, klog = run_ref(tmp_path, l70b, toks, 99, fa, last=16)
+    err = nmse(gpu, cpu)
+    assert err < TOL, err
+    k = kinds(klog)
+    assert k["mmq3g"] + k["mmq4 glu"] == 2, k
+    assert any(ln.startswith("mmq4 glu") and "M=28672" in ln and "K=8192" in ln for ln in klog), k
+    if fa:
+        assert k["fa_mma2"] == 2, k
+
+
 def test_llama3_8b_width_pp2048(l8b, tmp_path):
     """pp2048 as llama-bench runs it: -b 2048 -ub 512, four ubatches, causal attention over
     a KV cache growing to 2048 cells (512 queries x up to 2048 keys in the last one)"""
@@ -227,9 +292,12 @@ def test_mixtral_width_moe(mixtral, tmp_path):
     f, r = check_moe_layer0(dump_run(tmp_path, mixtral, t2, 0, "i", True), dump_run(tmp_path, mixtral, t2, 99, "i", True))
     print(f"decode: {f} of {r} layer-0 expert rows flipped")
     cpu_i, _, _ = run_ref(tmp_path, mixtral, t2, 0, 1, incremental=True, tag="i")
-    gpu_i, _, _ = run_ref(tmp_path, mixtral, t2, 99, 1, incremental=True, tag="i")
+    gpu_i, _, klog_i = run_ref(tmp_path, mixtral, t2, 99, 1, incremental=True, tag="i",
+                               env_extra={"GGML_MI355X_DISABLE_GRAPHS": "1"})
     per = [nmse(g, c) for g, c in zip(gpu_i, cpu_i)]
     assert np.median(per) < MOE_TOL, per
+    qkv = [ln for ln in klog_i if ln.startswith("qkv ")]
+    assert len(qkv) == 2 * len(t2) and all("qta=13 qtk=8 qtv=8" in ln for ln in qkv), (qkv[:4], klog_i[:20])
 
 
 def test_runner_launch_mix_equals_dropin(pkg, backend, l8b, tmp_path):

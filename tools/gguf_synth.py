@@ -33,6 +33,11 @@ SHAPES = {
                          n_ctx=8192, rope_base=500000.0),
     "llama3_70b": dict(n_vocab=128256, n_embd=8192, n_layer=80, n_head=64, n_head_kv=8, n_ff=28672,
                        n_ctx=8192, rope_base=500000.0),
+    # Llama-3-70B widths over two layers, with the 70B model's attn_v rule (LLM_TYPE_70B
+    # is an 80-layer model, so the flag stands in for the layer count): layer 0 attn_v Q5_K,
+    # layer 1 (use_more_bits) attn_v / ffn_down Q6_K
+    "llama3_70b_2l": dict(n_vocab=128256, n_embd=8192, n_layer=2, n_head=64, n_head_kv=8, n_ff=28672,
+                          n_ctx=8192, rope_base=500000.0, rule70b=True),
     "mixtral_8x7b": dict(n_vocab=32000, n_embd=4096, n_layer=32, n_head=32, n_head_kv=8, n_ff=14336,
                          n_ctx=32768, rope_base=1e6, n_expert=8, n_expert_used=2),
     "mixtral_2l": dict(n_vocab=32000, n_embd=4096, n_layer=2, n_head=32, n_head_kv=8, n_ff=14336,
@@ -62,7 +67,7 @@ def tensor_plan(s, recipe):
         # Q4_K -> Q5_K (:305-310)
         if n_exp == 8 and kind in ("k", "v") and recipe in ("q4_k_m", "q5_k_m"):
             return "q8_0"
-        if kind == "v" and recipe == "q4_k_m" and E == 8192 and L == 80 and not use_more_bits(i, L):
+        if kind == "v" and recipe == "q4_k_m" and (s.get("rule70b") or (E == 8192 and L == 80)) and not use_more_bits(i, L):
             return "q5_K"
         if recipe == "q4_k_m":
             return "q6_K" if kind in ("v", "down") and use_more_bits(i, L) else "q4_K"
