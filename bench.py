@@ -166,6 +166,17 @@ def host_threads():
     return int(os.environ.get("MX_CPU_THREADS", n))
 
 
+def cpu_model():
+    """lscpu's model name (record the host CPU beside the baseline)"""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(args):
     """Reference CPU backend (oracle/_ref, built from /root/reference sources) on the same
     GGUF, bounded sample, every CPU thread this process is granted (-t nproc).
@@ -176,16 +187,28 @@ def cpu_baseline(args):
     try:
         gguf = bench_gguf()
         r = subprocess.run([REF_BENCH, "-m", gguf, "-t", str(threads), "-p", str(args.cpu_pp), "-n", str(args.cpu_tg),
-                            "-r", "1"], capture_output=True, text=True, timeout=900)
+                            "-r", str(args.cpu_reps)], capture_output=True, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         res = json.loads(line)
         return {"value": res["tg_tok_s"], "unit": "tok/s", "cores": threads, "kind": "reference",
-                "pp_tok_s": res.get("pp_tok_s"),
+                "pp_tok_s": res.get("pp_tok_s"), "tg_samples": res.get("tg_samples"), "pp_samples": res.get("pp_samples"),
+                "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
                 "sample": f"reference CPU backend (libllama+ggml-cpu from /root/reference), same GGUF, "
-                          f"tg{args.cpu_tg} and pp{args.cpu_pp} after one warmup each, {threads} threads "
-                          f"(os.cpu_count() = {os.cpu_count()})"}
+                          f"tg{args.cpu_tg} and pp{args.cpu_pp}, one warmup then {args.cpu_reps} repetitions each "
+                          f"(llama-bench's loop), {threads} threads (the cgroup CPU quota of os.cpu_count() = "
+                          f"{os.cpu_count()})"}
     except Exception as e:  # noqa: BLE001 — the GPU number stays valid without the baseline
         return {"value": None, "unit": "tok/s", "cores": threads, "kind": "reference", "sample": f"failed: {e}"}
+
+
+def ref_bench(gguf, env, flags, timeout=900):
+    """one ref-llama-bench run -> its JSON line (or an error string)"""
+    r = subprocess.run([REF_BENCH, "-m", gguf] + [str(f) for f in flags], capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not line:
+        return f"failed rc={r.returncode}: {r.stderr[-300:]}", r.stderr
+    return json.loads(line[-1]), r.stderr
 
 
 def dropin_bench(args):
@@ -194,8 +217,9 @@ def dropin_bench(args):
     tools/llama-bench/llama-bench.cpp:1962-2010, warmup + -r repetitions) loads
     libggml-mi355x.so through GGML_BACKEND_PATH with every layer offloaded (-ngl 99), on
     the same Llama-3-8B Q4_K_M GGUF. Reports tg128 and pp512 at -fa 1 and -fa 0, at -fa 1
-    with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv) and the executor's counters per
-    llama_decode."""
+    with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv), pp2048 (-b 2048 -ub 512,
+    BASELINE configs[2]), tg128 at depth (-d: llama-bench.cpp:2191-2226, the KV cache
+    filled with D tokens first) and the executor's counters per llama_decode."""
     if not os.path.exists(REF_BENCH) or args.no_dropin:
         return None
     out = {"how": "reference libllama (oracle/_ref/ref-llama-bench) + GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, "
@@ -203,24 +227,59 @@ def dropin_bench(args):
     try:
         gguf = bench_gguf()
         env = dict(os.environ, GGML_BACKEND_PATH=LIB, GGML_MI355X_STATS="1")
+        base = ["-t", "8", "-ngl", "99", "-r", args.dropin_reps]
+        runs = []
         for fa, ctk in ((1, None), (0, None), (1, 8)):        # 8 = GGML_TYPE_Q8_0
             for test, pp, tg in (("tg128", 0, args.tg), ("pp512", args.pp, 0)):
                 if (pp or tg) == 0:
                     continue
                 key = f"{test}_fa{fa}" + ("_q8kv" if ctk else "")
-                r = subprocess.run([REF_BENCH, "-m", gguf, "-t", "8", "-ngl", "99", "-fa", str(fa), "-p", str(pp),
-                                    "-n", str(tg), "-r", str(args.dropin_reps), "-c", str(max(256, pp + tg))] +
-                                   (["-ctk", str(ctk)] if ctk else []),
-                                   capture_output=True, text=True, timeout=900, env=env)
-                line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-                if r.returncode != 0 or not line:
-                    out[key] = f"failed rc={r.returncode}: {r.stderr[-300:]}"
-                    continue
-                res = json.loads(line[-1])
-                out[f"{key}_tok_s"] = res["tg_tok_s"] if tg else res["pp_tok_s"]
-                st = [json.loads(s.split("stats ", 1)[1]) for s in r.stderr.splitlines() if "[mi355x] stats" in s]
-                if st and tg:
-                    out[f"{key}_executor"] = st[0]
+                runs.append((key, tg > 0, ["-fa", fa, "-p", pp, "-n", tg, "-c", max(256, pp + tg)] +
+                             (["-ctk", ctk] if ctk else [])))
+        if args.pp2048:
+            for fa in (1, 0):
+                runs.append((f"pp2048_fa{fa}", False, ["-fa", fa, "-p", 2048, "-n", 0, "-b", 2048, "-ub", 512, "-c", 2304]))
+        for d in args.depths:
+            runs.append((f"tg128_d{d}_fa1", True, ["-fa", 1, "-p", 0, "-n", args.tg, "-d", d, "-c", d + args.tg + 256]))
+        for key, is_tg, flags in runs:
+            res, err = ref_bench(gguf, env, base + flags)
+            if isinstance(res, str):
+                out[key] = res
+                continue
+            out[f"{key}_tok_s"] = res["tg_tok_s"] if is_tg else res["pp_tok_s"]
+            out[f"{key}_samples"] = res["tg_samples"] if is_tg else res["pp_samples"]
+            st = [json.loads(s.split("stats ", 1)[1]) for s in err.splitlines() if "[mi355x] stats" in s]
+            if st and is_tg and key == "tg128_fa1":
+                out[f"{key}_executor"] = st[0]
+    except Exception as e:  # noqa: BLE001
+        out["error"] = str(e)
+    return out
+
+
+def dropin_layer_split(args, world):
+    """N > 1: libllama's own layer split as llama-bench -sm layer measures it — ONE process
+    (rank 0's child) drives the first N GPUs through this backend, contiguous layer ranges
+    per device, boundary activations by cpy_tensor_async (hipMemcpyPeerAsync over xGMI),
+    pipeline parallelism on (src/llama-context.cpp:307-334). tg128 and pp512 at -fa 1."""
+    if not os.path.exists(REF_BENCH) or args.no_dropin:
+        return None
+    vis = os.environ.get("HIP_VISIBLE_DEVICES")
+    devs = vis.split(",")[:world] if vis else [str(i) for i in range(world)]
+    env = dict(os.environ, GGML_BACKEND_PATH=LIB, HIP_VISIBLE_DEVICES=",".join(devs))
+    out = {"how": f"reference libllama -sm layer -ts 1x{world} over HIP devices {','.join(devs)}, -ngl 99, -fa 1, "
+                  f"-r {args.dropin_reps}"}
+    try:
+        gguf = bench_gguf()
+        ts = ",".join(["1"] * world)
+        for key, is_tg, flags in (("tg128", True, ["-p", 0, "-n", args.tg, "-c", 256]),
+                                  ("pp512", False, ["-p", args.pp, "-n", 0, "-c", max(512, args.pp)])):
+            res, _ = ref_bench(gguf, env, ["-t", "8", "-ngl", "99", "-fa", "1", "-sm", "layer", "-ts", ts,
+                                           "-r", args.dropin_reps] + flags)
+            if isinstance(res, str):
+                out[key] = res
+                continue
+            out[f"{key}_tok_s"] = res["tg_tok_s"] if is_tg else res["pp_tok_s"]
+            out[f"{key}_samples"] = res["tg_samples"] if is_tg else res["pp_samples"]
     except Exception as e:  # noqa: BLE001
         out["error"] = str(e)
     return out
@@ -339,9 +398,13 @@ def main():
     ap.add_argument("--no-fa", action="store_true", help="llama-bench -fa 0 graph (KQ mul_mat + softmax)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the reference-libllama drop-in measurement")
-    ap.add_argument("--dropin-reps", type=int, default=3)
-    ap.add_argument("--cpu-pp", type=int, default=32)
-    ap.add_argument("--cpu-tg", type=int, default=16)
+    ap.add_argument("--dropin-reps", type=int, default=5, help="llama-bench -r (SURVEY §8d: 5)")
+    ap.add_argument("--depths", type=lambda v: [int(x) for x in v.split(",") if x], default=[4096, 16384],
+                    help="drop-in tg128 at these KV depths (llama-bench -d), comma list, '' for none")
+    ap.add_argument("--no-pp2048", dest="pp2048", action="store_false", help="skip the pp2048 legs (BASELINE configs[2])")
+    ap.add_argument("--cpu-pp", type=int, default=64)
+    ap.add_argument("--cpu-tg", type=int, default=32)
+    ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--skip-roofline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing (for scripts/pmc_roofline.sh's rocprofv3 --pmc passes)")
@@ -441,6 +504,21 @@ def main():
                 sess.decode(toks)
             be.synchronize()
             pp_tok_s = reps * args.pp / (time.perf_counter() - t1)
+    # pp2048 (BASELINE configs[2]): llama-bench -p 2048 -b 2048 -ub 512, four 512-token
+    # ubatches into a cache growing to 2048 cells; single GPU only
+    pp2048_tok_s = None
+    if args.pp2048 and mode != "pipeline" and args.pp > 0:
+        sess.free()
+        sess = pkg.Session(model, n_ctx=2304, n_ubatch=512, flash_attn=not args.no_fa)
+        toks = rng.integers(0, n_vocab, size=2048, dtype=np.int32)
+        sess.reset(); sess.decode(toks)
+        be.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(2):
+            sess.reset()
+            sess.decode(toks)
+        be.synchronize()
+        pp2048_tok_s = 2 * 2048 / (time.perf_counter() - t1)
 
     stats = be.stats()
     # weights one decoded token reads (all stages together)
@@ -448,6 +526,9 @@ def main():
     roof = None if (args.skip_roofline or shape.get("n_expert")) else roofline_glu(pkg, be, model)
     cpu = cpu_baseline(args) if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
     dropin = dropin_bench(args) if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
+    barrier(dist, local)
+    split_leg = dropin_layer_split(args, world) if (rank == 0 and world > 1 and args.model == "llama3_8b") else None
+    barrier(dist, local)
 
     if rank == 0:
         per_gpu_bytes_s = decode_bytes * tg_value / world
@@ -470,6 +551,7 @@ def main():
                        "model_shape": args.model, "recipe": recipe, "tg": args.tg, "pp": args.pp,
                        "flash_attn": not args.no_fa, "parallelism": par},
             "pp512_tok_s": round(pp_tok_s, 1) if pp_tok_s else None,
+            "pp2048_tok_s": round(pp2048_tok_s, 1) if pp2048_tok_s else None,
             "pp_roofline": ({"bound": "mfma", "achieved": round(pp_tok_s * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world, 1),
                              "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
                              "frac": round(pp_tok_s * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world / MFMA_F16_PEAK_TFS, 4),
@@ -481,6 +563,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "dropin": dropin,
+            "dropin_layer_split": split_leg,
             "pipelined": pipelined,
             "executor": stats,
         }

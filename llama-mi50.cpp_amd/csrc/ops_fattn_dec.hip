@@ -567,7 +567,13 @@ static const ggml_tensor * nf_base(const ggml_tensor * t) {
     return t;
 }
 
-// returns the number of graph nodes consumed from i (0: no match)
+static const bool g_no_attn_nofa_pp = getenv("GGML_MI355X_NO_ATTN_FUSION_PP") != nullptr;   // A/B: prefill chain node by node
+void fa_mma_nofa_launch(OpCtx & c, const ggml_tensor * q, const ggml_tensor * k, const ggml_tensor * v, const ggml_tensor * m,
+                        float scale, ggml_tensor * out);   // ops_fattn_mma.hip
+
+// returns the number of graph nodes consumed from i (0: no match). One query token: the
+// decode kernel above; n_q >= 16 (prefill ubatches): the transposed-V MFMA flash kernel
+// (fa_mma_nofa_launch), D = 128, n_kv % 64 == 0 (libllama pads the cache view to 256).
 int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
     auto use = [&](const ggml_tensor * t) { auto it = uses.find(t); return it == uses.end() ? 0 : it->second; };
     ggml_tensor * kq = g->nodes[i];
@@ -575,12 +581,16 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
     const ggml_tensor * k = kq->src[0], * q = kq->src[1];
     if (k->type != GGML_TYPE_F16 || q->type != GGML_TYPE_F32 || kq->type != GGML_TYPE_F32) return 0;
     const int D = (int) k->ne[0];
-    if ((D != 64 && D != 128) || q->ne[0] != D || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1) return 0;
+    const int n_q = (int) q->ne[1];
+    const bool pre = n_q >= 16 && !g_no_attn_nofa_pp;
+    if (!pre && n_q != 1) return 0;
+    if ((D != 64 && D != 128) || (pre && D != 128) || q->ne[0] != D || q->ne[3] != 1 || k->ne[3] != 1) return 0;
     const int n_kv = (int) k->ne[1], H = (int) q->ne[2], Hkv = (int) k->ne[2];
-    // P·V: 256/D threads per dimension, each a contiguous key range stepped by 8 keys
+    // decode P·V: 256/D threads per dimension, each a contiguous key range stepped by 8 keys
     // (16-byte V loads), so n_kv must split into 256/D parts of a multiple of 8 keys
-    if (H % Hkv || n_kv % (8 * (256 / D)) || n_kv > NF_MAX_KV || k->nb[0] != 2 || k->nb[1] % 16 || k->nb[2] % 16 || (uintptr_t) k->data % 16) return 0;
-    if (q->nb[0] != 4 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return 0;
+    if (H % Hkv || k->nb[0] != 2 || k->nb[1] % 16 || k->nb[2] % 16 || (uintptr_t) k->data % 16) return 0;
+    if (pre ? (n_kv % 64 || n_kv < 64) : (n_kv % (8 * (256 / D)) || n_kv > NF_MAX_KV)) return 0;
+    if (q->nb[0] != 4 || q->nb[2] % 16 || (uintptr_t) q->data % 16 || (pre && q->nb[1] % 16)) return 0;
     ggml_tensor * sm = nullptr, * kqv = nullptr, * out = nullptr;
     int last = i;
     for (int j = i + 1; j < g->n_nodes && j < i + 12; ++j) {
@@ -595,16 +605,19 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
     if (!sm || !kqv || !out) return 0;
     // the softmax: plain scale + mask, no ALiBi / sinks
     if (sm->src[2] || mx_op_param<float>(sm, 1) != 0.0f || sm->type != GGML_TYPE_F32 || !mx_is_contiguous(sm)) return 0;
+    if (kq->ne[0] != n_kv || kq->ne[1] != n_q || kq->ne[2] != H) return 0;
     const ggml_tensor * m = sm->src[1];
     if (m && ((m->type != GGML_TYPE_F16 && m->type != GGML_TYPE_F32) || m->ne[0] < n_kv || !mx_is_contiguous(m))) return 0;
+    if (m && pre && (m->ne[1] < n_q || m->ne[2] != 1 || m->ne[3] != 1 || m->nb[1] % 16 || (uintptr_t) m->data % 16)) return 0;
+    if (m && pre && m->type == GGML_TYPE_F32 && c.scratch->avail() < (size_t) n_kv * n_q * 2 + 256) return 0;
     // v: the transposed cache view [n_kv, D, Hkv], contiguous keys per dimension
     const ggml_tensor * v = kqv->src[0];
     if (v->type != GGML_TYPE_F16 || v->ne[0] != n_kv || v->ne[1] != D || v->ne[2] != Hkv || v->ne[3] != 1 || v->nb[0] != 2) return 0;
     if (v->nb[1] % 16 || v->nb[2] % 16 || (uintptr_t) v->data % 16) return 0;
-    if (kqv->ne[0] != D || kqv->ne[1] != 1 || kqv->ne[2] != H || kqv->type != GGML_TYPE_F32) return 0;
-    if (out->type != GGML_TYPE_F32 || !mx_is_contiguous(out) || mx_nelements(out) != (int64_t) D * H) return 0;
-    const ggml_tensor * pm = out->src[0];   // permute(kqv, 0, 2, 1, 3): element (d, h) -> out[h * D + d]
-    if (pm->ne[0] != D || pm->ne[1] != H || pm->nb[1] != kqv->nb[2]) return 0;
+    if (kqv->ne[0] != D || kqv->ne[1] != n_q || kqv->ne[2] != H || kqv->type != GGML_TYPE_F32) return 0;
+    if (out->type != GGML_TYPE_F32 || !mx_is_contiguous(out) || mx_nelements(out) != (int64_t) D * H * n_q) return 0;
+    const ggml_tensor * pm = out->src[0];   // permute(kqv, 0, 2, 1, 3): element (d, h, t) -> out[(t H + h) D + d]
+    if (pm->ne[0] != D || pm->ne[1] != H || pm->ne[2] != n_q || pm->nb[1] != kqv->nb[2] || pm->nb[2] != kqv->nb[1]) return 0;
     // intermediates read only inside the chain, nothing else in between
     if (use(kq) != 1 || use(sm) != 1 || ((kq->flags | sm->flags | kqv->flags) & GGML_TENSOR_FLAG_OUTPUT)) return 0;
     for (int j = i + 1; j <= last; ++j) {
@@ -616,6 +629,14 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         for (int j = last + 1; j < g->n_nodes; ++j)
             for (int s2 = 0; s2 < GGML_MAX_SRC; ++s2)
                 if (g->nodes[j]->src[s2] && nf_base(g->nodes[j]->src[s2]) == t) return 0;
+    if (pre) {
+        for (int j = i; j <= last; ++j) {
+            deferred_guard_node_ext(c, g->nodes[j]);
+            act_cache_invalidate(c.s, g->nodes[j]);
+        }
+        fa_mma_nofa_launch(c, q, k, v, m, mx_op_param<float>(sm, 0), out);
+        return last - i + 1;
+    }
     NfArgs a{};
     a.q = (const char *) q->data; a.q2 = q->nb[2];
     a.k = (const char *) k->data; a.k1 = k->nb[1]; a.k2 = k->nb[2];

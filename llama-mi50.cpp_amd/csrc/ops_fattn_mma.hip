@@ -243,8 +243,13 @@ __device__ __forceinline__ fhalf4 lds_tr16(const char * a) {   // ds_read_b64_tr
 __device__ __forceinline__ int fm2_off(int row, int ch) {     // byte offset in a 256-B-row tile
     return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
+// V^T tile (VT: the non-flash-attention path's transposed V cache, src/llama-kv-cache.cpp
+// cpy_v with v_trans): 128 dimension rows x 64 keys (128 B), 8-byte chunks of 4 keys
+// XOR-swizzled by (row >> 1) & 15, so the 32 rows one half-wave reads with ds_read_b64 at
+// one key chunk fall on 32 distinct bank pairs
+__device__ __forceinline__ int vt_off(int row, int q) { return 128 * row + 8 * (q ^ ((row >> 1) & 15)); }
 
-template <int HG>
+template <int HG, bool VT = false>
 __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
     constexpr int D = 128, NKS = D / 16, NDT = D / 32;
     constexpr int QB = 32 * (4 / HG);                          // queries per workgroup
@@ -309,17 +314,27 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
     };
     // K/V tile rows, 16 B per thread per instruction: 16 threads read one 256-B row
     // (unconditional: a load under a branch would make the loop-carried registers a
-    // scratch array; a dead tile reads one 16-B chunk for the whole workgroup instead)
+    // scratch array; a dead tile reads one 16-B chunk for the whole workgroup instead).
+    // VT: V^T rows (one per dimension, 64 keys = 128 B, p.v1 = the dimension stride): thread
+    // tid + 256 j loads keys 8 (u & 7) .. +7 of dimension u >> 3 (n_kv % 64 == 0: no clamp)
     uint4 kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3;
+#define FM2_VT_SRC(KT, J) (vb + ((size_t) ((tid + 256 * (J)) >> 3) * p.v1 + (size_t) (2 * ((KT) * FM_KT + 8 * ((tid + 256 * (J)) & 7)))))
 #define FM2_LOAD_KV(KT, LIVE) do { \
         const int kt_ = (KT); const bool lv_ = (LIVE); \
         const size_t r0_ = (size_t) min(kt_ * FM_KT + (tid >> 4), p.n_kv - 1), r1_ = (size_t) min(kt_ * FM_KT + 16 + (tid >> 4), p.n_kv - 1); \
         const size_t r2_ = (size_t) min(kt_ * FM_KT + 32 + (tid >> 4), p.n_kv - 1), r3_ = (size_t) min(kt_ * FM_KT + 48 + (tid >> 4), p.n_kv - 1); \
         const int c_ = 16 * (tid & 15); \
-        kr0 = *(const uint4 *) (kb + (lv_ ? r0_ * p.k1 + c_ : 0)); vr0 = *(const uint4 *) (vb + (lv_ ? r0_ * p.v1 + c_ : 0)); \
-        kr1 = *(const uint4 *) (kb + (lv_ ? r1_ * p.k1 + c_ : 0)); vr1 = *(const uint4 *) (vb + (lv_ ? r1_ * p.v1 + c_ : 0)); \
-        kr2 = *(const uint4 *) (kb + (lv_ ? r2_ * p.k1 + c_ : 0)); vr2 = *(const uint4 *) (vb + (lv_ ? r2_ * p.v1 + c_ : 0)); \
-        kr3 = *(const uint4 *) (kb + (lv_ ? r3_ * p.k1 + c_ : 0)); vr3 = *(const uint4 *) (vb + (lv_ ? r3_ * p.v1 + c_ : 0)); \
+        kr0 = *(const uint4 *) (kb + (lv_ ? r0_ * p.k1 + c_ : 0)); \
+        kr1 = *(const uint4 *) (kb + (lv_ ? r1_ * p.k1 + c_ : 0)); \
+        kr2 = *(const uint4 *) (kb + (lv_ ? r2_ * p.k1 + c_ : 0)); \
+        kr3 = *(const uint4 *) (kb + (lv_ ? r3_ * p.k1 + c_ : 0)); \
+        if constexpr (VT) { \
+            vr0 = *(const uint4 *) (lv_ ? FM2_VT_SRC(kt_, 0) : vb); vr1 = *(const uint4 *) (lv_ ? FM2_VT_SRC(kt_, 1) : vb); \
+            vr2 = *(const uint4 *) (lv_ ? FM2_VT_SRC(kt_, 2) : vb); vr3 = *(const uint4 *) (lv_ ? FM2_VT_SRC(kt_, 3) : vb); \
+        } else { \
+            vr0 = *(const uint4 *) (vb + (lv_ ? r0_ * p.v1 + c_ : 0)); vr1 = *(const uint4 *) (vb + (lv_ ? r1_ * p.v1 + c_ : 0)); \
+            vr2 = *(const uint4 *) (vb + (lv_ ? r2_ * p.v1 + c_ : 0)); vr3 = *(const uint4 *) (vb + (lv_ ? r3_ * p.v1 + c_ : 0)); \
+        } \
     } while (0)
 
     ffloat16v acc_o[NDT];                                       // O^T: column = query l32
@@ -342,10 +357,24 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
         fix_mask(kt, mA);
         {
             const int row = tid >> 4, ch = tid & 15;
-            *(uint4 *) (ks + fm2_off(row, ch)) = kr0; *(uint4 *) (vs + fm2_off(row, ch)) = vr0;
-            *(uint4 *) (ks + fm2_off(row + 16, ch)) = kr1; *(uint4 *) (vs + fm2_off(row + 16, ch)) = vr1;
-            *(uint4 *) (ks + fm2_off(row + 32, ch)) = kr2; *(uint4 *) (vs + fm2_off(row + 32, ch)) = vr2;
-            *(uint4 *) (ks + fm2_off(row + 48, ch)) = kr3; *(uint4 *) (vs + fm2_off(row + 48, ch)) = vr3;
+            *(uint4 *) (ks + fm2_off(row, ch)) = kr0;
+            *(uint4 *) (ks + fm2_off(row + 16, ch)) = kr1;
+            *(uint4 *) (ks + fm2_off(row + 32, ch)) = kr2;
+            *(uint4 *) (ks + fm2_off(row + 48, ch)) = kr3;
+            if constexpr (VT) {
+                const uint4 vv[4] = {vr0, vr1, vr2, vr3};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int u = tid + 256 * j, d = u >> 3, c = u & 7;
+                    *(uint2 *) (vs + vt_off(d, 2 * c)) = make_uint2(vv[j].x, vv[j].y);
+                    *(uint2 *) (vs + vt_off(d, 2 * c + 1)) = make_uint2(vv[j].z, vv[j].w);
+                }
+            } else {
+                *(uint4 *) (vs + fm2_off(row, ch)) = vr0;
+                *(uint4 *) (vs + fm2_off(row + 16, ch)) = vr1;
+                *(uint4 *) (vs + fm2_off(row + 32, ch)) = vr2;
+                *(uint4 *) (vs + fm2_off(row + 48, ch)) = vr3;
+            }
         }
         const bool live_cur = __syncthreads_or(any_live(mA));   // + the tiles are visible
         FM2_LOAD_KV(min(kt + 1, n_tiles - 1), true);
@@ -413,9 +442,16 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
                 const int r0 = 32 * (s >> 1) + 16 * (s & 1) + 4 * (g >> 1) + iq;
 #pragma unroll
                 for (int t = 0; t < NDT; ++t) {
-                    const int c0 = 4 * t + 2 * (g & 1) + (ip >> 1);
-                    const fhalf4 lo = lds_tr16(vs + fm2_off(r0, c0) + 8 * (ip & 1));
-                    const fhalf4 hi = lds_tr16(vs + fm2_off(r0 + 8, c0) + 8 * (ip & 1));
+                    fhalf4 lo, hi;
+                    if constexpr (VT) {   // A row = dimension 32 t + l32; its keys 4 hl + (0..3) and 8 + 4 hl + (0..3)
+                        const int d = 32 * t + l32, q = 8 * (s >> 1) + 4 * (s & 1) + hl;
+                        lo = *(const fhalf4 *) (vs + vt_off(d, q));
+                        hi = *(const fhalf4 *) (vs + vt_off(d, q + 2));
+                    } else {
+                        const int c0 = 4 * t + 2 * (g & 1) + (ip >> 1);
+                        lo = lds_tr16(vs + fm2_off(r0, c0) + 8 * (ip & 1));
+                        hi = lds_tr16(vs + fm2_off(r0 + 8, c0) + 8 * (ip & 1));
+                    }
                     const fhalf8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                     acc_o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pb[s], acc_o[t], 0, 0, 0);
                 }
@@ -446,6 +482,7 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
         }
     }
 #undef FM2_LOAD_KV
+#undef FM2_VT_SRC
 }
 
 bool fa_mma_ok(const ggml_tensor * dst) {
@@ -509,6 +546,55 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
     MX_KLOG("fa_mma D=%d n_q=%d n_kv=%d", (int) k->ne[0], p.n_q, p.n_kv);
     if (k->ne[0] == 64) k_fa_mma<64><<<grid, 128, 0, c.st>>>(p);
     else k_fa_mma<128><<<grid, 128, 0, c.st>>>(p);
+}
+
+// llama-bench's default -fa 0 prefill: the node chain MUL_MAT(k, q) -> SOFT_MAX(mask, scale)
+// -> MUL_MAT(v^T, kq) -> PERMUTE -> CONT (src/llama-graph.cpp:1740-1796) for n_q >= 16 query
+// rows in one k_fa_mma2<HG, VT = true> launch (exec: fuse_attn_nofa). Semantics per node:
+// kq = K·f16(q) with f32 accumulation (the first mul_mat's vec_dot_type conversion), the
+// softmax of kq·scale + mask, kqv = V^T·f16(p). The kernel's softmax is the online form of
+// the flash-attention path (exp in the log2 domain, P rounded to f16 before normalisation
+// instead of after: both round each probability once to f16, NMSE ~1e-7 against the chain).
+// The f32 mask of the non-FA graph is converted to the f16 mask the kernel reads — what
+// libllama's flash-attention graph does with ggml_cast(kq_mask, F16) (llama-graph.cpp);
+// exact for llama's 0 / -inf masks. dst: [D, H, n_q] contiguous (the CONT's output).
+__global__ void k_mask_to_f16(const char * m, size_t m1, int n_kv, int n_q, uint16_t * out) {
+    const int q = blockIdx.y, i = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i >= n_kv) return;
+    const float4 v = *(const float4 *) (m + (size_t) q * m1 + (size_t) i * 4);
+    uint2 h;
+    h.x = (uint32_t) f2h(v.x) | ((uint32_t) f2h(v.y) << 16);
+    h.y = (uint32_t) f2h(v.z) | ((uint32_t) f2h(v.w) << 16);
+    *(uint2 *) (out + (size_t) q * n_kv + i) = h;
+}
+
+void fa_mma_nofa_launch(OpCtx & c, const ggml_tensor * q, const ggml_tensor * k, const ggml_tensor * v, const ggml_tensor * m,
+                        float scale, ggml_tensor * out) {
+    FaMmaArgs p{};
+    const int D = (int) k->ne[0];
+    p.q = (const char *) q->data; p.q1 = q->nb[1]; p.q2 = q->nb[2];
+    p.k = (const char *) k->data; p.k1 = k->nb[1]; p.k2 = k->nb[2];
+    p.v = (const char *) v->data; p.v1 = v->nb[1]; p.v2 = v->nb[2];   // v: [n_kv, D, Hkv], keys contiguous
+    p.n_q = (int) q->ne[1]; p.n_kv = (int) k->ne[1]; p.H = (int) q->ne[2]; p.Hkv = (int) k->ne[2];
+    p.scale = scale;
+    if (m) {
+        if (m->type == GGML_TYPE_F32) {
+            uint16_t * m16 = (uint16_t *) c.scratch->take((size_t) p.n_kv * p.n_q * 2);
+            k_mask_to_f16<<<dim3((unsigned) mx_ceil_div(p.n_kv / 4, 256), (unsigned) p.n_q), 256, 0, c.st>>>(
+                (const char *) m->data, m->nb[1], p.n_kv, p.n_q, m16);
+            p.mask = (const char *) m16; p.m1 = (size_t) p.n_kv * 2;
+        } else {
+            p.mask = (const char *) m->data; p.m1 = m->nb[1];
+        }
+    }
+    p.dst = (char *) out->data; p.d1 = (size_t) D * 4; p.d2 = (size_t) D * 4 * p.H;
+    p.h = mmq_act_claim(c, out->data, (int64_t) D * p.H, p.n_q, p.d2);
+    const int Gt = p.H / p.Hkv, HG = Gt % 4 == 0 ? 4 : (Gt % 2 == 0 ? 2 : 1);
+    const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32 * (4 / HG)), (unsigned) (p.Hkv * (Gt / HG)));
+    MX_KLOG("attn_nofa_mma HG=%d n_q=%d n_kv=%d H=%d Hkv=%d mask=%d", HG, p.n_q, p.n_kv, p.H, p.Hkv, m ? (int) m->type : -1);
+    if (HG == 4) k_fa_mma2<4, true><<<g2, 256, 0, c.st>>>(p);
+    else if (HG == 2) k_fa_mma2<2, true><<<g2, 256, 0, c.st>>>(p);
+    else k_fa_mma2<1, true><<<g2, 256, 0, c.st>>>(p);
 }
 
 }  // namespace mx

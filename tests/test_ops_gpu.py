@@ -530,3 +530,49 @@ def test_attn_nofa_decode_chain(pkg, backend, n_kv, H, Hkv, D, mask_t):
         pr = (e / e.sum()).astype(np.float16).astype(np.float64)
         ref[h] = vt[h // G].astype(np.float64) @ pr
     assert nmse(y, ref) < 1e-6, nmse(y, ref)
+
+
+@pytest.mark.parametrize("n_q,n_kv,H,Hkv,mask_t", [(512, 512, 32, 8, "f32"), (64, 256, 8, 8, "f16"), (100, 192, 16, 4, "f32"),
+                                                   (512, 2048, 32, 8, "f32")])
+def test_attn_nofa_prefill_chain(pkg, backend, n_q, n_kv, H, Hkv, mask_t):
+    """-fa 0 prefill attention (llama-bench's default): the same node chain as the decode
+    case with n_q query rows, run as one transposed-V MFMA flash kernel (k_fa_mma2<HG, VT>,
+    klog attn_nofa_mma) against the node-by-node semantics in float64 (q and p rounded to
+    f16 as the mul_mats convert them). Causal mask with the queries at the end of the cache
+    (the prefill of a later ubatch), f32 as libllama's non-FA graph builds it or f16."""
+    D = 128
+    rng = np.random.default_rng(n_q + n_kv + H)
+    q = rng.standard_normal((H, n_q, D)).astype(np.float32)
+    k = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16)
+    vt = rng.standard_normal((Hkv, D, n_kv)).astype(np.float16)
+    mask = np.zeros((n_q, n_kv), np.float32)
+    for i in range(n_q):
+        mask[i, n_kv - n_q + i + 1:] = -np.inf
+    scale = 1.0 / np.sqrt(D)
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, n_q, H)
+        tk = ctx.new_tensor("f16", D, n_kv, Hkv)
+        tv = ctx.new_tensor("f16", n_kv, D, Hkv)
+        tm = ctx.new_tensor(mask_t, n_kv, n_q)
+        kq = ctx.mul_mat(tk, tq)
+        sm = ctx.soft_max_ext(kq, tm, scale)
+        kqv = ctx.mul_mat(tv, sm)
+        out = ctx.cont(ctx.permute(kqv, 0, 2, 1, 3))
+        feed = [(tq, q), (tk, k.view(np.uint16)), (tv, vt.view(np.uint16)),
+                (tm, mask if mask_t == "f32" else mask.astype(np.float16).view(np.uint16))]
+        return [out], feed
+
+    backend.klog(True)
+    y = run(pkg, backend, build)[0].reshape(n_q, H, D)
+    log = backend.klog_read()
+    backend.klog(False)
+    assert any(ln.startswith("attn_nofa_mma") for ln in log), log
+    G = H // Hkv
+    ref = np.empty((n_q, H, D))
+    for h in range(H):
+        s = (q[h].astype(np.float16).astype(np.float64) @ k[h // G].astype(np.float64).T) * scale + mask
+        e = np.exp(s - s.max(1, keepdims=True))
+        pr = (e / e.sum(1, keepdims=True)).astype(np.float16).astype(np.float64)
+        ref[:, h] = pr @ vt[h // G].astype(np.float64).T
+    assert nmse(y, ref) < 1e-5, nmse(y, ref)
