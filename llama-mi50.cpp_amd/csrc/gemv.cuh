@@ -79,8 +79,12 @@ __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
 // instead of under their latency. Each read and its lgkmcnt(0) wait are one asm
 // statement (outputs exist only once the data has landed); writes are waited for by the
 // next lds_barrier.
+// Round 3: default OFF. Same-box A/B at HEAD (profiles/r03/ab_noasm): the decode SwiGLU
+// 17.52 -> 16.76 us and tg128 594.4 / 595.2 -> 597.1 / 597.6 tok/s without the asm
+// accesses; the bisect put the whole round-2 SwiGLU regression (15.25 -> 17.3 us,
+// profiles/r03/bisect_swiglu_roofline.txt) on the commit that introduced them.
 #ifndef MX_PROLOGUE_ASM
-#define MX_PROLOGUE_ASM 1
+#define MX_PROLOGUE_ASM 0
 #endif
 #if MX_PROLOGUE_ASM
 __device__ __forceinline__ uint32_t lds_off(const void * p) {

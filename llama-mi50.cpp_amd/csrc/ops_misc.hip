@@ -155,11 +155,62 @@ __global__ void k_set_rows_q8_0(const char * __restrict__ src, const char * __re
     for (int b = threadIdx.x; b < nblk; b += blockDim.x) quantize_block_q8_0(in + 32 * b, out + 34 * b);
 }
 
+// SET_ROWS of one-element rows: the transposed V cache store of the non-flash-attention
+// graph (src/llama-kv-cache.cpp cpy_v with v_trans: v_cur [n_embd_v, n_tokens] reshaped to
+// [1, n_embd_v * n_tokens], one index per element, element (d, t) -> row d * kv_size +
+// cell(t)). A workgroup per row (the general kernel) made that 524,288 workgroups of one
+// 2-byte store at pp512: 92 us per layer. Here a workgroup takes a tile of 32 tokens x 64
+// dimensions of the flat index i = t * R + d (R = n_embd_v, the row length before the
+// reshape), reads values and indices along d (coalesced), transposes through LDS and
+// stores along t, so consecutive lanes write consecutive cache cells. Any index values
+// are handled (it only permutes which lane stores which element).
+template <typename TI, typename TD>
+__global__ __launch_bounds__(256) void k_set_elems(const float * __restrict__ src, const TI * __restrict__ idx, char * __restrict__ dst,
+                                                   size_t dnb1, int64_t n, int64_t R) {
+    __shared__ float val[32][65];
+    __shared__ int64_t ind[32][65];
+    const int64_t d0 = (int64_t) blockIdx.x * 64, t0 = (int64_t) blockIdx.y * 32;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int l = threadIdx.x + 256 * e, dl = l & 63, tl = l >> 6;
+        const int64_t d = d0 + dl, i = (t0 + tl) * R + d;
+        const bool ok = d < R && i < n;
+        val[tl][dl] = ok ? src[i] : 0.f;
+        ind[tl][dl] = ok ? (int64_t) idx[i] : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int l = threadIdx.x + 256 * e, tl = l & 31, dl = l >> 5;
+        const int64_t r = ind[tl][dl];
+        if (r < 0) continue;
+        TD * o = (TD *) (dst + (size_t) r * dnb1);
+        if constexpr (std::is_same<TD, float>::value) *o = val[tl][dl];
+        else *o = f2h(val[tl][dl]);
+    }
+}
+
 void op_set_rows(OpCtx & c, ggml_tensor * dst) {
     const ggml_tensor * s0 = dst->src[0];
     const ggml_tensor * s1 = dst->src[1];
     const int64_t nr = s0->ne[1] * s0->ne[2] * s0->ne[3];
     if (nr == 0) return;
+    if (s0->ne[0] == 1 && s0->ne[2] == 1 && s0->ne[3] == 1 && s0->type == GGML_TYPE_F32 && s0->nb[1] == 4 && s1->ne[0] == nr &&
+        s1->nb[0] == (size_t) mx_type(s1->type).size && (dst->type == GGML_TYPE_F16 || dst->type == GGML_TYPE_F32)) {
+        // the row length before libllama's reshape to [1, n] (the transposed V store): the
+        // tile shape for coalesced stores; any value is correct
+        int64_t R = 64;
+        if ((s0->op == GGML_OP_RESHAPE || s0->op == GGML_OP_VIEW) && s0->src[0] && s0->src[0]->ne[0] > 1) R = s0->src[0]->ne[0];
+        const dim3 grid((unsigned) mx_ceil_div(R, 64), (unsigned) mx_ceil_div(mx_ceil_div(nr, R), 32));
+        MX_KLOG("set_elems n=%lld R=%lld type=%d", (long long) nr, (long long) R, (int) dst->type);
+        const float * a = (const float *) s0->data;
+        char * o = (char *) dst->data;
+#define SE(TI, TD) k_set_elems<TI, TD><<<grid, 256, 0, c.st>>>(a, (const TI *) s1->data, o, dst->nb[1], nr, R)
+        if (s1->type == GGML_TYPE_I64) { if (dst->type == GGML_TYPE_F16) SE(int64_t, uint16_t); else SE(int64_t, float); }
+        else { if (dst->type == GGML_TYPE_F16) SE(int32_t, uint16_t); else SE(int32_t, float); }
+#undef SE
+        return;
+    }
     const dim3 grid((unsigned) nr), blk(s0->ne[0] >= 256 ? 256 : 64);
     T4 g0 = geo(s0), g1 = geo(s1), gd = geo(dst);
     const char * a = (const char *) s0->data;

@@ -118,6 +118,37 @@ def test_set_rows_f16_bit_exact(pkg, backend, orc, idx_type):
     assert not out[untouched].any()
 
 
+@pytest.mark.parametrize("idx_type,n_tok,dtype", [("i64", 512, "f16"), ("i64", 7, "f16"), ("i32", 100, "f32")])
+def test_set_rows_transposed_v(pkg, backend, orc, idx_type, n_tok, dtype):
+    """the non-flash-attention V store (llama_kv_cache::cpy_v, v_trans): v_cur [D, n_tok]
+    reshaped to [1, D * n_tok], one index per element, element (d, t) -> cache element
+    d * kv + cell(t); set_elems transposes through LDS (klog) and must be bit-exact"""
+    rng = np.random.default_rng(n_tok)
+    D, kv = 1024, 768
+    v = (rng.standard_normal((n_tok, D)) * 3).astype(np.float32)
+    cells = np.sort(rng.permutation(kv)[:n_tok]) if n_tok < 16 else np.arange(100, 100 + n_tok)
+    idx = (np.arange(D)[None, :] * kv + cells[:, None]).astype(np.int64 if idx_type == "i64" else np.int32)  # [n_tok, D]
+
+    def build(ctx):
+        cache = ctx.new_tensor(dtype, D * kv)
+        tv = ctx.new_tensor("f32", D, n_tok)
+        ti = ctx.new_tensor(idx_type, D * n_tok)
+        dst = ctx.set_rows(ctx.reshape(cache, 1, D * kv), ctx.reshape(tv, 1, D * n_tok), ti)
+        zero = np.zeros(D * kv, np.uint16 if dtype == "f16" else np.float32)
+        return [dst, cache], [(cache, zero), (tv, v), (ti, idx.reshape(-1))]
+
+    backend.klog(True)
+    out = run(pkg, backend, build)[1].reshape(D, kv)
+    log = backend.klog_read()
+    backend.klog(False)
+    assert any(ln.startswith("set_elems") and "R=1024" in ln for ln in log), log
+    ref = orc.f32_to_f16(v).view(np.uint16) if dtype == "f16" else v
+    out = out.view(np.uint16) if dtype == "f16" else out
+    assert np.array_equal(out[:, cells], ref.T.reshape(D, n_tok))
+    mask = np.ones(kv, bool); mask[cells] = False
+    assert not out[:, mask].any()
+
+
 @pytest.mark.parametrize("ne0,nrows", [(4096, 3), (64, 5), (1025, 4), (8192, 1)])
 def test_rms_norm_fused_mul(pkg, backend, orc, ne0, nrows):
     rng = np.random.default_rng(ne0)

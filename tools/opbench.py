@@ -253,6 +253,11 @@ CASES = {
     "pp_down_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 14336, 4096),
     "ffn_q4k": lambda p, b, r: case_ffn(p, b, r),
     "ffn_block": lambda p, b, r: case_ffn_block(p, b, r),
+    # workgroup-balance probes: 448 SwiGLU workgroups (F 14336) are 1.75 per CU; F 16384 /
+    # 8192 / 12288 give exactly 2 / 1 / 1.5 per CU
+    "ffn_block_16384": lambda p, b, r: case_ffn_block(p, b, r, F=16384),
+    "ffn_block_12288": lambda p, b, r: case_ffn_block(p, b, r, F=12288),
+    "ffn_block_8192": lambda p, b, r: case_ffn_block(p, b, r, F=8192),
     "ffn_q4k_q6k": lambda p, b, r: case_ffn(p, b, r, tdown="q6_K"),
     "fa_256": lambda p, b, r: case_fa(p, b, r, 256),
     "fa_1024": lambda p, b, r: case_fa(p, b, r, 1024),
@@ -352,6 +357,9 @@ def main():
                 print(f"blocks {name}: n={len(a)} start[p50,p90,max]={np.percentile(st,50):.0f},{np.percentile(st,90):.0f},{st.max():.0f}ns "
                       f"end[min,p50,max]={en.min():.0f},{np.percentile(en,50):.0f},{en.max():.0f}ns dur[p10,p50,p90]={np.percentile(dur,10):.0f},"
                       f"{np.percentile(dur,50):.0f},{np.percentile(dur,90):.0f}ns", flush=True)
+                q = [0, 10, 25, 50, 75, 90, 100]
+                print(f"blocks {name}: dur pct {q} = {[int(np.percentile(dur, x)) for x in q]} ns; "
+                      f"end pct = {[int(np.percentile(en, x)) for x in q]} ns", flush=True)
         if args.sweep3 and not name.startswith(("fa_", "rms", "pp_")):
             for cfg in range(6):
                 for bpc in args.bpc:
