@@ -57,18 +57,23 @@ __device__ __forceinline__ uint2 ldu8(const char * p) {   // 8 bytes, any 2-byte
 }
 
 // G = query heads per workgroup (a divisor of the GQA ratio Gt; K/V are read once per
-// workgroup), NW = waves per workgroup (the chunk is NW x 16/32 keys)
-template <int D, int G, int NW, bool KQ = false>
+// workgroup), NW = waves per workgroup (the chunk is NW x NI x 64/(D/8) keys), NI = key-row
+// load instructions per wave and chunk. LONG (round 3, caches beyond one chunk): every
+// workgroup takes exactly ONE chunk, so all of a split's K/V bytes are in flight at once
+// (the looping split form paid one memory round trip per 64-key chunk: 34.5 us at 16k
+// keys), any number of splits; the (O, max, sum) partials are merged by
+// k_fattn_dec2_combine, a parallel second launch (one workgroup per query head).
+template <int D, int G, int NW, bool KQ = false, int NI = FD_NI, bool LONG = false>
 __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     constexpr int NT = 64 * NW;
     constexpr int LPK = D / 8;            // lanes per key row
     constexpr int KPI = 64 / LPK;         // keys per wave instruction
-    constexpr int KPW = FD_NI * KPI;      // keys per wave per chunk
+    constexpr int KPW = NI * KPI;         // keys per wave per chunk
     constexpr int CS = NW * KPW;          // keys per chunk (workgroup)
     typedef _Float16 h2v __attribute__((ext_vector_type(2)));
     __shared__ float wm[NW][G], wl[NW][G];
     __shared__ __align__(16) float wo[NW][G][D];
-    __shared__ float sM[G][FD_MAXSPLIT], sF[G][FD_MAXSPLIT], sL[G];
+    __shared__ float sM[G][LONG ? 1 : FD_MAXSPLIT], sF[G][LONG ? 1 : FD_MAXSPLIT], sL[G];
     __shared__ int s_last;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     const char * kb = p.k + (size_t) hk * p.k2 + (size_t) (iq3 % p.ns_kv) * p.k3 + lofs;
     const char * vb = p.v + (size_t) hk * p.v2 + (size_t) (iq3 % p.ns_kv) * p.v3 + lofs;
     const uint16_t * mrow = (const uint16_t *) (p.mask ? p.mask + (size_t) iq1 * p.m1 + (size_t) (iq3 % p.mne3) * p.m3 : p.k);
-    const int nch = (p.n_kv + CS - 1) / CS, cpb = (nch + p.nsplit - 1) / p.nsplit;
+    const int nch = (p.n_kv + CS - 1) / CS, cpb = LONG ? 1 : (nch + p.nsplit - 1) / p.nsplit;
     unsigned long long * tr = (blockIdx.x == 0 && blockIdx.y == 0) ? p.trace : nullptr;
     MX_TRACE(tr, 0);
     MX_TRACE_BLK(p.trace_blk, 0);
@@ -160,21 +165,21 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         const int key0 = ch * CS + wave * KPW + kq;
         // every load of the chunk first, unconditional (clamped: a load under a branch
         // costs a wait at the join): mask, K rows, V rows — coalesced, LPK lanes per row
-        uint16_t mraw[FD_NI];
-        uint4 kr[FD_NI], vr[FD_NI];
-        uint16_t kd[FD_NI], vd[FD_NI];                        // KQ: block scales
+        uint16_t mraw[NI];
+        uint4 kr[NI], vr[NI];
+        uint16_t kd[NI], vd[NI];                              // KQ: block scales
 #pragma unroll
-        for (int t = 0; t < FD_NI; ++t) mraw[t] = mrow[min(key0 + t * KPI, p.n_kv - 1)];
+        for (int t = 0; t < NI; ++t) mraw[t] = mrow[min(key0 + t * KPI, p.n_kv - 1)];
         if constexpr (KQ) {
 #pragma unroll
-            for (int t = 0; t < FD_NI; ++t) {
+            for (int t = 0; t < NI; ++t) {
                 const size_t ko = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1;
                 const uint2 w = ldu8(kb + ko);
                 kr[t] = make_uint4(w.x, w.y, 0, 0);
                 kd[t] = ld_u16(kb - lofs + dofs + ko);
             }
 #pragma unroll
-            for (int t = 0; t < FD_NI; ++t) {
+            for (int t = 0; t < NI; ++t) {
                 const size_t vo = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1;
                 const uint2 w = ldu8(vb + vo);
                 vr[t] = make_uint4(w.x, w.y, 0, 0);
@@ -182,20 +187,20 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             }
         } else {
 #pragma unroll
-            for (int t = 0; t < FD_NI; ++t) kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
+            for (int t = 0; t < NI; ++t) kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
 #pragma unroll
-            for (int t = 0; t < FD_NI; ++t) vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
+            for (int t = 0; t < NI; ++t) vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (ci == 0) MX_TRACE(tr, 1);
-        float mk[FD_NI];
+        float mk[NI];
 #pragma unroll
-        for (int t = 0; t < FD_NI; ++t) mk[t] = key0 + t * KPI < p.n_kv ? (p.mask ? h2f(mraw[t]) : 0.f) : -INFINITY;
+        for (int t = 0; t < NI; ++t) mk[t] = key0 + t * KPI < p.n_kv ? (p.mask ? h2f(mraw[t]) : 0.f) : -INFINITY;
         // scores: q·k over the row's LPK lanes (DPP), one per (head, key) in every lane of the row
-        float s[G][FD_NI];
-        if (ci == 0) { asm volatile("" :: "v"(kr[0].x), "v"(vr[0].x), "v"(vr[FD_NI - 1].w)); MX_TRACE(tr, 2); }
+        float s[G][NI];
+        if (ci == 0) { asm volatile("" :: "v"(kr[0].x), "v"(vr[0].x), "v"(vr[NI - 1].w)); MX_TRACE(tr, 2); }
 #pragma unroll
-        for (int t = 0; t < FD_NI; ++t) {
+        for (int t = 0; t < NI; ++t) {
 #pragma unroll
             for (int h = 0; h < G; ++h) {
                 float acc;
@@ -218,14 +223,14 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         for (int h = 0; h < G; ++h) {
             float mc = s[h][0];
 #pragma unroll
-            for (int t = 1; t < FD_NI; ++t) mc = fmaxf(mc, s[h][t]);
+            for (int t = 1; t < NI; ++t) mc = fmaxf(mc, s[h][t]);
 #pragma unroll
             for (int off = LPK; off < 64; off <<= 1) mc = fmaxf(mc, __shfl_xor(mc, off, 64));
             const float Mn = fmaxf(M[h], mc);
             const float a = M[h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(M[h] - Mn);
-            float pr[FD_NI], lc = 0.f;
+            float pr[NI], lc = 0.f;
 #pragma unroll
-            for (int t = 0; t < FD_NI; ++t) { pr[t] = Mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[h][t] - Mn); lc += pr[t]; }
+            for (int t = 0; t < NI; ++t) { pr[t] = Mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[h][t] - Mn); lc += pr[t]; }
 #pragma unroll
             for (int off = LPK; off < 64; off <<= 1) lc += __shfl_xor(lc, off, 64);
             L[h] = L[h] * a + lc;
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) o[h][i] *= a;
 #pragma unroll
-            for (int t = 0; t < FD_NI; ++t) {
+            for (int t = 0; t < NI; ++t) {
                 if constexpr (KQ) {
                     const float dv = h2f(vd[t]);
                     const uint32_t vw[2] = {vr[t].x, vr[t].y};
@@ -286,6 +291,9 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         if (p.nsplit == 1) {
             float * out = (float *) (p.dst + (size_t) (hb + h) * p.d1 + (size_t) iq1 * p.d2 + (size_t) iq3 * p.d3);
             out[d] = Lw == 0.f ? 0.f : O / Lw;
+        } else if constexpr (LONG) {      // plain stores: the combine is a later launch
+            part[h * (D + 2) + d] = O;
+            if (d == 0) { part[h * (D + 2) + D] = Mw; part[h * (D + 2) + D + 1] = Lw; }
         } else {
             // agent-scope (write-through) stores: visible to every XCD once completed,
             // without the L2 writeback a __threadfence() release does
@@ -298,7 +306,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     }
     MX_TRACE(tr, 5);
     MX_TRACE_BLK(p.trace_blk, 1);
-    if (p.nsplit == 1) return;
+    if (p.nsplit == 1 || LONG) return;
 
     // ---- split merge by the last workgroup of this (q row, KV head) to arrive
     __builtin_amdgcn_s_waitcnt(0);           // this thread's partial stores have completed
@@ -346,6 +354,57 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch / replay
 }
 
+// Merge of the LONG geometry's split partials: one workgroup per query head; the (max,
+// sum) of every split first (threads over splits), then O = Σ_s w_s O_s with the four waves
+// taking every fourth split and each lane D/64 dimensions (all of a wave's loads of a
+// split in one instruction), the waves' sums added through LDS. Max in the log2 domain
+// as the partials are. Replaces the looping in-launch merge for caches of > 16 chunks.
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_fattn_dec2_combine(FaDecArgs p) {
+    constexpr int PW = G * (D + 2), DPL = D / 64;
+    extern __shared__ float wsp[];                            // [nsplit] split weights
+    __shared__ float red[4][D], rm[4], rl[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = blockIdx.x % G, rs = blockIdx.x / G;        // rs = (iq3 n_q + iq1) slots + hslot
+    const int Gt = p.H / p.Hkv, NGB = Gt / G, slots = p.Hkv * NGB;
+    const int hslot = rs % slots, iq1 = (rs / slots) % p.n_q, iq3 = rs / (slots * p.n_q);
+    const int hb = (hslot / NGB) * Gt + (hslot % NGB) * G;
+    const float * pb = p.part + (size_t) rs * p.nsplit * PW + h * (D + 2);
+    float m = -INFINITY;
+    for (int sp = tid; sp < p.nsplit; sp += 256) m = fmaxf(m, pb[(size_t) sp * PW + D]);
+    m = wave_max(m);
+    if (lane == 0) rm[wave] = m;
+    __syncthreads();
+    const float Mx = fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3]));
+    float l = 0.f;
+    for (int sp = tid; sp < p.nsplit; sp += 256) {
+        const float ms = pb[(size_t) sp * PW + D];
+        const float f = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - Mx);
+        wsp[sp] = f;
+        l += f * pb[(size_t) sp * PW + D + 1];
+    }
+    l = wave_sum(l);
+    if (lane == 0) rl[wave] = l;
+    __syncthreads();
+    const float L = (rl[0] + rl[1]) + (rl[2] + rl[3]);
+    float o[DPL] = {};
+#pragma unroll 8
+    for (int sp = wave; sp < p.nsplit; sp += 4) {
+        const float f = wsp[sp];
+        const float * op = pb + (size_t) sp * PW + DPL * lane;
+        if constexpr (DPL == 2) { const float2 v = *(const float2 *) op; o[0] += f * v.x; o[1] += f * v.y; }
+        else o[0] += f * op[0];
+    }
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) red[wave][DPL * lane + j] = o[j];
+    __syncthreads();
+    if (tid < D) {
+        const float O = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+        float * out = (float *) (p.dst + (size_t) (hb + h) * p.d1 + (size_t) iq1 * p.d2 + (size_t) iq3 * p.d3);
+        out[tid] = L == 0.f ? 0.f : O / L;
+    }
+}
+
 // eligibility: f16 K/V, D 64/128, GQA ratio 1-8, a plain f16 mask broadcast over heads,
 // no softcap / ALiBi / sinks, few query rows (decode)
 bool fa_dec2_ok(const ggml_tensor * dst) {
@@ -365,11 +424,10 @@ bool fa_dec2_ok(const ggml_tensor * dst) {
     if (q->nb[1] % 16 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return false;
     if (q->ne[3] != k->ne[3] && k->ne[3] != 1) return false;
     if (k->ne[1] > INT32_MAX / 2 || q->ne[1] * q->ne[3] * q->ne[2] > MX_FA_CNT) return false;
-    // longer caches: the split-merging geometry measured slower than the v1 kernel +
-    // combine (fa_1024 12.3 vs 12.6 us, fa_4096 17.5 vs 16.3, opbench on MI355X), so only
-    // the single-split geometry is used unless g_tune[10] = 3 forces the split one
-    // (q8_0 caches have no v1 kernel: every length takes this one)
-    if (g_tune[10] != 3 && !kq && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;
+    // caches beyond one 16-wave chunk take the LONG geometry (fd_cfg); g_tune[10] = 4 keeps
+    // them on the v1 kernel + combine (round-2 behaviour: 18.4 + 12.0 us at 16k keys)
+    if (g_tune[10] == 4 && !kq && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;
+    if (k->ne[1] > (int64_t) 32768 * 4 * 8 * (64 / (D / 8))) return false;   // FD_LONG_MAXSPLIT chunks
     return true;
 }
 
@@ -378,18 +436,30 @@ bool fa_dec2_ok(const ggml_tensor * dst) {
 // K/V re-read from L2 by the GQA group): no split merge, whose publish / count / gather
 // round trips cost ~4 us; longer caches use 4-wave workgroups over the whole GQA group
 // and up to 16 splits merged in the same launch.
-struct FdCfg { int G, NW, nsplit; };
+// LONG: 4-wave workgroups over min(Gt, 2) query heads (K/V read once per workgroup for
+// those heads, from L2 by the group's other workgroup), 8 key rows per lane per chunk —
+// 128 keys (64 KB of f16 K/V at D 128) in flight per workgroup, one chunk each.
+struct FdCfg { int G, NW, nsplit; bool lng; };
+constexpr int FD_LONG_NI = 8;
+constexpr int FD_LONG_MAXSPLIT = 32768;   // the combine's split weights in LDS (128 KB): 4M keys at D 128
 static FdCfg fd_cfg(int D, int Gt, int64_t n_kv) {
     const int cs16 = 16 * FD_NI * (64 / (D / 8)), cs4 = 4 * FD_NI * (64 / (D / 8));
-    if (g_tune[10] == 2 || (g_tune[10] != 3 && n_kv <= cs16)) return {1, 16, (int) mx_ceil_div(n_kv, cs16)};
-    return {Gt, 4, (int) std::min<int64_t>(FD_MAXSPLIT, mx_ceil_div(n_kv, cs4))};
+    if (g_tune[10] == 2 || (g_tune[10] != 3 && n_kv <= cs16)) return {1, 16, (int) mx_ceil_div(n_kv, cs16), false};
+    if (g_tune[10] == 3) return {Gt, 4, (int) std::min<int64_t>(FD_MAXSPLIT, mx_ceil_div(n_kv, cs4)), false};
+    // sweeps: g_tune[28] keys rows per lane (4 / 8 / 16), g_tune[29] heads per workgroup (D 128, f16)
+    const int ni = D == 128 && g_tune[28] ? g_tune[28] : FD_LONG_NI;
+    // two heads per workgroup measured best (fa_4096 7.7 vs 8.5 us for four, fa_16384 17.7
+    // vs 18.5; profiles/r03/opbench_fa_long_sweep.txt)
+    const int g = D == 128 && g_tune[29] ? std::min(g_tune[29], Gt) : std::min(Gt, 2);
+    const int csl = 4 * ni * (64 / (D / 8));
+    return {g, 4, (int) mx_ceil_div(n_kv, csl), true};
 }
 
 size_t fa_dec2_scratch(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0], * k = dst->src[1];
     const int64_t D = k->ne[0];
     const FdCfg f = fd_cfg((int) D, (int) (q->ne[2] / k->ne[2]), k->ne[1]);
-    return (size_t) (q->ne[1] * q->ne[3] * q->ne[2]) * std::min(f.nsplit, FD_MAXSPLIT) * (D + 2) * sizeof(float) + 256;
+    return (size_t) (q->ne[1] * q->ne[3] * q->ne[2]) * (f.lng ? f.nsplit : std::min(f.nsplit, FD_MAXSPLIT)) * (D + 2) * sizeof(float) + 256;
 }
 
 void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
@@ -406,7 +476,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     a.scale = mx_op_param<float>(dst, 0);
     const int D = (int) k->ne[0], Gt = a.H / a.Hkv;
     const FdCfg f = fd_cfg(D, Gt, a.n_kv);
-    MX_ASSERT(f.nsplit <= FD_MAXSPLIT);
+    MX_ASSERT(f.lng ? f.nsplit <= 65535 : f.nsplit <= FD_MAXSPLIT);
     a.nsplit = f.nsplit;
     a.part = (float *) c.scratch->take(fa_dec2_scratch(dst));
     a.cnt = c.s->fa_cnt;
@@ -425,7 +495,31 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     } else a.pf_n = 0;
     const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
     const bool kq = k->type == GGML_TYPE_Q8_0;
-    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv, (int) kq, pf_rows);
+    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u long=%d", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv,
+            (int) kq, pf_rows, (int) f.lng);
+    if (f.lng) {
+        const unsigned gc = gx * (unsigned) f.G;                     // one combine workgroup per query head
+        const size_t lds = (size_t) f.nsplit * sizeof(float);
+#define FL(DD, GG) if (D == DD && f.G == GG) { \
+            if (kq) k_fattn_dec2<DD, GG, 4, true, FD_LONG_NI, true><<<grid, 256, 0, c.st>>>(a); \
+            else k_fattn_dec2<DD, GG, 4, false, FD_LONG_NI, true><<<grid, 256, 0, c.st>>>(a); \
+            static const bool attr = [] { HIP_CHECK(hipFuncSetAttribute((const void *) k_fattn_dec2_combine<DD, GG>, \
+                hipFuncAttributeMaxDynamicSharedMemorySize, FD_LONG_MAXSPLIT * (int) sizeof(float))); return true; }(); \
+            (void) attr; \
+            k_fattn_dec2_combine<DD, GG><<<gc, 256, lds, c.st>>>(a); \
+            return; }
+        const int ni = D == 128 && g_tune[28] ? g_tune[28] : FD_LONG_NI;
+        if (ni != FD_LONG_NI && !kq) {   // sweep geometries (f16, D 128)
+#define FS(NI_, GG) if (ni == NI_ && f.G == GG) { \
+                k_fattn_dec2<128, GG, 4, false, NI_, true><<<grid, 256, 0, c.st>>>(a); \
+                k_fattn_dec2_combine<128, GG><<<gc, 256, lds, c.st>>>(a); return; }
+            FS(4, 1) FS(4, 2) FS(4, 4) FS(16, 1) FS(16, 2) FS(16, 4)
+#undef FS
+        }
+        FL(128, 1) FL(128, 2) FL(128, 4) FL(64, 1) FL(64, 2) FL(64, 4)
+#undef FL
+        MX_ABORT("fattn dec2 long D=%d G=%d", D, f.G);
+    }
 #define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { \
         if (kq) k_fattn_dec2<DD, GG, NWW, true><<<grid, 64 * NWW, 0, c.st>>>(a); \
         else k_fattn_dec2<DD, GG, NWW><<<grid, 64 * NWW, 0, c.st>>>(a); \

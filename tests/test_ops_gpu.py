@@ -289,7 +289,11 @@ def test_fused_gate_up_swiglu(pkg, backend, orc, tname, N):
                                                # prefill kernel v2 (k_fa_mma2, D 128): 4 / 2 / 1 heads
                                                # per workgroup, GQA 8 (two head groups), ragged tiles
                                                (512, 512, 32, 8, 128), (200, 450, 6, 3, 128), (77, 77, 16, 2, 128),
-                                               (33, 1000, 4, 4, 128)])
+                                               (33, 1000, 4, 4, 128),
+                                               # decode LONG geometry (one 128-key chunk per workgroup,
+                                               # parallel combine): llama-bench -d 16384, GQA 8 (70B:
+                                               # two head groups), a ragged 33000-key cache
+                                               (1, 16384, 32, 8, 128), (1, 8000, 64, 8, 128), (1, 33000, 8, 8, 128)])
 def test_flash_attn(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
     rng = np.random.default_rng(n_q * 1000 + n_kv)
     q = rng.standard_normal((H, n_q, D)).astype(np.float32)

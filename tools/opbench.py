@@ -262,6 +262,8 @@ CASES = {
     "fa_256": lambda p, b, r: case_fa(p, b, r, 256),
     "fa_1024": lambda p, b, r: case_fa(p, b, r, 1024),
     "fa_4096": lambda p, b, r: case_fa(p, b, r, 4096),
+    "fa_16384": lambda p, b, r: case_fa(p, b, r, 16384),
+    "fa_32768": lambda p, b, r: case_fa(p, b, r, 32768),
     "fa_pp512": lambda p, b, r: case_fa(p, b, r, 512, n_q=512),
     "fa_pp2048": lambda p, b, r: case_fa(p, b, r, 2048, n_q=512),
     "rms_mul": lambda p, b, r: case_rms(p, b, r),
