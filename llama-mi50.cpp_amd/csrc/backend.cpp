@@ -439,7 +439,7 @@ static ggml_backend_dev_t rg_get(ggml_backend_reg_t, size_t i) { return i < g_de
 
 static ggml_backend_feature * rg_features(ggml_backend_reg_t) {
     static ggml_backend_feature f[] = {
-        {"ARCH", "gfx950"}, {"WAVE", "64"}, {"MFMA", "f16,bf16,i8"}, {"HIP_GRAPHS", "1"}, {nullptr, nullptr},
+        {"ARCH", "gfx950"}, {"WAVE", "64"}, {"MFMA", "f16"}, {"DOT", "v_dot4_i32_i8,v_dot2_f32_f16"}, {"HIP_GRAPHS", "1"}, {nullptr, nullptr},
     };
     return f;
 }

@@ -42,21 +42,34 @@ __device__ __forceinline__ int64_t read_idx(const char * p, int is64, int64_t i)
 // 4 waves x 64/L. Weight types per matrix: QTA (q), QTK (k), QTV (v) — the recipes mix
 // them (Q4_K_M: v Q6_K on the use_more_bits layers, Q5_K on the others at 70B; 8-expert
 // Q4_K_M/Q5_K_M: k and v Q8_0, src/llama-quant.cpp:302-321).
-template <int QTA, int QTK, int QTV, int MODE, int LA = 16, int UA = 4, int LV = 16, int UV = 4>
-__global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
+// BAL (round 3): one workgroup per 16 q rows that also takes 4 k rows and 4 v rows (7 waves:
+// 0-3 q, 4 k, 5-6 v at 32 lanes per row) — the 448-block grid of the split layout (q 256 +
+// k 64 + v 128 blocks: 1.75 per CU, so 192 CUs streamed two blocks while 64 idled) becomes
+// 256 equal blocks (59.5 KB each at Llama-3-8B), one per CU; wave-uniform matrix choice.
+template <int QTA, int QTK, int QTV, int MODE, int LA = 16, int UA = 4, int LV = 16, int UV = 4, bool BAL = false>
+__global__ __launch_bounds__(BAL ? 448 : 256) void k_qkv_rope_store(QkvArgs p) {
     static_assert(LA <= 32, "RoPE pairs must share a wave");
+    static_assert(!BAL || (LA == 16 && LV == 32), "balanced layout: 4 q/k rows, 2 v rows per wave");
+    constexpr int NT = BAL ? 448 : 256;
     extern __shared__ __align__(16) char smem[];
     constexpr int RBA = 4 * (64 / LA), RBV = 4 * (64 / LV);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // XCD-contiguous order within each matrix's block range (gemv.cuh xcd_block): every
-    // 128-B line of q_out and of the K/V cache rows is then written by one XCD's L2
-    const int m = (int) blockIdx.x < p.nblk_q ? 0 : ((int) blockIdx.x < p.nblk_q + p.nblk_k ? 1 : 2);
-    const int base = m == 0 ? 0 : (m == 1 ? p.nblk_q : p.nblk_q + p.nblk_k);
-    const int nb = m == 0 ? p.nblk_q : (m == 1 ? p.nblk_k : (int) gridDim.x - p.nblk_q - p.nblk_k);
-    const int bl = (base & 7) == 0 ? xcd_block((int) blockIdx.x - base, nb, p.xs.xcd) : (int) blockIdx.x - base;
+    int m, bl, row;
+    if constexpr (BAL) {
+        m = wave < 4 ? 0 : (wave == 4 ? 1 : 2);
+        bl = (gridDim.x & 7) == 0 ? xcd_block((int) blockIdx.x, (int) gridDim.x, p.xs.xcd) : (int) blockIdx.x;
+        row = m == 0 ? bl * 16 + wave * 4 + lane / 16 : (m == 1 ? bl * 4 + lane / 16 : bl * 4 + (wave - 5) * 2 + lane / 32);
+    } else {
+        // XCD-contiguous order within each matrix's block range (gemv.cuh xcd_block): every
+        // 128-B line of q_out and of the K/V cache rows is then written by one XCD's L2
+        m = (int) blockIdx.x < p.nblk_q ? 0 : ((int) blockIdx.x < p.nblk_q + p.nblk_k ? 1 : 2);
+        const int base = m == 0 ? 0 : (m == 1 ? p.nblk_q : p.nblk_q + p.nblk_k);
+        const int nb = m == 0 ? p.nblk_q : (m == 1 ? p.nblk_k : (int) gridDim.x - p.nblk_q - p.nblk_k);
+        bl = (base & 7) == 0 ? xcd_block((int) blockIdx.x - base, nb, p.xs.xcd) : (int) blockIdx.x - base;
+        row = m == 2 ? bl * RBV + wave * (64 / LV) + lane / LV : bl * RBA + wave * (64 / LA) + lane / LA;
+    }
     const int L = m == 2 ? LV : LA;
     const int sub = lane % L;
-    const int row = m == 2 ? bl * RBV + wave * (64 / LV) + lane / LV : bl * RBA + wave * (64 / LA) + lane / LA;
     const bool valid = row < p.rows[m];
     const char * rows[1] = {p.w[m] + (int64_t) (valid ? row : p.rows[m] - 1) * p.w_row[m]};
     const LdsAct a = lds_act(smem, p.K);
@@ -77,11 +90,12 @@ __global__ __launch_bounds__(256) void k_qkv_rope_store(QkvArgs p) {
     // computed per lane (theta loop + libm sincos) it cost ~2 us per launch
     float2 csn = p.tab[i0 / 2];
     auto fence = [&] { asm volatile("" : "+v"(pos)); asm volatile("" : "+v"(kvrow)); asm volatile("" : "+v"(csn.x)); asm volatile("" : "+v"(csn.y)); };
-    StageRegs<256, MODE> sr;
-    stage_issue<256, MODE>(p.xs, p.K, a, sr);
-    if (m == 2) gemv_rows_staged<QTV, LV, UV, 1, 256, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, sr, acc, fence);   // block-uniform branch
-    else if (QTK != QTA && m == 1) gemv_rows_staged<QTK, LA, UA, 1, 256, MODE>(rows, p.units_k, sub, a, p.xs, p.K, red, sr, acc, fence);
-    else gemv_rows_staged<QTA, LA, UA, 1, 256, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, sr, acc, fence);
+    StageRegs<NT, MODE> sr;
+    stage_issue<NT, MODE>(p.xs, p.K, a, sr);
+    // block-uniform branch (BAL: wave-uniform; every arm reaches the same barriers)
+    if (m == 2) gemv_rows_staged<QTV, LV, UV, 1, NT, MODE>(rows, p.units_v, sub, a, p.xs, p.K, red, sr, acc, fence);
+    else if (QTK != QTA && m == 1) gemv_rows_staged<QTK, LA, UA, 1, NT, MODE>(rows, p.units_k, sub, a, p.xs, p.K, red, sr, acc, fence);
+    else gemv_rows_staged<QTA, LA, UA, 1, NT, MODE>(rows, p.units_a, sub, a, p.xs, p.K, red, sr, acc, fence);
     MX_TRACE(tr, 3);
     MX_TRACE_BLK(p.trace_blk, 1);
     const float v = acc[0];   // row sum: in lane sub == L-1 (every lane of the row for L <= 16)
@@ -296,13 +310,29 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     for (int j = i; j <= last; ++j) act_cache_invalidate(c.s, g->nodes[j]);
 #undef GEOS
     if (mode != XS_NORM && cfg != 5) return 0;   // the other sources exist in the default geometry only
-    const dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
+    dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
+    unsigned nthr = 256;
+    // balanced layout (GQA 4: q rows = 4 x k rows = 4 x v rows, one block per 16 q rows),
+    // default geometry, the norm / f32 / q8 sources a 448-thread block stages in one pass;
+    // g_tune[30] = 1 keeps the split layout (A/B)
+    const bool bal = g_tune[30] != 1 && cfg == 5 && wq->ne[1] % 16 == 0 && wq->ne[1] == 4 * wk->ne[1] && wq->ne[1] == 4 * wv->ne[1] &&
+                     p.K <= 16 * 448 && (mode == XS_NORM || mode == XS_Q8 || mode == XS_F32);
+    if (bal) {
+        void (*kb)(QkvArgs) = nullptr;
+#define QKB(TA, TK, TV) if (ta == TA && tk == TK && tv == TV) kb = mode == XS_Q8 ? k_qkv_rope_store<TA, TK, TV, XS_Q8, 16, 2, 32, 2, true> : \
+        mode == XS_F32 ? k_qkv_rope_store<TA, TK, TV, XS_F32, 16, 2, 32, 2, true> : k_qkv_rope_store<TA, TK, TV, XS_NORM, 16, 2, 32, 2, true>;
+        QKB(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, GGML_TYPE_Q4_K) QKB(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, GGML_TYPE_Q6_K)
+        QKB(GGML_TYPE_Q4_K, GGML_TYPE_Q8_0, GGML_TYPE_Q8_0) QKB(GGML_TYPE_Q5_K, GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
+        QKB(GGML_TYPE_Q4_0, GGML_TYPE_Q4_0, GGML_TYPE_Q4_0) QKB(GGML_TYPE_Q8_0, GGML_TYPE_Q8_0, GGML_TYPE_Q8_0)
+#undef QKB
+        if (kb) { kern = kb; grid = dim3((unsigned) (wq->ne[1] / 16)); nthr = 448; }
+    }
     if (kq8) {
         p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
         p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
     }
-    MX_KLOG("qkv qta=%d qtk=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d", ta, tk, tv, mode, cfg, p.K, (int) kq8);
-    hipLaunchKernelGGL(kern, grid, dim3(256), gemv_lds_bytes(p.K, mode), c.st, p);
+    MX_KLOG("qkv qta=%d qtk=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d bal=%d", ta, tk, tv, mode, cfg, p.K, (int) kq8, (int) (nthr == 448));
+    hipLaunchKernelGGL(kern, grid, dim3(nthr), gemv_lds_bytes(p.K, mode), c.st, p);
     if (kq8) {
         k_kv_store_q8<<<(unsigned) mx_ceil_div(wk->ne[1] + wv->ne[1], 256), 256, 0, c.st>>>(p, (int) wk->ne[1], (int) wv->ne[1]);
     }
