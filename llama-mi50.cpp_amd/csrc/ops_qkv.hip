@@ -313,9 +313,10 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     dim3 grid((unsigned) (p.nblk_q + p.nblk_k + nblk_v));
     unsigned nthr = 256;
     // balanced layout (GQA 4: q rows = 4 x k rows = 4 x v rows, one block per 16 q rows),
-    // default geometry, the norm / f32 / q8 sources a 448-thread block stages in one pass;
-    // g_tune[30] = 1 keeps the split layout (A/B)
-    const bool bal = g_tune[30] != 1 && cfg == 5 && wq->ne[1] % 16 == 0 && wq->ne[1] == 4 * wk->ne[1] && wq->ne[1] == 4 * wv->ne[1] &&
+    // default geometry, the norm / f32 / q8 sources a 448-thread block stages in one pass.
+    // Opt-in (g_tune[30] = 1): measured 7.12 vs 6.71 us alone (opbench attn_in) and within
+    // the noise in tg128 (584 vs 582 tok/s), profiles/r03/qkv_balanced_ab.txt
+    const bool bal = g_tune[30] == 1 && cfg == 5 && wq->ne[1] % 16 == 0 && wq->ne[1] == 4 * wk->ne[1] && wq->ne[1] == 4 * wv->ne[1] &&
                      p.K <= 16 * 448 && (mode == XS_NORM || mode == XS_Q8 || mode == XS_F32);
     if (bal) {
         void (*kb)(QkvArgs) = nullptr;
