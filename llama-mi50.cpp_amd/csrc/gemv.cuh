@@ -83,6 +83,9 @@ __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
 // 17.52 -> 16.76 us and tg128 594.4 / 595.2 -> 597.1 / 597.6 tok/s without the asm
 // accesses; the bisect put the whole round-2 SwiGLU regression (15.25 -> 17.3 us,
 // profiles/r03/bisect_swiglu_roofline.txt) on the commit that introduced them.
+#ifndef MX_PROLOGUE_ONE      // A/B build switch: 0 = the loop form of round 1 (each half read per use)
+#define MX_PROLOGUE_ONE 1
+#endif
 #ifndef MX_PROLOGUE_ASM
 #define MX_PROLOGUE_ASM 0
 #endif
@@ -308,7 +311,7 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
         lds_barrier();                        // staged x (and norm weight) visible
         // K <= 16 NT (every SwiGLU / lm_head grid): each thread reads its one 16-value half
         // (and norm weight) once, in one round trip, and keeps it for Σx² and quantisation
-        const bool one = nhg <= NT;
+        const bool one = MX_PROLOGUE_ONE && nhg <= NT;
         float v1[16], w1[16];
         if (one && t < nhg) {
             if constexpr (MODE == XS_NORM_LDS) lds_rd16x2(xf + 16 * t, xf + K + 16 * t, v1, w1);

@@ -47,6 +47,11 @@ __device__ __forceinline__ bool g2_item(const G2Args & p, const char *& w, const
     return true;
 }
 
+// A/B build switch: MX_GEMV_EXT=0 compiles the MoE item and prefetch-row branches out
+#ifndef MX_GEMV_EXT
+#define MX_GEMV_EXT 1
+#endif
+
 // EPI 0 store, 1 SwiGLU(w, w2), 2 + residual. W waves per block; with W = 8 and
 // LPR = 16 a block owns 32 consecutive rows and (q8o != null) also emits the q8
 // activation of its 32 outputs for the next GEMV (the FFN down projection).
@@ -56,7 +61,7 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     constexpr int NM = EPI == 1 ? 2 : 1;
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (!p.ids && blockIdx.y > 0) {            // prefetch rows: workgroup-uniform, before any barrier
+    if (MX_GEMV_EXT && !p.ids && blockIdx.y > 0) {   // prefetch rows: workgroup-uniform, before any barrier
         const unsigned L = blockIdx.x + gridDim.x * blockIdx.y, xcd = L & 7;
         const unsigned T = (gridDim.x * (gridDim.y - 1) >> 3) * (64 * W), t0 = ((L - gridDim.x) >> 3) * (64 * W) + threadIdx.x;
         unsigned acc = 0;
@@ -77,7 +82,7 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     XStage xs = p.xs;
     float * dst = p.dst;
     int8_t * q8o = p.q8o; float * q8od = p.q8od, * q8os = p.q8os;
-    if (p.ids && !g2_item(p, wb, wb2, xs, dst, q8o, q8od, q8os)) return;
+    if (MX_GEMV_EXT && p.ids && !g2_item(p, wb, wb2, xs, dst, q8o, q8od, q8os)) return;
     const char * rows[NM];
     rows[0] = wb + rr * p.w_row;
     if constexpr (NM == 2) rows[1] = wb2 + rr * p.w_row;

@@ -35,6 +35,9 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int M4_KC = 128;        // K per chunk (half a super-block)
+#ifndef MX_M4_LDA
+#define MX_M4_LDA 1               // MFMA steps the LDS activation reads run ahead (1 or 2)
+#endif
 constexpr int M4_MAXSEG = 3;
 constexpr float M4_WSCALE = 1024.0f;
 
@@ -118,6 +121,20 @@ __device__ __forceinline__ uint32_t pair_bytes(uint32_t w, int hi_pair) {
     return __builtin_amdgcn_perm(0u, w, hi_pair ? 0x0c030c02u : 0x0c010c00u);
 }
 __device__ __forceinline__ h2 as_h2(uint32_t u) { h2 v; __builtin_memcpy(&v, &u, 4); return v; }
+// (x & m) | b as one v_and_or_b32 (mask from an SGPR, bias from a VGPR: GFX9 VOP3 reads
+// one constant-bus operand and no literal; the compiler otherwise emits v_and + v_or)
+#ifndef MX_M4_ANDOR
+#define MX_M4_ANDOR 0
+#endif
+__device__ __forceinline__ uint32_t m4_and_or(uint32_t x, uint32_t m, uint32_t b) {
+#if MX_M4_ANDOR
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m), "v"(b));
+    return r;
+#else
+    return (x & m) | b;
+#endif
+}
 
 // dequantised scales of one lane's unit: lo / hi sub-block (d*sc, -dmin*m) x 2^10, f16;
 // Q5_K also the qh bit index of the two sub-blocks
@@ -130,9 +147,12 @@ __device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, i
     if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
         const int g = 2 * hf + h;                              // sub-block pair (2g, 2g+1) of unit U
         const uint32_t s0 = dw(r.hd, 1), s1 = dw(r.hd, 2), s2 = dw(r.hd, 3);
-        // get_scale_min_k4 (ggml-quants.c:703) of sub-blocks 2g, 2g+1, packed extraction
-        const uint32_t scw = g < 2 ? (s0 & 0x3F3F3F3Fu) : ((s2 & 0x0F0F0F0Fu) | ((s0 >> 2) & 0x30303030u));
-        const uint32_t mnw = g < 2 ? (s1 & 0x3F3F3F3Fu) : (((s2 >> 4) & 0x0F0F0F0Fu) | ((s1 >> 2) & 0x30303030u));
+        // get_scale_min_k4 (ggml-quants.c:703) of sub-blocks 2g, 2g+1, packed extraction.
+        // g < 2 <=> hf == 0 (h is 0 or 1): written on the wave-uniform hf, so the select is
+        // scalar — as `g < 2` the compiler branched on the lane's h (exec-mask branches in
+        // every MFMA step)
+        const uint32_t scw = hf == 0 ? (s0 & 0x3F3F3F3Fu) : ((s2 & 0x0F0F0F0Fu) | ((s0 >> 2) & 0x30303030u));
+        const uint32_t mnw = hf == 0 ? (s1 & 0x3F3F3F3Fu) : (((s2 >> 4) & 0x0F0F0F0Fu) | ((s1 >> 2) & 0x30303030u));
         const uint32_t scp = scw >> (16 * (g & 1)), mnp = mnw >> (16 * (g & 1));
         const float d = h2f((uint16_t) (dw(r.hd, 0) & 0xFFFF)) * M4_WSCALE;
         const float dm = h2f((uint16_t) (dw(r.hd, 0) >> 16)) * M4_WSCALE;
@@ -171,8 +191,8 @@ __device__ __forceinline__ h8 m4_deq(const M4W<QT> & r, const M4Scale & s, int h
 #pragma unroll
             for (int pp = 0; pp < 2; ++pp) {
                 const uint32_t x = pair_bytes(w, pp);
-                uint32_t v = hi ? ((x & 0x00F000F0u) | 0x54005400u)     // 64 + q (high nibble in place)
-                                : ((x & 0x000F000Fu) | 0x64006400u);    // 1024 + q
+                uint32_t v = hi ? m4_and_or(x, 0x00F000F0u, 0x54005400u)     // 64 + q (high nibble in place)
+                                : m4_and_or(x, 0x000F000Fu, 0x64006400u);    // 1024 + q
                 if constexpr (QT == GGML_TYPE_Q5_K) {
                     const uint32_t y = pair_bytes(qh, pp);
                     v |= hi ? (((y >> (s.gb + 1)) & 0x00010001u) << 8) : (((y >> s.gb) & 0x00010001u) << 4);
@@ -268,15 +288,19 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
     auto compute = [&](const M4W<QT> & rw, int i) {
         const uint4 * L = lds + (i % M4_S) * TILE;
         const int kc = c0 + i;
-        h8 a0[TT], a1[TT];
-        lda(L, 0, 0, a0);
+        // activation fragments MX_M4_LDA steps ahead (ring of MX_M4_LDA + 1 register sets)
+        constexpr int D = MX_M4_LDA;
+        h8 af[D + 1][TT];
+#pragma unroll
+        for (int st = 0; st < D; ++st) lda(L, st >> 2, st & 3, af[st]);
+        // the two units' scales once per chunk (they depend on j only, not on the step)
+        const M4Scale sj[2] = {m4_scales<QT>(rw, kc, h, 0), m4_scales<QT>(rw, kc, h, 1)};
 #pragma unroll
         for (int st = 0; st < 8; ++st) {
             const int j = st >> 2, q = st & 3;
-            const M4Scale s = m4_scales<QT>(rw, kc, h, j);
-            h8 (&cur)[TT] = (st & 1) ? a1 : a0;
-            h8 (&nxt)[TT] = (st & 1) ? a0 : a1;
-            if (st < 7) lda(L, (st + 1) >> 2, (st + 1) & 3, nxt);
+            const M4Scale & s = sj[j];
+            h8 (&cur)[TT] = af[st % (D + 1)];
+            if (st + D < 8) lda(L, (st + D) >> 2, (st + D) & 3, af[(st + D) % (D + 1)]);
             const h8 b = m4_deq<QT>(rw, s, h, j, q);
 #pragma unroll
             for (int t = 0; t < TT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], b, acc[t], 0, 0, 0);
