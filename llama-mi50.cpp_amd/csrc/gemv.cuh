@@ -83,8 +83,12 @@ __device__ __forceinline__ LdsAct lds_act(char * smem, int64_t K) {
 // 17.52 -> 16.76 us and tg128 594.4 / 595.2 -> 597.1 / 597.6 tok/s without the asm
 // accesses; the bisect put the whole round-2 SwiGLU regression (15.25 -> 17.3 us,
 // profiles/r03/bisect_swiglu_roofline.txt) on the commit that introduced them.
-#ifndef MX_PROLOGUE_ONE      // A/B build switch: 0 = the loop form of round 1 (each half read per use)
-#define MX_PROLOGUE_ONE 1
+// MX_PROLOGUE_ONE=1: each thread reads its 16-value half (and norm weight) once and keeps
+// it in registers (round 2, 0d87f1f). Default 0 (round 1's loop, each half read per use):
+// with the dense/EXT split of k_gemv2 the same-box decode ran 620 / 619 tok/s against
+// 602 / 615 with it (profiles/r03/ab_gemv_variants.txt)
+#ifndef MX_PROLOGUE_ONE
+#define MX_PROLOGUE_ONE 0
 #endif
 #ifndef MX_PROLOGUE_ASM
 #define MX_PROLOGUE_ASM 0

@@ -47,21 +47,19 @@ __device__ __forceinline__ bool g2_item(const G2Args & p, const char *& w, const
     return true;
 }
 
-// A/B build switch: MX_GEMV_EXT=0 compiles the MoE item and prefetch-row branches out
-#ifndef MX_GEMV_EXT
-#define MX_GEMV_EXT 1
-#endif
-
+// EXT: the MUL_MAT_ID item (p.ids) and prefetch-row (grid.y > 0) branches. Compiled only
+// into the launches that use them: as runtime branches in every dense decode GEMV they
+// cost tg128 594 -> 602-615 tok/s (same box, profiles/r03/ab_gemv_variants.txt).
 // EPI 0 store, 1 SwiGLU(w, w2), 2 + residual. W waves per block; with W = 8 and
 // LPR = 16 a block owns 32 consecutive rows and (q8o != null) also emits the q8
 // activation of its 32 outputs for the next GEMV (the FFN down projection).
-template <int QT, int LPR, int UPL, int EPI, int W, int MODE>
+template <int QT, int LPR, int UPL, int EPI, int W, int MODE, bool EXT>
 __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     extern __shared__ __align__(16) char smem[];
     constexpr int NM = EPI == 1 ? 2 : 1;
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (MX_GEMV_EXT && !p.ids && blockIdx.y > 0) {   // prefetch rows: workgroup-uniform, before any barrier
+    if (EXT && !p.ids && blockIdx.y > 0) {   // prefetch rows: workgroup-uniform, before any barrier
         const unsigned L = blockIdx.x + gridDim.x * blockIdx.y, xcd = L & 7;
         const unsigned T = (gridDim.x * (gridDim.y - 1) >> 3) * (64 * W), t0 = ((L - gridDim.x) >> 3) * (64 * W) + threadIdx.x;
         unsigned acc = 0;
@@ -82,7 +80,7 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     XStage xs = p.xs;
     float * dst = p.dst;
     int8_t * q8o = p.q8o; float * q8od = p.q8od, * q8os = p.q8os;
-    if (MX_GEMV_EXT && p.ids && !g2_item(p, wb, wb2, xs, dst, q8o, q8od, q8os)) return;
+    if (EXT && p.ids && !g2_item(p, wb, wb2, xs, dst, q8o, q8od, q8os)) return;
     const char * rows[NM];
     rows[0] = wb + rr * p.w_row;
     if constexpr (NM == 2) rows[1] = wb2 + rr * p.w_row;
@@ -128,6 +126,19 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     }
 }
 
+template <int QT, int LPR, int UPL, int EPI, int W, bool EXT>
+static void launch_mode(hipStream_t st, const G2Args & p, int mode, dim3 grid, size_t lds) {
+    switch (mode) {
+        case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8, EXT><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_NORM_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_LDS, EXT><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_F32_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32_LDS, EXT><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_NORM: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM, EXT><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_NORM_H2: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_H2, EXT><<<grid, 64 * W, lds, st>>>(p); break;
+        case XS_F32_H2: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32_H2, EXT><<<grid, 64 * W, lds, st>>>(p); break;
+        default: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32, EXT><<<grid, 64 * W, lds, st>>>(p); break;
+    }
+}
+
 template <int QT, int LPR, int UPL, int EPI, int W = 4>
 static void launch_cfg(hipStream_t st, const G2Args & p0, bool regs = false) {
     G2Args p = p0;
@@ -140,15 +151,8 @@ static void launch_cfg(hipStream_t st, const G2Args & p0, bool regs = false) {
     MX_KLOG("gemv2 qt=%d lpr=%d upl=%d epi=%d w=%d mode=%d K=%d M=%d q8o=%d pf=%d", QT, LPR, UPL, EPI, W, mode, p.K, p.nrows, p.q8o != nullptr, p.pf_n);
     dim3 grid = grid0;
     if (p.pf_n && !p.ids) grid.y = 2;           // one row of prefetch workgroups (grid0.x % 8 == 0)
-    switch (mode) {
-        case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8><<<grid, 64 * W, lds, st>>>(p); break;
-        case XS_NORM_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_LDS><<<grid, 64 * W, lds, st>>>(p); break;
-        case XS_F32_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32_LDS><<<grid, 64 * W, lds, st>>>(p); break;
-        case XS_NORM: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM><<<grid, 64 * W, lds, st>>>(p); break;
-        case XS_NORM_H2: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_H2><<<grid, 64 * W, lds, st>>>(p); break;
-        case XS_F32_H2: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32_H2><<<grid, 64 * W, lds, st>>>(p); break;
-        default: k_gemv2<QT, LPR, UPL, EPI, W, XS_F32><<<grid, 64 * W, lds, st>>>(p); break;
-    }
+    if (p.ids || p.pf_n) launch_mode<QT, LPR, UPL, EPI, W, true>(st, p, mode, grid, lds);
+    else launch_mode<QT, LPR, UPL, EPI, W, false>(st, p, mode, grid, lds);
 }
 
 template <int QT, int EPI>

@@ -35,6 +35,17 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int M4_KC = 128;        // K per chunk (half a super-block)
+// timing experiments only (variant builds, results wrong): 1 no per-chunk vmcnt wait and
+// barrier, 2 no dequantisation (raw weight bits as the B operand), 4 LDS activation
+// fragments read once per chunk
+// X (template) bits: 8 = the short Q6_K dequantisation (MX_M4_Q6V2 sets it by default);
+// timing experiments only (g_tune[31], results wrong): 1 no per-chunk wait and barrier,
+// 2 no dequantisation (raw weight bits as the B operand), 4 LDS activation fragments read
+// once per chunk
+#ifndef MX_M4_Q6V2
+#define MX_M4_Q6V2 0
+#endif
+constexpr int M4_XDEF = MX_M4_Q6V2 ? 8 : 0;
 #ifndef MX_M4_LDA
 #define MX_M4_LDA 1               // MFMA steps the LDS activation reads run ahead (1 or 2)
 #endif
@@ -123,8 +134,8 @@ __device__ __forceinline__ uint32_t pair_bytes(uint32_t w, int hi_pair) {
 __device__ __forceinline__ h2 as_h2(uint32_t u) { h2 v; __builtin_memcpy(&v, &u, 4); return v; }
 // (x & m) | b as one v_and_or_b32 (mask from an SGPR, bias from a VGPR: GFX9 VOP3 reads
 // one constant-bus operand and no literal; the compiler otherwise emits v_and + v_or)
-#ifndef MX_M4_ANDOR
-#define MX_M4_ANDOR 0
+#ifndef MX_M4_ANDOR      // same box: glu 210.4 -> 205.9 us, down Q4_K 97.4 -> 93.5 (profiles/r03/ab_mmq4.txt)
+#define MX_M4_ANDOR 1
 #endif
 __device__ __forceinline__ uint32_t m4_and_or(uint32_t x, uint32_t m, uint32_t b) {
 #if MX_M4_ANDOR
@@ -176,7 +187,7 @@ __device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, i
 
 // B operand of MFMA step q of unit j (q 0,1: the low sub-block's positions 8q..8q+7 of
 // the 16-byte chunk; q 2,3: the high one's 8(q-2)..), element e = position + e
-template <int QT>
+template <int QT, int X>
 __device__ __forceinline__ h8 m4_deq(const M4W<QT> & r, const M4Scale & s, int h, int j, int q) {
     const bool hi = q >= 2;
     const int pd = 2 * (q & 1);                                // first of the chunk's two dwords
@@ -209,6 +220,23 @@ __device__ __forceinline__ h8 m4_deq(const M4W<QT> & r, const M4Scale & s, int h
         const int sh = (hi ? 4 : 0) + 2 * h;                   // qh bit pair: position < 32 (h 0) or not
 #pragma unroll
         for (int dd = 0; dd < 2; ++dd) {
+            if constexpr (X & 8) {
+            // per dword: the four 2-bit qh fields OR'd into the f16 exponent byte 0x54 (one
+            // v_and_or), then per value pair one perm puts them in the high bytes, one
+            // v_and_or adds the nibbles (pre-shifted for the low half): ~6.5 VALU per pair
+            // instead of ~10.5
+            uint32_t w = dw(ql, pd + dd);
+            if (!hi) w <<= 4;
+            const uint32_t t = m4_and_or(dw(qhv, pd + dd) >> sh, 0x03030303u, 0x54545454u);
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const uint32_t hb = __builtin_amdgcn_perm(0u, t, pp ? 0x030c020cu : 0x010c000cu);
+                const uint32_t v = m4_and_or(pair_bytes(w, pp), 0x00F000F0u, hb);          // 64 + q6
+                const h2 f = (as_h2(v) - h2{96, 96}) * (hi ? s.shi : s.slo);            // (q6 - 32) d sc
+                out[4 * dd + 2 * pp] = f[0];
+                out[4 * dd + 2 * pp + 1] = f[1];
+            }
+            } else {
             const uint32_t w = dw(ql, pd + dd), qh = dw(qhv, pd + dd);
 #pragma unroll
             for (int pp = 0; pp < 2; ++pp) {
@@ -218,6 +246,7 @@ __device__ __forceinline__ h8 m4_deq(const M4W<QT> & r, const M4Scale & s, int h
                 const h2 f = (as_h2(v) - h2{96, 96}) * (hi ? s.shi : s.slo);            // (q6 - 32) d sc
                 out[4 * dd + 2 * pp] = f[0];
                 out[4 * dd + 2 * pp + 1] = f[1];
+            }
             }
         }
     }
@@ -251,7 +280,7 @@ constexpr int M4_S = 4;            // activation ring stages (prefetch distance 
 // each of this wave's DMA pieces). Weight registers rotate over three sets (loads two
 // chunks ahead), the activation ring runs M4_S - 1 chunks ahead; one barrier per chunk
 // (it also retires the stage the previous chunk read, which the DMA then refills).
-template <int QT, int TT>
+template <int QT, int TT, int X>
 __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, const int (&cols)[TT],
                                          uint4 * lds, int c0, int nc, f16v (&acc)[TT], unsigned long long * tr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -299,9 +328,15 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
         for (int st = 0; st < 8; ++st) {
             const int j = st >> 2, q = st & 3;
             const M4Scale & s = sj[j];
-            h8 (&cur)[TT] = af[st % (D + 1)];
-            if (st + D < 8) lda(L, (st + D) >> 2, (st + D) & 3, af[(st + D) % (D + 1)]);
-            const h8 b = m4_deq<QT>(rw, s, h, j, q);
+            h8 (&cur)[TT] = af[(X & 4) ? 0 : st % (D + 1)];
+            if (!(X & 4) && st + D < 8) lda(L, (st + D) >> 2, (st + D) & 3, af[(st + D) % (D + 1)]);
+            h8 b;
+            if constexpr (X & 2) {   // timing only
+                int4 w;
+                if constexpr (QT == GGML_TYPE_Q6_K) w = j ? rw.l1 : rw.l0; else w = j ? rw.q1 : rw.q0;
+                __builtin_memcpy(&b, &w, 16);
+            }
+            else b = m4_deq<QT, X>(rw, s, h, j, q);
 #pragma unroll
             for (int t = 0; t < TT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], b, acc[t], 0, 0, 0);
         }
@@ -319,10 +354,12 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
     auto iter = [&](int i, const M4W<QT> & rc, M4W<QT> & rn) {
         // instructions issued after DMA(i): >= DMA(i+1), DMA(i+2) and two chunks of weight
         // loads in steady state; the last chunks drain everything
-        if (i + 2 < nc) m4_wait_vm<2 * NDMA + 2 * NW>();
-        else m4_wait_vm<0>();
+        if constexpr (!(X & 1)) {
+            if (i + 2 < nc) m4_wait_vm<2 * NDMA + 2 * NW>();
+            else m4_wait_vm<0>();
+        }
         if (i == 2) MX_TRACE(tr, 2);
-        m4_barrier();
+        if constexpr (!(X & 1)) m4_barrier();
         if (i == 2) MX_TRACE(tr, 3);
         __builtin_amdgcn_sched_barrier(0);
         if (i + M4_S - 1 < nc) dma(i + M4_S - 1);
@@ -346,7 +383,7 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
 // gathered through p.gather, outputs scattered through p.scatter.
 // Split K (EPI 0, grid.z = p.ksplit > 1): each workgroup sums its share of the K chunks
 // into p.part[z][token][global row]; k_mmq4_reduce adds the shares in order.
-template <int QTA, int QTB, int TT, int EPI>
+template <int QTA, int QTB, int TT, int EPI, int X = M4_XDEF>
 __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
     extern __shared__ __align__(16) uint4 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -398,8 +435,8 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
     f16v acc[TT];
     unsigned long long * tr = (blockIdx.x | blockIdx.y | blockIdx.z) == 0 ? p.trace : nullptr;
     MX_TRACE(tr, 0);
-    if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT>(p, wrow, cols, lds, c0, nc, acc, tr);
-    else m4_kloop<QTB, TT>(p, wrow, cols, lds, c0, nc, acc, tr);
+    if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT, X>(p, wrow, cols, lds, c0, nc, acc, tr);
+    else m4_kloop<QTB, TT, X>(p, wrow, cols, lds, c0, nc, acc, tr);
 
     if (p.trace_blk && tid == 0 && bid < 65536) p.trace_blk[2 * bid + 1] = __builtin_amdgcn_s_memrealtime();
     constexpr float inv = 1.0f / M4_WSCALE;
@@ -481,15 +518,30 @@ bool mmq4_on() { return g_tune[17] != 1 && getenv("GGML_MI355X_MMQ4_OFF") == nul
 static bool m4_all() { return g_tune[17] >= 2; }
 static bool m4_plain_ok(int64_t K) { return m4_all() || (g_tune[17] == 0 && K >= 8192); }
 
-template <int QTA, int QTB, int TT, int EPI>
-static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
+template <int QTA, int QTB, int TT, int EPI, int X = M4_XDEF>
+static void m4_kernel_x(hipStream_t st, const M4Args & a, dim3 g) {
     constexpr int lds = M4_S * 32 * TT * 256;
     static const bool attr = [] {
-        HIP_CHECK(hipFuncSetAttribute((const void *) k_mmq4<QTA, QTB, TT, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        HIP_CHECK(hipFuncSetAttribute((const void *) k_mmq4<QTA, QTB, TT, EPI, X>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         return true;
     }();
     (void) attr;
-    k_mmq4<QTA, QTB, TT, EPI><<<g, 64 * M4_WAVES, lds, st>>>(a);
+    k_mmq4<QTA, QTB, TT, EPI, X><<<g, 64 * M4_WAVES, lds, st>>>(a);
+}
+
+template <int QTA, int QTB, int TT, int EPI>
+static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
+    if constexpr (QTA == QTB && TT == 4 && EPI < 2 && QTA != GGML_TYPE_Q5_K) {
+        switch (g_tune[31]) {   // timing experiments (X bits above), the prefill GEMM shapes only
+            case 1: return m4_kernel_x<QTA, QTB, TT, EPI, 1 | M4_XDEF>(st, a, g);
+            case 2: return m4_kernel_x<QTA, QTB, TT, EPI, 2 | M4_XDEF>(st, a, g);
+            case 4: return m4_kernel_x<QTA, QTB, TT, EPI, 4 | M4_XDEF>(st, a, g);
+            case 7: return m4_kernel_x<QTA, QTB, TT, EPI, 7 | M4_XDEF>(st, a, g);
+            case 8: return m4_kernel_x<QTA, QTB, TT, EPI, 8>(st, a, g);
+            default: break;
+        }
+    }
+    m4_kernel_x<QTA, QTB, TT, EPI>(st, a, g);
 }
 
 template <int EPI, int TT>
