@@ -42,10 +42,15 @@ constexpr int M4_KC = 128;        // K per chunk (half a super-block)
 // timing experiments only (g_tune[31], results wrong): 1 no per-chunk wait and barrier,
 // 2 no dequantisation (raw weight bits as the B operand), 4 LDS activation fragments read
 // once per chunk
+// Defaults measured on MI355X (opbench after a warm-up arm, profiles/r03/ab_mmq4_x.txt):
+// glu 185.7 -> 173.5 us, down Q4_K 83.8 -> 77.4 us (X 0 -> 24)
 #ifndef MX_M4_Q6V2
-#define MX_M4_Q6V2 0
+#define MX_M4_Q6V2 1
 #endif
-constexpr int M4_XDEF = MX_M4_Q6V2 ? 8 : 0;
+#ifndef MX_M4_PIPE
+#define MX_M4_PIPE 1
+#endif
+constexpr int M4_XDEF = (MX_M4_Q6V2 ? 8 : 0) | (MX_M4_PIPE ? 16 : 0);
 #ifndef MX_M4_LDA
 #define MX_M4_LDA 1               // MFMA steps the LDS activation reads run ahead (1 or 2)
 #endif
@@ -318,12 +323,37 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
         const uint4 * L = lds + (i % M4_S) * TILE;
         const int kc = c0 + i;
         // activation fragments MX_M4_LDA steps ahead (ring of MX_M4_LDA + 1 register sets)
-        constexpr int D = MX_M4_LDA;
+        constexpr int D = (X & 16) ? 2 : MX_M4_LDA;
         h8 af[D + 1][TT];
 #pragma unroll
         for (int st = 0; st < D; ++st) lda(L, st >> 2, st & 3, af[st]);
         // the two units' scales once per chunk (they depend on j only, not on the step)
         const M4Scale sj[2] = {m4_scales<QT>(rw, kc, h, 0), m4_scales<QT>(rw, kc, h, 1)};
+        if constexpr (X & 16) {
+            // software-pipelined: step st+1's B operand is dequantised while step st's MFMAs
+            // run, the schedule interleaving one MFMA, one LDS read and NV VALU instructions
+            // (a block of 4 MFMAs followed by the dequantisation left the matrix pipe idle
+            // while the VALU ran, with both waves of a SIMD in the same phase)
+            constexpr int NV = QT == GGML_TYPE_Q6_K ? 7 : 6;
+            h8 bq[2];
+            bq[0] = m4_deq<QT, X>(rw, sj[0], h, 0, 0);
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                h8 (&cur)[TT] = af[st % (D + 1)];
+                if (st + D < 8) lda(L, (st + D) >> 2, (st + D) & 3, af[(st + D) % (D + 1)]);
+                if (st + 1 < 8) bq[(st + 1) & 1] = m4_deq<QT, X>(rw, sj[(st + 1) >> 2], h, (st + 1) >> 2, (st + 1) & 3);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], bq[st & 1], acc[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);   // one scheduling region per step
+            }
+            return;
+        }
 #pragma unroll
         for (int st = 0; st < 8; ++st) {
             const int j = st >> 2, q = st & 3;
@@ -511,12 +541,13 @@ __global__ void k_mmq4_reduce(M4Args p) {
 // ---------------------------------------------------------------------------
 static bool m4_kq(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
 
-// g_tune[17]: 0 = v4 where it measured faster than v2/v3 (profiles/r02/opbench_mmq4.txt:
-// the gate/up/SwiGLU pair, and plain GEMMs over K >= 8192 — the FFN down projection), 1 =
-// v4 off, 3 = v4 everywhere, 2 / 4 = v4 everywhere at 64 / 128 tokens per tile
+// g_tune[17]: 0 = v4 for every K-quant prefill GEMM it takes (round 3: with the pipelined
+// loop and the cost-model split, also the q/k/v group and the K = 4096 projections),
+// 5 = round 2's choice (v4 for the gate/up/SwiGLU pair and K >= 8192 only), 1 = v4 off,
+// 3 = v4 everywhere, 2 / 4 = v4 everywhere at 64 / 128 tokens per tile
 bool mmq4_on() { return g_tune[17] != 1 && getenv("GGML_MI355X_MMQ4_OFF") == nullptr; }
-static bool m4_all() { return g_tune[17] >= 2; }
-static bool m4_plain_ok(int64_t K) { return m4_all() || (g_tune[17] == 0 && K >= 8192); }
+static bool m4_all() { return g_tune[17] != 5; }
+static bool m4_plain_ok(int64_t K) { return m4_all() || K >= 8192; }
 
 template <int QTA, int QTB, int TT, int EPI, int X = M4_XDEF>
 static void m4_kernel_x(hipStream_t st, const M4Args & a, dim3 g) {
@@ -534,10 +565,10 @@ static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
     if constexpr (QTA == QTB && TT == 4 && EPI < 2 && QTA != GGML_TYPE_Q5_K) {
         switch (g_tune[31]) {   // timing experiments (X bits above), the prefill GEMM shapes only
             case 1: return m4_kernel_x<QTA, QTB, TT, EPI, 1 | M4_XDEF>(st, a, g);
-            case 2: return m4_kernel_x<QTA, QTB, TT, EPI, 2 | M4_XDEF>(st, a, g);
-            case 4: return m4_kernel_x<QTA, QTB, TT, EPI, 4 | M4_XDEF>(st, a, g);
-            case 7: return m4_kernel_x<QTA, QTB, TT, EPI, 7 | M4_XDEF>(st, a, g);
-            case 8: return m4_kernel_x<QTA, QTB, TT, EPI, 8>(st, a, g);
+            case 2: return m4_kernel_x<QTA, QTB, TT, EPI, 2 | (M4_XDEF & 8)>(st, a, g);
+            case 4: return m4_kernel_x<QTA, QTB, TT, EPI, 4 | (M4_XDEF & 8)>(st, a, g);   // (no pipelining)
+            case 7: return m4_kernel_x<QTA, QTB, TT, EPI, 7 | (M4_XDEF & 8)>(st, a, g);
+            case 32: return m4_kernel_x<QTA, QTB, TT, EPI, 0>(st, a, g);                  // round-2 form
             default: break;
         }
     }
@@ -564,20 +595,28 @@ static int m4_tt() {
     return 4;
 }
 
-// K shares so that the grid holds >= one workgroup per CU (the workgroup takes the CU:
-// 128 KB ring), each share >= 4 chunks; g_tune[20] forces it
-static int m4_ksplit(int64_t wgs, int nk) {
+// K shares: the k_mmq4 workgroup takes a whole CU (128 KB ring), so a grid of G
+// workgroups runs in ceil(G / 256) rounds of ceil(nk / ks) chunks each (~2.7 us per chunk
+// at 128 tokens, profiles/r03/ab_mmq4_x.txt); a split adds the k_mmq4_reduce pass (launch
+// + (ks + 1) partial planes of N x M floats at ~5 TB/s). Pick the cheapest ks <= 8 with
+// >= 4 chunks per share. g_tune[20] forces it.
+static int m4_ksplit(int64_t wgs, int nk, int64_t n, int64_t m) {
     if (g_tune[20] > 0) return std::min(g_tune[20], nk);
-    int ks = 1;
-    while (wgs * ks < 256 && nk / (2 * ks) >= 4 && ks < 8) ks *= 2;
-    return ks;
+    int best = 1;
+    double bt = 1e30;
+    for (int ks = 1; ks <= 8 && nk / ks >= 4; ++ks) {
+        const double t = (double) mx_ceil_div(wgs * ks, 256) * (double) mx_ceil_div(nk, ks) * 2.7 +
+                         (ks > 1 ? 2.0 + (double) (ks + 1) * (double) (n * m * 4) / 5e6 : 0.0);
+        if (t < bt) { bt = t; best = ks; }
+    }
+    return best;
 }
 
 size_t mmq4_scratch(const ggml_tensor * dst) {
     const ggml_tensor * w = dst->src[0], * x = dst->src[1];
     if (!m4_kq(w->type) || x->ne[1] <= 8) return 0;
     const int64_t rows = mx_ceil_div(w->ne[1] + w->ne[1] / 2, 256) * 256;   // room for a q/k/v group
-    const int ks = m4_ksplit(mx_ceil_div(x->ne[1], 128) * mx_ceil_div(w->ne[1], 256), (int) (w->ne[0] / M4_KC));
+    const int ks = m4_ksplit(mx_ceil_div(x->ne[1], 128) * mx_ceil_div(rows, 256), (int) (w->ne[0] / M4_KC), x->ne[1], rows);
     return ks > 1 ? (size_t) ks * x->ne[1] * rows * 4 + 256 : 0;
 }
 
@@ -590,7 +629,7 @@ static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int 
     const int64_t gx = mx_ceil_div(a.N, 32 * tt);
     a.ksplit = 1;
     if (EPI == 0) {
-        int ks = m4_ksplit(gx * tiles_y, nk);
+        int ks = m4_ksplit(gx * tiles_y, nk, a.N, (int64_t) tiles_y * 32 * M4_WAVES);
         const size_t need = (size_t) ks * a.N * tiles_y * 32 * M4_WAVES * 4;
         if (ks > 1 && c.scratch->avail() >= need + 256) {
             a.ksplit = ks;

@@ -82,6 +82,22 @@ def case_gemm(pkg, be, rng, tname, K, M, N=512):
     return ctx, [g]
 
 
+def case_gemm_qkv(pkg, be, rng, K=4096, Mq=4096, Mkv=1024, tv="q4_K", N=512):
+    """prefill q/k/v projections sharing x (one graph: the executor's grouped GEMM)"""
+    tq = NAMES["q4_K"]
+    wq, _ = rand_quant(tq, Mq, K, rng)
+    wk, _ = rand_quant(tq, Mkv, K, rng)
+    wv, _ = rand_quant(NAMES[tv], Mkv, K, rng)
+    ctx = pkg.Context()
+    x = ctx.new_tensor("f32", K, N)
+    a, b, c = ctx.new_tensor(tq, K, Mq), ctx.new_tensor(tq, K, Mkv), ctx.new_tensor(NAMES[tv], K, Mkv)
+    g = ctx.build(ctx.mul_mat(a, x), ctx.mul_mat(b, x), ctx.mul_mat(c, x))
+    ctx.alloc(be)
+    a.set(wq); b.set(wk); c.set(wv)
+    x.set(rng.standard_normal((N, K)).astype(np.float32))
+    return ctx, [g]
+
+
 def case_gemm_glu(pkg, be, rng, tname, K, M, N=512):
     """prefill gate/up/SwiGLU GEMM pair (fused): 2 x M weight rows x N tokens over K."""
     tid = NAMES[tname]
@@ -246,6 +262,10 @@ CASES = {
     "pp_down_q6k": lambda p, b, r: case_gemm(p, b, r, "q6_K", 14336, 4096),
     "pp_k_q4k": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 1024),
     "pp_glu_q4k": lambda p, b, r: case_gemm_glu(p, b, r, "q4_K", 4096, 14336),
+    "pp_qkv": lambda p, b, r: case_gemm_qkv(p, b, r),
+    "pp_qkv_v6": lambda p, b, r: case_gemm_qkv(p, b, r, tv="q6_K"),
+    "pp_glu_q4k_2048": lambda p, b, r: case_gemm_glu(p, b, r, "q4_K", 4096, 14336, N=2048),
+    "pp_q_q4k_2048": lambda p, b, r: case_gemm(p, b, r, "q4_K", 4096, 4096, N=2048),
     "pp_glu_q5k": lambda p, b, r: case_gemm_glu(p, b, r, "q5_K", 4096, 14336),
     "pp_moe_q5k": lambda p, b, r: case_moe(p, b, r),
     "pp_moe_q5k_skew": lambda p, b, r: case_moe(p, b, r, skew=0.9),
