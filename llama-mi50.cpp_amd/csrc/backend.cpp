@@ -723,6 +723,8 @@ extern "C" size_t ggml_backend_mi355x_klog_read(char * out, size_t n) {
     return mx::g_klog_buf.size();
 }
 
+namespace mx { unsigned g_tune_gen = 0; }   // part of every cgraph signature (exec.cpp)
+// a changed knob changes the launches a graph makes: captured graphs must not replay
 extern "C" void ggml_backend_mi355x_set_tune(int idx, int value) {
-    if (idx >= 0 && idx < 32) mx::g_tune[idx] = value;
+    if (idx >= 0 && idx < 32 && mx::g_tune[idx] != value) { mx::g_tune[idx] = value; ++mx::g_tune_gen; }
 }

@@ -216,6 +216,9 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses
 int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i);
 // -fa 0 decode attention chain (ops_fattn_dec.hip)
 int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
+// FLASH_ATTN_EXT -> RESHAPE -> MUL_MAT(wo) -> ADD(residual) of one decode token (ops_attn_o.hip)
+int fuse_attn_oproj(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
+bool t_overlaps_ext(const ggml_tensor * a, const ggml_tensor * b);
 int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 // the executor's guard for a node about to run (deferred norms it reads or overwrites)
 void deferred_guard_node_ext(OpCtx & c, const ggml_tensor * n);

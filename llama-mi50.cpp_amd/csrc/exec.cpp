@@ -59,9 +59,10 @@ static inline void sig_tensor(SigCursor & c, const ggml_tensor * t) {
 }
 
 // returns true when g's signature equals the stored key (which is updated to g's)
+extern unsigned g_tune_gen;   // backend.cpp: bumped by every changed ggml_backend_mi355x_set_tune
 static bool graph_signature_same(const ggml_cgraph * g, std::vector<uint64_t> & key) {
     SigCursor c{key};
-    c.put((uint64_t) g->n_nodes);
+    c.put((uint64_t) g->n_nodes | ((uint64_t) g_tune_gen << 32));
     for (int i = 0; i < g->n_nodes; ++i) {
         const ggml_tensor * n = g->nodes[i];
         sig_tensor(c, n);
@@ -99,6 +100,7 @@ static bool overlaps(const void * a, size_t na, const void * b, size_t nb) {
 static bool t_overlaps(const ggml_tensor * a, const ggml_tensor * b) {
     return a && b && a->data && b->data && overlaps(a->data, mx_nbytes(a), b->data, mx_nbytes(b));
 }
+bool t_overlaps_ext(const ggml_tensor * a, const ggml_tensor * b) { return t_overlaps(a, b); }
 
 XStage xstage_of(Stream * s, const ggml_tensor * x) {
     for (const DeferredNorm & d : s->deferred)
@@ -456,6 +458,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             if (n->op == GGML_OP_MUL_MAT && !g_no_attn_nofa) {
                 const int k = fuse_attn_nofa(c, g, i, uses);
                 if (k > 0) { i += k - 1; s->n_fused += 3; s->n_nodes_run += 4; deferred_retire(s, g, i0, i); continue; }
+            }
+            if (n->op == GGML_OP_FLASH_ATTN_EXT) {
+                const int k = fuse_attn_oproj(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             }
             if (n->op == GGML_OP_MUL_MAT_ID && try_fuse_moe_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
             if (n->op == GGML_OP_SOFT_MAX && !g_no_moe_fusion && !g_no_topk) {

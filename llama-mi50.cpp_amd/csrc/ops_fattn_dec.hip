@@ -423,7 +423,8 @@ bool fa_dec2_ok(const ggml_tensor * dst) {
     } else if (k->nb[1] % 16 || v->nb[1] % 16 || k->nb[2] % 16 || v->nb[2] % 16 || (uintptr_t) k->data % 16 || (uintptr_t) v->data % 16) return false;
     if (q->nb[1] % 16 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return false;
     if (q->ne[3] != k->ne[3] && k->ne[3] != 1) return false;
-    if (k->ne[1] > INT32_MAX / 2 || q->ne[1] * q->ne[3] * q->ne[2] > MX_FA_CNT) return false;
+    // counters [0, MX_FA_CNT / 2): the upper half holds k_attn_o's row-chunk epochs (ops_attn_o.hip)
+    if (k->ne[1] > INT32_MAX / 2 || q->ne[1] * q->ne[3] * q->ne[2] > MX_FA_CNT / 2) return false;
     // caches beyond one 16-wave chunk take the LONG geometry (fd_cfg); g_tune[10] = 4 keeps
     // them on the v1 kernel + combine (round-2 behaviour: 18.4 + 12.0 us at 16k keys)
     if (g_tune[10] == 4 && !kq && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;

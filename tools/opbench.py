@@ -235,6 +235,39 @@ def case_fa(pkg, be, rng, n_kv, H=32, Hkv=8, D=128, n_q=1):
     return ctx, [g]
 
 
+def case_attn_o(pkg, be, rng, n_kv=256, H=32, Hkv=8, D=128, M=4096):
+    """decode attention -> output projection (Q4_K) -> + residual: one k_attn_o launch
+    (ops_attn_o.hip, opt-in): --ab 27=64 (v2), 27=96 (v2, one key split), 27=16 (v1); the
+    default runs it unfused (k_fattn_dec2 + the GEMV)"""
+    from qgen import NAMES
+    K = D * H
+    w, _ = rand_quant(NAMES["q4_K"], M, K, rng)
+    n = copies_for(len(w))
+    ctx = pkg.Context()
+    q = ctx.new_tensor("f32", D, 1, H)
+    k = ctx.new_tensor("f16", D, n_kv, Hkv)
+    v = ctx.new_tensor("f16", D, n_kv, Hkv)
+    m = ctx.new_tensor("f16", n_kv, 1)
+    r = ctx.new_tensor("f32", M, 1)
+    fa = ctx.flash_attn_ext(q, k, v, m, 1.0 / np.sqrt(D))
+    ws, graphs = [], []
+    for _ in range(n):
+        tw = ctx.new_tensor(NAMES["q4_K"], K, M)
+        ws.append(tw)
+        graphs.append(None)
+    outs = [ctx.add(ctx.mul_mat(tw, ctx.reshape(fa, K, 1)), r) for tw in ws]
+    graphs = [ctx.build(o) for o in outs]
+    ctx.alloc(be)
+    for tw in ws:
+        tw.set(w)
+    q.set(rng.standard_normal((H, 1, D)).astype(np.float32))
+    k.set(rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16))
+    v.set(rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16))
+    m.set(np.zeros((1, n_kv), np.float16).view(np.uint16))
+    r.set(rng.standard_normal(M).astype(np.float32))
+    return ctx, graphs
+
+
 def case_rms(pkg, be, rng, K=4096):
     ctx = pkg.Context()
     x = ctx.new_tensor("f32", K, 1)
@@ -287,6 +320,7 @@ CASES = {
     "fa_pp512": lambda p, b, r: case_fa(p, b, r, 512, n_q=512),
     "fa_pp2048": lambda p, b, r: case_fa(p, b, r, 2048, n_q=512),
     "rms_mul": lambda p, b, r: case_rms(p, b, r),
+    "attn_o": lambda p, b, r: case_attn_o(p, b, r),
 }
 
 
