@@ -56,6 +56,37 @@ __device__ __forceinline__ uint2 ldu8(const char * p) {   // 8 bytes, any 2-byte
     return v;
 }
 
+// Reductions over the key rows of a wave: lanes l ^ LPK, l ^ 2 LPK, ... For LPK = 16 (D 128)
+// by the gfx950 row-swap instructions (VALU; with both operands = v the two results add up
+// to v[l] + v[l ^ 16] / v[l ^ 32]) instead of ds_bpermute shuffles (the same change took
+// ~1 us of latency out of ops_attn_o.hip's attention); other LPK by shuffles.
+template <int LPK>
+__device__ __forceinline__ float kr_sum(float v) {
+    if constexpr (LPK == 16) {
+        auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+        auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    } else {
+#pragma unroll
+        for (int off = LPK; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+        return v;
+    }
+}
+template <int LPK>
+__device__ __forceinline__ float kr_max(float v) {
+    if constexpr (LPK == 16) {
+        auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+    } else {
+#pragma unroll
+        for (int off = LPK; off < 64; off <<= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+        return v;
+    }
+}
+
 // G = query heads per workgroup (a divisor of the GQA ratio Gt; K/V are read once per
 // workgroup), NW = waves per workgroup (the chunk is NW x NI x 64/(D/8) keys), NI = key-row
 // load instructions per wave and chunk. LONG (round 3, caches beyond one chunk): every
@@ -224,15 +255,13 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             float mc = s[h][0];
 #pragma unroll
             for (int t = 1; t < NI; ++t) mc = fmaxf(mc, s[h][t]);
-#pragma unroll
-            for (int off = LPK; off < 64; off <<= 1) mc = fmaxf(mc, __shfl_xor(mc, off, 64));
+            mc = kr_max<LPK>(mc);
             const float Mn = fmaxf(M[h], mc);
             const float a = M[h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(M[h] - Mn);
             float pr[NI], lc = 0.f;
 #pragma unroll
             for (int t = 0; t < NI; ++t) { pr[t] = Mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[h][t] - Mn); lc += pr[t]; }
-#pragma unroll
-            for (int off = LPK; off < 64; off <<= 1) lc += __shfl_xor(lc, off, 64);
+            lc = kr_sum<LPK>(lc);
             L[h] = L[h] * a + lc;
             M[h] = Mn;
 #pragma unroll
@@ -259,9 +288,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
 #pragma unroll
     for (int h = 0; h < G; ++h) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int off = LPK; off < 64; off <<= 1) o[h][i] += __shfl_xor(o[h][i], off, 64);
+        for (int i = 0; i < 8; ++i) o[h][i] = kr_sum<LPK>(o[h][i]);
         if (lane == 0) { wm[wave][h] = M[h]; wl[wave][h] = L[h]; }
         if (kq == 0) {
             *(float4 *) &wo[wave][h][8 * c] = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
