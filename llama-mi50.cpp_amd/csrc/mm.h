@@ -28,6 +28,12 @@ bool mmq4_moe(OpCtx & c, ggml_tensor * dst);     // MUL_MAT_ID prefill, expert-g
 bool mmq4_mul_mat(OpCtx & c, const ggml_tensor * w, const ggml_tensor * x, const _Float16 * xa, int64_t kp,
                   ggml_tensor * out, const ggml_tensor * res);
 bool mmq4_group(OpCtx & c, ggml_tensor * const * mms, int n, const _Float16 * xa, int64_t kp);
+// split-K partials handed to a consumer instead of k_mmq4_reduce (ops_qkv.hip's prefill
+// q/k/v epilogue sums them itself): while g_m4_split is set, a split segment-group launch
+// without residual / f16 copy fills it (ks > 1) and skips the reduce pass. Partial of
+// (plane z, token t, global row r): part[(z N + t) part_ld + r]; segment s starts at row0[s].
+struct M4Split { const float * part; int part_ld; int ks; int row0[3]; };
+extern thread_local M4Split * g_m4_split;
 bool mmq4_glu_ok(const ggml_tensor * wg, const ggml_tensor * wu, const ggml_tensor * x, const ggml_tensor * glu);
 void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const ggml_tensor * x, const _Float16 * xa,
               int64_t kp, ggml_tensor * glu, _Float16 * h, int64_t h_col);

@@ -545,6 +545,8 @@ static bool m4_kq(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || 
 // loop and the cost-model split, also the q/k/v group and the K = 4096 projections),
 // 5 = round 2's choice (v4 for the gate/up/SwiGLU pair and K >= 8192 only), 1 = v4 off,
 // 3 = v4 everywhere, 2 / 4 = v4 everywhere at 64 / 128 tokens per tile
+thread_local M4Split * g_m4_split = nullptr;
+
 bool mmq4_on() { return g_tune[17] != 1 && getenv("GGML_MI355X_MMQ4_OFF") == nullptr; }
 static bool m4_all() { return g_tune[17] != 5; }
 static bool m4_plain_ok(int64_t K) { return m4_all() || K >= 8192; }
@@ -640,7 +642,16 @@ static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int 
     }
     const dim3 g = EPI == 2 ? dim3((unsigned) tiles_y, (unsigned) gx, (unsigned) nz) : dim3((unsigned) gx, (unsigned) tiles_y, (unsigned) nz);
     const bool ok = tt == 4 ? m4_go<EPI, 4>(c.st, a, ta, tb, g) : m4_go<EPI, 2>(c.st, a, ta, tb, g);
-    if (ok && a.ksplit > 1) {
+    bool taken = false;
+    if (ok && a.ksplit > 1 && g_m4_split && !a.h) {
+        taken = true;
+        for (int s = 0; s < a.nseg; ++s) taken = taken && a.seg[s].res == nullptr;
+        if (taken) {
+            g_m4_split->part = a.part; g_m4_split->part_ld = a.part_ld; g_m4_split->ks = a.ksplit;
+            for (int s = 0; s < 3; ++s) g_m4_split->row0[s] = s < a.nseg ? a.seg[s].tile0 * 32 * M4_WAVES : 0;
+        }
+    }
+    if (ok && a.ksplit > 1 && !taken) {
         const dim3 gr((unsigned) mx_ceil_div(a.part_ld, 256), (unsigned) a.N);
         k_mmq4_reduce<<<gr, 256, 0, c.st>>>(a);
     }

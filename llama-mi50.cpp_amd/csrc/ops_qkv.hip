@@ -10,6 +10,8 @@
 // (ggml-cuda.cu:3088-3122). Semantics per node are unchanged: GEMV as mmvq,
 // RoPE as ops.cpp:5523-5800 (theta by repeated multiplication), f32→f16 RNE stores.
 #include "backend.h"
+#include "mm.h"
+#include <functional>
 #include "gemv.cuh"
 
 namespace mx {
@@ -143,10 +145,8 @@ __global__ __launch_bounds__(256) void k_kv_store_q8(QkvArgs p, int nk, int nv) 
 // (cos θ·m, sin θ·m) for every dimension pair of one position: rope_yarn
 // (ggml-cpu/ops.cpp:5529-5546) with theta by repeated multiplication as rope_cache_init
 // (ops.cpp:5548-5566) — the per-pair values of op_rope, computed once per token.
-__global__ void k_rope_table(QkvArgs p, float2 * tab) {
-    const int i = threadIdx.x + blockIdx.x * blockDim.x;   // pair index
-    if (i >= p.n_dims / 2) return;
-    float theta = (float) p.pos[0];
+__device__ __forceinline__ float2 qkv_rope_cs(const QkvArgs & p, float pf, int i) {
+    float theta = pf;
     for (int k = 0; k < i; ++k) theta *= p.theta_scale;
     if (p.ff) theta /= p.ff[i];
     const float ti = p.freq_scale * theta;
@@ -157,7 +157,71 @@ __global__ void k_rope_table(QkvArgs p, float2 * tab) {
         th = ti * (1 - mix) + theta * mix;
         ms *= 1.0f + 0.1f * logf(1.0f / p.freq_scale);
     }
-    tab[i] = make_float2(cosf(th) * ms, sinf(th) * ms);
+    return make_float2(cosf(th) * ms, sinf(th) * ms);
+}
+
+__global__ void k_rope_table(QkvArgs p, float2 * tab) {
+    const int i = threadIdx.x + blockIdx.x * blockDim.x;   // pair index
+    if (i >= p.n_dims / 2) return;
+    tab[i] = qkv_rope_cs(p, (float) p.pos[0], i);
+}
+
+// Prefill (n_tokens > 1) epilogue of the q/k/v projections (round 3): ROPE(q) -> the rope
+// output, ROPE(k) -> K cache rows, v -> V cache rows, in one launch after the grouped GEMM
+// instead of 2 ROPE + 2 SET_ROWS launches (k_rope2 + k_set_rows: ~26 us per pp512 layer).
+// One workgroup per token: its (cos, sin) table in LDS (qkv_rope_cs: the k_rope2 / CPU
+// values, bit-identical), then every adjacent row pair of q, k and v (NORMAL rope pairs
+// 2i, 2i+1); f32 -> f16 cache stores round to nearest even as SET_ROWS does.
+struct QkvPpArgs {
+    const float * q; const float * k; const float * v;   // projections [M, N] f32, contiguous
+    const float * part; int part_ld, ks, N, row0[3];     // SPLIT: the GEMM's split-K partials instead (mm.h M4Split)
+    float * rq;                                          // roped q [n_dims, heads, N], contiguous
+    char * kc; size_t kc_nb1; const int64_t * kidx;      // K cache view rows (f16), row per token
+    char * vc; size_t vc_nb1; const int64_t * vidx;
+    int Mq, Mk, Mv;
+};
+// SPLIT: the q/k/v GEMM ran split-K and left its partial planes; the sum over planes (in
+// plane order, as k_mmq4_reduce adds them) replaces the reduce pass and its round trip
+template <bool SPLIT>
+__device__ __forceinline__ float2 qkv_pp_ld(const QkvPpArgs & e, const float * x, int seg, int t, int j) {
+    if constexpr (!SPLIT) return ((const float2 *) x)[j];
+    const float * b = e.part + (size_t) t * e.part_ld + e.row0[seg] + 2 * j;
+    float2 v = *(const float2 *) b;
+    for (int z = 1; z < e.ks; ++z) {
+        const float2 w = *(const float2 *) (b + (size_t) z * e.N * e.part_ld);
+        v.x += w.x; v.y += w.y;
+    }
+    return v;
+}
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void k_qkv_pp_epi(QkvArgs p, QkvPpArgs e) {
+    __shared__ float2 tab[MX_ROPE_TAB];
+    const int t = blockIdx.x;
+    const int np = p.n_dims / 2;
+    const float pf = (float) p.pos[t];
+    for (int i = threadIdx.x; i < np; i += blockDim.x) tab[i] = qkv_rope_cs(p, pf, i);
+    __syncthreads();
+    const int pq = e.Mq / 2, pk = e.Mk / 2, pv = e.Mv / 2;
+    const float2 * q = (const float2 *) (e.q + (size_t) t * e.Mq);
+    const float2 * k = (const float2 *) (e.k + (size_t) t * e.Mk);
+    const float2 * v = (const float2 *) (e.v + (size_t) t * e.Mv);
+    float2 * rq = (float2 *) (e.rq + (size_t) t * e.Mq);
+    uint32_t * kr = (uint32_t *) (e.kc + (size_t) e.kidx[t] * e.kc_nb1);
+    uint32_t * vr = (uint32_t *) (e.vc + (size_t) e.vidx[t] * e.vc_nb1);
+    for (int j = threadIdx.x; j < pq + pk + pv; j += blockDim.x) {
+        if (j < pq) {
+            const float2 x = qkv_pp_ld<SPLIT>(e, (const float *) q, 0, t, j), cs = tab[j % np];
+            rq[j] = make_float2(x.x * cs.x - x.y * cs.y, x.x * cs.y + x.y * cs.x);
+        } else if (j < pq + pk) {
+            const int jj = j - pq;
+            const float2 x = qkv_pp_ld<SPLIT>(e, (const float *) k, 1, t, jj), cs = tab[jj % np];
+            kr[jj] = (uint32_t) f2h(x.x * cs.x - x.y * cs.y) | ((uint32_t) f2h(x.x * cs.y + x.y * cs.x) << 16);
+        } else {
+            const int jj = j - pq - pk;
+            const float2 x = qkv_pp_ld<SPLIT>(e, (const float *) v, 2, t, jj);
+            vr[jj] = (uint32_t) f2h(x.x) | ((uint32_t) f2h(x.y) << 16);
+        }
+    }
 }
 
 static const ggml_tensor * base_of(const ggml_tensor * t) {
@@ -167,6 +231,95 @@ static const ggml_tensor * base_of(const ggml_tensor * t) {
 
 static float yarn_corr(int n_dims, int n_ctx_orig, float n_rot, float base) {
     return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float) M_PI)) / (2 * logf(base));
+}
+
+
+
+// Prefill form of the match below (n_tokens > 8, f16 caches, V stored untransposed — the
+// -fa 1 graph): the three projections as the grouped GEMM (k_mmq4 / k_mmq3m), then
+// k_qkv_pp_epi for the two ROPEs and the two SET_ROWS. g_tune[27] bit 128 or
+// GGML_MI355X_NO_QKV_PP=1: node by node (A/B).
+static const bool g_no_qkv_pp = getenv("GGML_MI355X_NO_QKV_PP") != nullptr;
+static int qkv_prefill(OpCtx & c, ggml_cgraph * g, int i, int last, const ggml_tensor * x, ggml_tensor * mq, ggml_tensor * mk,
+                       ggml_tensor * mv, ggml_tensor * rq, ggml_tensor * rk, ggml_tensor * sk, ggml_tensor * sv,
+                       const std::function<int(const ggml_tensor *)> & uses) {
+    if (g_no_qkv_pp || (g_tune[27] & 128)) return 0;
+    const int64_t N = x->ne[1];
+    if (x->ne[2] != 1 || x->ne[3] != 1 || N > INT32_MAX) return 0;
+    for (const ggml_tensor * r : {rq, rk}) {
+        if (mx_op_param<int32_t>(r, 2) != GGML_ROPE_TYPE_NORMAL || r->type != GGML_TYPE_F32 || !mx_is_contiguous(r)) return 0;
+        if (r->src[1]->type != GGML_TYPE_I32 || r->src[1]->ne[0] != N) return 0;
+    }
+    if (memcmp(rq->op_params, rk->op_params, 11 * sizeof(int32_t)) != 0 || rq->src[1] != rk->src[1] || rq->src[2] != rk->src[2]) return 0;
+    const int n_dims = mx_op_param<int32_t>(rq, 1);
+    if (n_dims != rq->ne[0] || n_dims != rk->ne[0] || n_dims % 2 || n_dims > 2 * MX_ROPE_TAB || (rq->src[2] && rq->src[2]->type != GGML_TYPE_F32)) return 0;
+    const int64_t Mq = mq->ne[0], Mk = mk->ne[0], Mv = mv->ne[0];
+    for (const ggml_tensor * m : {mq, mk, mv})
+        if (m->type != GGML_TYPE_F32 || !mx_is_contiguous(m) || m->ne[1] != N || m->ne[2] != 1 || m->ne[3] != 1 || m->ne[0] % 2) return 0;
+    if (mx_nelements(rq) != Mq * N || mx_nelements(rk) != Mk * N || Mq % n_dims || Mk % n_dims) return 0;
+    if ((mq->flags | mk->flags | mv->flags | rk->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
+    if (uses(mq) != 1 || uses(mk) != 1 || uses(mv) != 1 || uses(rk) != 1) return 0;
+    // SET_ROWS: f16 cache views, one row of the projection per token, I64 indices
+    const ggml_tensor * kix = sk->src[1], * vix = sv->src[1];
+    if (sk->type != GGML_TYPE_F16 || sv->type != GGML_TYPE_F16 || sk->nb[0] != 2 || sv->nb[0] != 2) return 0;
+    if (sk->ne[0] != Mk || sk->src[0]->ne[0] != Mk || sk->src[0]->ne[1] != N || kix->ne[0] != N || kix->type != GGML_TYPE_I64) return 0;
+    if (sv->ne[0] != Mv || sv->src[0]->ne[0] != Mv || sv->src[0]->ne[1] != N || vix->ne[0] != N || vix->type != GGML_TYPE_I64) return 0;
+    if (sk->nb[1] % 4 || sv->nb[1] % 4 || (uintptr_t) sk->data % 4 || (uintptr_t) sv->data % 4) return 0;
+    if (!mx_is_contiguous(kix) || !mx_is_contiguous(vix)) return 0;
+    for (int j = i; j <= last; ++j) {
+        deferred_guard_node_ext(c, g->nodes[j]);
+        act_cache_invalidate(c.s, g->nodes[j]);
+    }
+    // The fused launch moves mk / mv (and the stores) ahead of the nodes between the
+    // members; libllama's order (q, RoPE(q), v, k, RoPE(k): build_attn's expansion) lets the
+    // allocator place a later projection over one that has died in between (mv over mq).
+    // Overlapping outputs go to scratch copies instead (shallow tensor copies, data moved);
+    // the rope output may sit exactly on mq (each thread reads its pair before writing it).
+    const bool disjoint = !t_overlaps_ext(mq, mk) && !t_overlaps_ext(mq, mv) && !t_overlaps_ext(mk, mv) &&
+                          !t_overlaps_ext(x, mq) && !t_overlaps_ext(x, mk) && !t_overlaps_ext(x, mv) &&
+                          !t_overlaps_ext(rq, mk) && !t_overlaps_ext(rq, mv) && (rq->data == mq->data || !t_overlaps_ext(rq, mq));
+    ggml_tensor tcp[3];
+    ggml_tensor * mms[3] = {mq, mk, mv};
+    if (!disjoint) {
+        const size_t need = (size_t) (Mq + Mk + Mv) * N * sizeof(float) + 3 * 256;
+        if (c.scratch->avail() < need) return 0;
+        for (int k = 0; k < 3; ++k) {
+            tcp[k] = *mms[k];
+            tcp[k].data = c.scratch->take((size_t) mms[k]->ne[0] * N * sizeof(float));
+            mms[k] = &tcp[k];
+        }
+    }
+    M4Split sp{};
+    g_m4_split = (g_tune[27] & 256) ? nullptr : &sp;   // bit 256: keep the reduce pass (A/B)
+    const bool grouped = mmq_group_run(c, mms, 3);
+    g_m4_split = nullptr;
+    if (!grouped) { sp.ks = 0; op_mul_mat(c, mms[0]); op_mul_mat(c, mms[1]); op_mul_mat(c, mms[2]); }
+    QkvArgs p{};
+    p.pos = (const int32_t *) rq->src[1]->data;
+    p.ff = rq->src[2] ? (const float *) rq->src[2]->data : nullptr;
+    p.n_dims = n_dims;
+    const int n_ctx_orig = mx_op_param<int32_t>(rq, 4);
+    const float base = mx_op_param<float>(rq, 5);
+    p.freq_scale = mx_op_param<float>(rq, 6);
+    p.ext_factor = mx_op_param<float>(rq, 7);
+    p.attn_factor = mx_op_param<float>(rq, 8);
+    p.theta_scale = powf(base, -2.0f / n_dims);
+    p.corr0 = std::max(0.0f, floorf(yarn_corr(n_dims, n_ctx_orig, mx_op_param<float>(rq, 9), base)));
+    p.corr1 = std::min((float) (n_dims - 1), ceilf(yarn_corr(n_dims, n_ctx_orig, mx_op_param<float>(rq, 10), base)));
+    QkvPpArgs e{};
+    e.q = (const float *) mms[0]->data; e.k = (const float *) mms[1]->data; e.v = (const float *) mms[2]->data;
+    e.rq = (float *) rq->data;
+    e.kc = (char *) sk->data; e.kc_nb1 = sk->nb[1]; e.kidx = (const int64_t *) kix->data;
+    e.vc = (char *) sv->data; e.vc_nb1 = sv->nb[1]; e.vidx = (const int64_t *) vix->data;
+    e.Mq = (int) Mq; e.Mk = (int) Mk; e.Mv = (int) Mv;
+    MX_KLOG("qkv_pp N=%lld Mq=%lld Mk=%lld Mv=%lld n_dims=%d ks=%d disjoint=%d", (long long) N, (long long) Mq, (long long) Mk,
+            (long long) Mv, n_dims, sp.ks, (int) disjoint);
+    if (sp.ks > 1) {
+        e.part = sp.part; e.part_ld = sp.part_ld; e.ks = sp.ks; e.N = (int) N;
+        for (int k = 0; k < 3; ++k) e.row0[k] = sp.row0[k];
+        k_qkv_pp_epi<true><<<(unsigned) N, 256, 0, c.st>>>(p, e);
+    } else k_qkv_pp_epi<false><<<(unsigned) N, 256, 0, c.st>>>(p, e);
+    return last - i + 1;
 }
 
 // Returns the number of graph nodes consumed starting at i (0 = not fused).
@@ -206,6 +359,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     ggml_tensor * mq = (ggml_tensor *) base_of(rq->src[0]), * mk = (ggml_tensor *) base_of(rk->src[0]);
     ggml_tensor * mv = (ggml_tensor *) base_of(sv->src[0]);
     if (mq == mk || mq == mv || mk == mv) return 0;
+    if (x->ne[1] > 8) return qkv_prefill(c, g, i, last, x, mq, mk, mv, rq, rk, sk, sv, uses);
     if (x->ne[1] != 1 || x->ne[2] != 1 || x->ne[3] != 1) return 0;
     if (!g_gemv2 || !gemv2_ok(mq->src[0], x, mq) || !gemv2_ok(mk->src[0], x, mk) || !gemv2_ok(mv->src[0], x, mv)) return 0;
     const ggml_tensor * wq = mq->src[0], * wk = mk->src[0], * wv = mv->src[0];

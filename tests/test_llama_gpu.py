@@ -34,6 +34,36 @@ def test_prefill_matches_incremental_decode(pkg, tiny):
     s1.free(); s2.free()
 
 
+def test_prefill_qkv_epilogue_fusion(pkg, backend, tiny):
+    """prefill q/k/v: the grouped GEMM + ONE k_qkv_pp_epi launch for ROPE(q), ROPE(k) and
+    the two KV SET_ROWS (ops_qkv.hip qkv_prefill) against the node-by-node ROPE / SET_ROWS
+    kernels (g_tune[27] bit 128): the same GEMM and the same rope table arithmetic (the
+    rotation's multiply-adds may contract differently in the two kernels: last-bit
+    differences), so the logits and the cache contents written by the prompt agree
+    (checked through a decode step that reads the cache)"""
+    rng = np.random.default_rng(7)
+    toks = rng.integers(0, TINY["n_vocab"], 40).astype(np.int32)
+    lib = pkg._lib.load()
+    out = []
+    for tune in (0, 128):
+        lib.ggml_backend_mi355x_set_tune(27, tune)
+        try:
+            backend.klog(True)
+            s = pkg.Session(tiny, n_ctx=256, flash_attn=True)
+            a = s.decode_all(toks)
+            b = s.decode(toks[:1])
+            log = backend.klog_read()
+            backend.klog(False)
+            s.free()
+        finally:
+            lib.ggml_backend_mi355x_set_tune(27, 0)
+        assert any(l.startswith("qkv_pp ") for l in log) == (tune == 0), [l for l in log if "qkv" in l][:4]
+        out.append((a, b))
+    assert np.all(np.isfinite(out[0][0]))
+    assert nmse(out[0][0], out[1][0]) < 1e-9
+    assert nmse(out[0][1], out[1][1]) < 1e-9
+
+
 def test_flash_attn_graph_matches_softmax_graph(pkg, tiny):
     rng = np.random.default_rng(1)
     toks = rng.integers(0, TINY["n_vocab"], 12).astype(np.int32)
