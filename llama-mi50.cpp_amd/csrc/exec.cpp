@@ -245,17 +245,31 @@ static bool try_fuse_rms_mul(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
 }
 
 // MUL_MAT → ADD(mm, residual): the GEMV epilogue adds the residual
-// (attention output projection and FFN down projection of every layer).
-static bool try_fuse_mm_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
-    if (i + 1 >= g->n_nodes) return false;
+// (attention output projection and FFN down projection of every layer). Prefill, when the
+// next pair is RMS_NORM(add) → MUL(norm, w) (ffn_norm / the next attn_norm): the reduce,
+// the residual and the norm in one pass after the GEMM (ops_mm.hip mm_add_rms_norm).
+// Returns the number of nodes consumed (0: no match).
+bool mm_add_rms_norm(OpCtx & c, ggml_tensor * mm, const ggml_tensor * res, ggml_tensor * add, const ggml_tensor * norm,
+                     const ggml_tensor * w, ggml_tensor * mul);   // ops_mm.hip
+static int try_fuse_mm_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
+    if (i + 1 >= g->n_nodes) return 0;
     ggml_tensor * mm = g->nodes[i];
     ggml_tensor * add = g->nodes[i + 1];
-    if (add->op != GGML_OP_ADD) return false;
+    if (add->op != GGML_OP_ADD) return 0;
     const ggml_tensor * res = add->src[0] == mm ? add->src[1] : (add->src[1] == mm ? add->src[0] : nullptr);
-    if (!res || res == mm || uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return false;
+    if (!res || res == mm || uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
     act_cache_invalidate(c.s, add);
-    if (mmvq_small_batch_ok(mm)) return mmvq_fused_add(c, mm, res, add);
-    return mmq_fused_add(c, mm, res, add);
+    if (mmvq_small_batch_ok(mm)) return mmvq_fused_add(c, mm, res, add) ? 2 : 0;
+    if (i + 3 < g->n_nodes) {
+        ggml_tensor * norm = g->nodes[i + 2], * mul = g->nodes[i + 3];
+        const ggml_tensor * w = mul->op == GGML_OP_MUL ? (mul->src[0] == norm ? mul->src[1] : (mul->src[1] == norm ? mul->src[0] : nullptr)) : nullptr;
+        if (norm->op == GGML_OP_RMS_NORM && norm->src[0] == add && w && uses[norm] == 1 && mx_are_same_shape(mul, norm) &&
+            !((norm->flags | mul->flags) & GGML_TENSOR_FLAG_OUTPUT)) {
+            act_cache_invalidate(c.s, mul);
+            if (mm_add_rms_norm(c, mm, res, add, norm, w, mul)) return 4;
+        }
+    }
+    return mmq_fused_add(c, mm, res, add) ? 2 : 0;
 }
 
 // MUL_MAT(gate) , MUL_MAT(up) , GLU(gate, up) with one activation column:
@@ -474,7 +488,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             }
             if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             if (n->op == GGML_OP_MUL_MAT && try_group_mm(c, g, i, done)) continue;
-            if (n->op == GGML_OP_MUL_MAT && try_fuse_mm_add(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; deferred_retire(s, g, i0, i); continue; }
+            if (n->op == GGML_OP_MUL_MAT) {
+                const int k = try_fuse_mm_add(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; deferred_retire(s, g, i0, i); continue; }
+            }
         }
         deferred_guard_node(c, n);
         act_cache_invalidate(s, n);

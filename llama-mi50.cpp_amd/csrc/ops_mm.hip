@@ -960,6 +960,110 @@ bool mmq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, g
 }
 
 
+// MUL_MAT -> ADD(residual) -> RMS_NORM -> MUL(w) of a prefill ubatch (round 3): the output
+// projection + ffn_norm and the FFN down projection + the next layer's attn_norm. After
+// the GEMM, ONE pass per token row sums its split-K partial planes (or reads the plain
+// product), adds the residual, stores the sum (the next residual) and writes the norm·w
+// rows with their f16 copy for the next GEMM — instead of k_mmq4_reduce (+ residual) and
+// k_rms_norm_v4, which re-read the sum. The arithmetic is the two kernels' own: planes in
+// order, then the residual; k_rms_norm_v4's per-thread float4 sums and block_sum.
+template <int VPT, bool SPLIT>
+__global__ __launch_bounds__(256) void k_add_rms_norm(const float * __restrict__ part, int part_ld, int ks, int N,
+                                                      const float * prod, size_t p_col,
+                                                      const float * res, size_t r_col, float * add, size_t a_col,
+                                                      const float * __restrict__ w, float * __restrict__ y, size_t y_col,
+                                                      float eps, int n, _Float16 * __restrict__ h) {
+    __shared__ float lds[16];
+    const int t = blockIdx.x, n4 = n / 4;
+    const float4 * pr = (const float4 *) (res + (size_t) t * r_col);
+    float4 * pa = (float4 *) (add + (size_t) t * a_col);
+    float4 v[VPT];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+        const int i = threadIdx.x + 256 * j, ii = min(i, n4 - 1);
+        float4 a;
+        if constexpr (SPLIT) {
+            const float4 * pp = (const float4 *) (part + (size_t) t * part_ld) + ii;
+            a = pp[0];
+            for (int z = 1; z < ks; ++z) {
+                const float4 b = pp[(size_t) z * N * part_ld / 4];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+        } else a = ((const float4 *) (prod + (size_t) t * p_col))[ii];
+        const float4 r = pr[ii];
+        a.x += r.x; a.y += r.y; a.z += r.z; a.w += r.w;
+        v[j] = a;
+        if (i < n4) s += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+    }
+    s = block_sum(s, lds);                  // (its barriers also order every read of res before the stores)
+    const float scale = 1.0f / sqrtf(s / (float) n + eps);
+    const float4 * pw = (const float4 *) w;
+    float4 * py = (float4 *) (y + (size_t) t * y_col);
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+        const int i = threadIdx.x + 256 * j;
+        if (i >= n4) break;
+        pa[i] = v[j];
+        float4 o = make_float4(v[j].x * scale, v[j].y * scale, v[j].z * scale, v[j].w * scale);
+        const float4 wv = pw[i];
+        o.x *= wv.x; o.y *= wv.y; o.z *= wv.z; o.w *= wv.w;
+        py[i] = o;
+        if (h) {
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            *(h4 *) (h + (size_t) t * n + 4 * i) = h4{(_Float16) o.x, (_Float16) o.y, (_Float16) o.z, (_Float16) o.w};
+        }
+    }
+}
+
+static const bool g_no_add_norm = getenv("GGML_MI355X_NO_ADD_NORM_FUSION") != nullptr;   // A/B
+bool mm_add_rms_norm(OpCtx & c, ggml_tensor * mm, const ggml_tensor * res, ggml_tensor * add, const ggml_tensor * norm,
+                     const ggml_tensor * w, ggml_tensor * mul) {
+    if (g_no_add_norm || (g_tune[27] & 512)) return false;
+    const ggml_tensor * wt = mm->src[0], * x = mm->src[1];
+    const bool kq = wt->type == GGML_TYPE_Q4_K || wt->type == GGML_TYPE_Q5_K || wt->type == GGML_TYPE_Q6_K;
+    if (!kq || g_mmq_v1 || g_mmq_glu_off || wt->ne[0] % 256 || x->ne[1] <= 8 || !mmq_ok(mm)) return false;
+    if (x->ne[2] != 1 || x->ne[3] != 1 || wt->ne[2] != 1 || wt->ne[3] != 1) return false;
+    const int64_t n = add->ne[0], N = add->ne[1];
+    auto rows16 = [&](const ggml_tensor * t) {
+        return t->type == GGML_TYPE_F32 && t->ne[0] == n && t->ne[1] == N && t->ne[2] == 1 && t->ne[3] == 1 && t->nb[0] == 4 &&
+               t->nb[1] % 16 == 0 && (uintptr_t) t->data % 16 == 0;
+    };
+    if (!rows16(add) || !rows16(res) || !rows16(mul) || !mx_are_same_shape(add, mm) || N > INT32_MAX) return false;
+    if (n % 4 || n < 128 || n > 4 * 256 * 8) return false;
+    if (w->type != GGML_TYPE_F32 || mx_nelements(w) != n || !mx_is_contiguous(w) || (uintptr_t) w->data % 16) return false;
+    // the norm rows are written while other rows' sums are still being read
+    if (t_overlaps_ext(mul, add) || t_overlaps_ext(mul, res) || t_overlaps_ext(mul, w) || t_overlaps_ext(mul, x)) return false;
+    if (add->data != res->data && t_overlaps_ext(add, res)) return false;
+    deferred_guard_read(c, x);
+    deferred_guard_read(c, res);
+    deferred_guard_write(c, add);
+    deferred_guard_write(c, mul);
+    // the product alone (the residual is added below), into add — or, when the ADD runs in
+    // place over the residual, into scratch (unless the GEMM splits: then only partials)
+    ggml_tensor prod = *add;
+    if (add->data == res->data) {
+        if (c.scratch->avail() < (size_t) n * N * 4 + 256) return false;
+        prod.data = c.scratch->take((size_t) n * N * 4);
+        prod.nb[1] = (size_t) n * 4; prod.nb[2] = prod.nb[3] = (size_t) n * N * 4;
+    }
+    M4Split sp{};
+    g_m4_split = &sp;
+    mmq_run_ex(c, mm, &prod, nullptr);
+    g_m4_split = nullptr;
+    const float eps = mx_op_param<float>(norm, 0);
+    _Float16 * h = mmq_act_claim(c, mul->data, n, N, mul->nb[1]);
+    const int vpt = (int) mx_ceil_div(n / 4, 256);
+    MX_KLOG("add_rms_norm n=%lld N=%lld ks=%d", (long long) n, (long long) N, sp.ks);
+#define AN(V, S) k_add_rms_norm<V, S><<<(unsigned) N, 256, 0, c.st>>>(sp.part, sp.part_ld, sp.ks, (int) N, (const float *) prod.data, \
+        prod.nb[1] / 4, (const float *) res->data, \
+        res->nb[1] / 4, (float *) add->data, add->nb[1] / 4, (const float *) w->data, (float *) mul->data, mul->nb[1] / 4, eps, (int) n, h)
+    if (sp.ks > 1) { if (vpt <= 2) AN(2, true); else if (vpt <= 4) AN(4, true); else AN(8, true); }
+    else { if (vpt <= 2) AN(2, false); else if (vpt <= 4) AN(4, false); else AN(8, false); }
+#undef AN
+    return true;
+}
+
 bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu) {
     const ggml_tensor * wg = gate->src[0], * wu = up->src[0];
     const ggml_tensor * x = gate->src[1];

@@ -35,17 +35,18 @@ def test_prefill_matches_incremental_decode(pkg, tiny):
 
 
 def test_prefill_qkv_epilogue_fusion(pkg, backend, tiny):
-    """prefill q/k/v: the grouped GEMM + ONE k_qkv_pp_epi launch for ROPE(q), ROPE(k) and
-    the two KV SET_ROWS (ops_qkv.hip qkv_prefill) against the node-by-node ROPE / SET_ROWS
-    kernels (g_tune[27] bit 128): the same GEMM and the same rope table arithmetic (the
-    rotation's multiply-adds may contract differently in the two kernels: last-bit
-    differences), so the logits and the cache contents written by the prompt agree
-    (checked through a decode step that reads the cache)"""
+    """prefill fusions against node-by-node execution: q/k/v = the grouped GEMM + ONE
+    k_qkv_pp_epi launch for ROPE(q), ROPE(k) and the two KV SET_ROWS (ops_qkv.hip
+    qkv_prefill; off: g_tune[27] bit 128), and MUL_MAT -> ADD -> RMS_NORM -> MUL = the GEMM +
+    ONE k_add_rms_norm pass (ops_mm.hip mm_add_rms_norm; off: bit 512). Same GEMMs, the
+    same rope table and norm arithmetic (multiply-adds may contract differently in
+    different kernels: last-bit differences), so the logits and the cache contents written
+    by the prompt agree (checked through a decode step that reads the cache)"""
     rng = np.random.default_rng(7)
     toks = rng.integers(0, TINY["n_vocab"], 40).astype(np.int32)
     lib = pkg._lib.load()
     out = []
-    for tune in (0, 128):
+    for tune in (0, 128 | 512):
         lib.ggml_backend_mi355x_set_tune(27, tune)
         try:
             backend.klog(True)
@@ -58,6 +59,7 @@ def test_prefill_qkv_epilogue_fusion(pkg, backend, tiny):
         finally:
             lib.ggml_backend_mi355x_set_tune(27, 0)
         assert any(l.startswith("qkv_pp ") for l in log) == (tune == 0), [l for l in log if "qkv" in l][:4]
+        assert any(l.startswith("add_rms_norm ") for l in log) == (tune == 0), log[:8]
         out.append((a, b))
     assert np.all(np.isfinite(out[0][0]))
     assert nmse(out[0][0], out[1][0]) < 1e-9
