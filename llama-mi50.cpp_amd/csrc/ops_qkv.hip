@@ -180,47 +180,74 @@ struct QkvPpArgs {
     char * vc; size_t vc_nb1; const int64_t * vidx;
     int Mq, Mk, Mv;
 };
-// SPLIT: the q/k/v GEMM ran split-K and left its partial planes; the sum over planes (in
-// plane order, as k_mmq4_reduce adds them) replaces the reduce pass and its round trip
-template <bool SPLIT>
-__device__ __forceinline__ float2 qkv_pp_ld(const QkvPpArgs & e, const float * x, int seg, int t, int j) {
-    if constexpr (!SPLIT) return ((const float2 *) x)[j];
-    const float * b = e.part + (size_t) t * e.part_ld + e.row0[seg] + 2 * j;
-    float2 v = *(const float2 *) b;
-    for (int z = 1; z < e.ks; ++z) {
-        const float2 w = *(const float2 *) (b + (size_t) z * e.N * e.part_ld);
-        v.x += w.x; v.y += w.y;
+// KS: 0 = the plain projections; > 0 = the q/k/v GEMM ran split-K (KS planes; -1: any
+// count) and left its partial planes, summed here in plane order as k_mmq4_reduce adds
+// them — the reduce pass and its round trip are gone. Pairs are processed CH at a time
+// with every load of a chunk issued before any store (a loop that consumed each load
+// before the next was one memory round trip per pair: 11.7 us per pp512 layer).
+template <int KS>
+__device__ __forceinline__ float2 qkv_pp_ld(const QkvPpArgs & e, int seg, int t, int j) {
+    if constexpr (KS == 0) {
+        const float * x = seg == 0 ? e.q + (size_t) t * e.Mq : seg == 1 ? e.k + (size_t) t * e.Mk : e.v + (size_t) t * e.Mv;
+        return ((const float2 *) x)[j];
+    } else {
+        const float * b = e.part + (size_t) t * e.part_ld + e.row0[seg] + 2 * j;
+        const size_t pl = (size_t) e.N * e.part_ld;
+        float2 v = *(const float2 *) b;
+        if constexpr (KS > 0) {
+#pragma unroll
+            for (int z = 1; z < KS; ++z) { const float2 w = *(const float2 *) (b + z * pl); v.x += w.x; v.y += w.y; }
+        } else {
+            for (int z = 1; z < e.ks; ++z) { const float2 w = *(const float2 *) (b + z * pl); v.x += w.x; v.y += w.y; }
+        }
+        return v;
     }
-    return v;
 }
-template <bool SPLIT>
+template <int KS>
 __global__ __launch_bounds__(256) void k_qkv_pp_epi(QkvArgs p, QkvPpArgs e) {
     __shared__ float2 tab[MX_ROPE_TAB];
     const int t = blockIdx.x;
     const int np = p.n_dims / 2;
     const float pf = (float) p.pos[t];
     for (int i = threadIdx.x; i < np; i += blockDim.x) tab[i] = qkv_rope_cs(p, pf, i);
-    __syncthreads();
-    const int pq = e.Mq / 2, pk = e.Mk / 2, pv = e.Mv / 2;
-    const float2 * q = (const float2 *) (e.q + (size_t) t * e.Mq);
-    const float2 * k = (const float2 *) (e.k + (size_t) t * e.Mk);
-    const float2 * v = (const float2 *) (e.v + (size_t) t * e.Mv);
+    const int pq = e.Mq / 2, pk = e.Mk / 2, pv = e.Mv / 2, total = pq + pk + pv;
     float2 * rq = (float2 *) (e.rq + (size_t) t * e.Mq);
     uint32_t * kr = (uint32_t *) (e.kc + (size_t) e.kidx[t] * e.kc_nb1);
     uint32_t * vr = (uint32_t *) (e.vc + (size_t) e.vidx[t] * e.vc_nb1);
-    for (int j = threadIdx.x; j < pq + pk + pv; j += blockDim.x) {
-        if (j < pq) {
-            const float2 x = qkv_pp_ld<SPLIT>(e, (const float *) q, 0, t, j), cs = tab[j % np];
-            rq[j] = make_float2(x.x * cs.x - x.y * cs.y, x.x * cs.y + x.y * cs.x);
-        } else if (j < pq + pk) {
-            const int jj = j - pq;
-            const float2 x = qkv_pp_ld<SPLIT>(e, (const float *) k, 1, t, jj), cs = tab[jj % np];
-            kr[jj] = (uint32_t) f2h(x.x * cs.x - x.y * cs.y) | ((uint32_t) f2h(x.x * cs.y + x.y * cs.x) << 16);
-        } else {
-            const int jj = j - pq - pk;
-            const float2 x = qkv_pp_ld<SPLIT>(e, (const float *) v, 2, t, jj);
-            vr[jj] = (uint32_t) f2h(x.x) | ((uint32_t) f2h(x.y) << 16);
+    constexpr int CH = 6;
+    auto load_chunk = [&](int j0, float2 (&x)[CH]) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int j = min(j0 + 256 * c, total - 1);           // clamped: loads, not branches
+            const int seg = j < pq ? 0 : j < pq + pk ? 1 : 2;
+            x[c] = qkv_pp_ld<KS>(e, seg, t, seg == 0 ? j : seg == 1 ? j - pq : j - pq - pk);
         }
+    };
+    auto store_chunk = [&](int j0, const float2 (&x)[CH]) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int j = j0 + 256 * c;
+            if (j >= total) break;
+            if (j < pq) {
+                const float2 cs = tab[j % np];
+                rq[j] = make_float2(x[c].x * cs.x - x[c].y * cs.y, x[c].x * cs.y + x[c].y * cs.x);
+            } else if (j < pq + pk) {
+                const int jj = j - pq;
+                const float2 cs = tab[jj % np];
+                kr[jj] = (uint32_t) f2h(x[c].x * cs.x - x[c].y * cs.y) | ((uint32_t) f2h(x[c].x * cs.y + x[c].y * cs.x) << 16);
+            } else {
+                const int jj = j - pq - pk;
+                vr[jj] = (uint32_t) f2h(x[c].x) | ((uint32_t) f2h(x[c].y) << 16);
+            }
+        }
+    };
+    float2 x[CH];
+    load_chunk(threadIdx.x, x);                  // the first chunk's loads fly while the table is built
+    __syncthreads();
+    store_chunk(threadIdx.x, x);
+    for (int j0 = threadIdx.x + CH * 256; j0 < total; j0 += CH * 256) {
+        load_chunk(j0, x);
+        store_chunk(j0, x);
     }
 }
 
@@ -317,8 +344,9 @@ static int qkv_prefill(OpCtx & c, ggml_cgraph * g, int i, int last, const ggml_t
     if (sp.ks > 1) {
         e.part = sp.part; e.part_ld = sp.part_ld; e.ks = sp.ks; e.N = (int) N;
         for (int k = 0; k < 3; ++k) e.row0[k] = sp.row0[k];
-        k_qkv_pp_epi<true><<<(unsigned) N, 256, 0, c.st>>>(p, e);
-    } else k_qkv_pp_epi<false><<<(unsigned) N, 256, 0, c.st>>>(p, e);
+        if (sp.ks == 2) k_qkv_pp_epi<2><<<(unsigned) N, 256, 0, c.st>>>(p, e);
+        else k_qkv_pp_epi<-1><<<(unsigned) N, 256, 0, c.st>>>(p, e);
+    } else k_qkv_pp_epi<0><<<(unsigned) N, 256, 0, c.st>>>(p, e);
     return last - i + 1;
 }
 
