@@ -148,7 +148,12 @@ struct mxr_context {
     std::vector<ggml_tensor *> kc, vc;
     std::vector<std::unique_ptr<GraphInst>> graphs;
     uint64_t tick = 0;
-    char * h_in = nullptr; size_t h_in_cap = 0;
+    // input staging: two pinned buffers in turn, each guarded by the event recorded after
+    // its upload, so the host fills ubatch i+1's inputs while the GPU runs ubatch i (a
+    // prompt's ubatches without logits are not synchronised one by one)
+    char * h_in_buf[2] = {nullptr, nullptr}; size_t h_in_cap[2] = {0, 0};
+    hipEvent_t h_in_ev[2] = {nullptr, nullptr};
+    int h_in_k = 0;
     float * h_logits = nullptr; size_t h_logits_cap = 0;
 };
 
@@ -418,7 +423,11 @@ void mxr_context_free(mxr_context * c) {
     if (!c) return;
     for (auto & g : c->graphs) { mxg_free(g->ctx); mxg_free(g->ictx); }
     mxg_free(c->kvctx);
-    if (c->h_in) hipHostFree(c->h_in);
+    for (int k = 0; k < 2; ++k) {
+        if (c->h_in_ev[k]) (void) hipEventSynchronize(c->h_in_ev[k]);
+        if (c->h_in_buf[k]) hipHostFree(c->h_in_buf[k]);
+        if (c->h_in_ev[k]) hipEventDestroy(c->h_in_ev[k]);
+    }
     if (c->h_logits) hipHostFree(c->h_logits);
     delete c;
 }
@@ -596,7 +605,7 @@ static GraphInst * build_graph(mxr_context * c, int n_tokens, int n_kv, int n_ou
 static GraphInst * get_graph(mxr_context * c, int n_tokens, int n_kv, int n_out) {
     for (auto & g : c->graphs)
         if (g->n_tokens == n_tokens && g->n_kv == n_kv && g->n_out == n_out) { g->last_use = ++c->tick; return g.get(); }
-    if (c->graphs.size() >= 3) {  // evict least recently used
+    if (c->graphs.size() >= 6) {  // evict least recently used (a pp2048 prompt alone has 4 shapes: n_kv 512 .. 2048)
         size_t victim = 0;
         for (size_t i = 1; i < c->graphs.size(); ++i) if (c->graphs[i]->last_use < c->graphs[victim]->last_use) victim = i;
         mxg_synchronize(c->m->be);
@@ -618,15 +627,19 @@ static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_toke
     const int n_out = all_logits ? n_tokens : 1;
     GraphInst * g = get_graph(c, n_tokens, n_kv, n_out);
     if (!g) return -2;
-    // host staging (pinned) laid out exactly like the device input buffer
-    if (c->h_in_cap < g->in_bytes) {
-        if (c->h_in) HIP_CHECK(hipHostFree(c->h_in));
-        HIP_CHECK(hipHostMalloc((void **) &c->h_in, g->in_bytes, hipHostMallocDefault));
-        c->h_in_cap = g->in_bytes;
+    // host staging (pinned) laid out exactly like the device input buffer; this buffer's
+    // previous upload (two ubatches ago) must have completed before it is rewritten
+    const int hk = c->h_in_k;
+    c->h_in_k ^= 1;
+    if (c->h_in_ev[hk]) HIP_CHECK(hipEventSynchronize(c->h_in_ev[hk]));
+    else HIP_CHECK(hipEventCreateWithFlags(&c->h_in_ev[hk], hipEventDisableTiming));
+    if (c->h_in_cap[hk] < g->in_bytes) {
+        if (c->h_in_buf[hk]) HIP_CHECK(hipHostFree(c->h_in_buf[hk]));
+        HIP_CHECK(hipHostMalloc((void **) &c->h_in_buf[hk], g->in_bytes, hipHostMallocDefault));
+        c->h_in_cap[hk] = g->in_bytes;
     }
-    // the previous upload may still be in flight on the stream
-    mxg_synchronize(c->m->be);
-    auto at = [&](ggml_tensor * t) { return c->h_in + ((char *) t->data - g->in_base); };
+    char * h_stage = c->h_in_buf[hk];
+    auto at = [&](ggml_tensor * t) { return h_stage + ((char *) t->data - g->in_base); };
     if (tokens) memcpy(at(g->tokens), tokens, n_tokens * sizeof(int32_t));
     else memset(at(g->tokens), 0, n_tokens * sizeof(int32_t));   // later pipeline stages: unused
     int32_t * pos = (int32_t *) at(g->pos);
@@ -646,8 +659,9 @@ static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_toke
         for (int j = 0; j < n_kv; ++j) mask[(int64_t) i * n_kv + j] = (j <= c->pos + i) ? 0.0f : -INFINITY;
     if (g->out_ids) ((int32_t *) at(g->out_ids))[0] = n_tokens - 1;
     ggml_backend_t be = c->m->be;
-    be->iface.set_tensor_async(be, g->tokens, c->h_in, 0, g->in_bytes);
+    be->iface.set_tensor_async(be, g->tokens, h_stage, 0, g->in_bytes);
     hipStream_t st_be = stream_of_backend(be);
+    HIP_CHECK(hipEventRecord(c->h_in_ev[hk], st_be));
     if (g->hin) {   // previous stage's hidden state (device or host pointer)
         if (!h_in) return -4;
         HIP_CHECK(hipMemcpyAsync(g->hin->data, h_in, mx_nbytes(g->hin), hipMemcpyDefault, st_be));
@@ -664,7 +678,9 @@ static int32_t decode_ubatch(mxr_context * c, const int32_t * tokens, int n_toke
         }
         be->iface.get_tensor_async(be, g->logits, c->h_logits, 0, lbytes);
     }
-    mxg_synchronize(be);
+    // results the caller reads (logits, the hand-off hidden state) need the stream done;
+    // a prompt ubatch without outputs returns at once
+    if ((out && g->logits) || (g->hout && h_out)) mxg_synchronize(be);
     if (out && g->logits) memcpy(out, c->h_logits, lbytes);
     c->pos += n_tokens;
     return 0;
