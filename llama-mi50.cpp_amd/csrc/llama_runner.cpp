@@ -421,6 +421,7 @@ mxr_context * mxr_context_new(mxr_model * m, int32_t n_ctx, int32_t n_ubatch, in
 
 void mxr_context_free(mxr_context * c) {
     if (!c) return;
+    mxg_synchronize(c->m->be);   // a prompt's last ubatches may still run (decode_ubatch syncs only for outputs)
     for (auto & g : c->graphs) { mxg_free(g->ctx); mxg_free(g->ictx); }
     mxg_free(c->kvctx);
     for (int k = 0; k < 2; ++k) {
