@@ -1035,6 +1035,9 @@ bool mm_add_rms_norm(OpCtx & c, ggml_tensor * mm, const ggml_tensor * res, ggml_
     // the norm rows are written while other rows' sums are still being read
     if (t_overlaps_ext(mul, add) || t_overlaps_ext(mul, res) || t_overlaps_ext(mul, w) || t_overlaps_ext(mul, x)) return false;
     if (add->data != res->data && t_overlaps_ext(add, res)) return false;
+    // every refusal comes before the deferred-norm guards act (mmq4_scratch sizes the arena
+    // for this product and the split-K planes together)
+    if (add->data == res->data && c.scratch->avail() < (size_t) n * N * 4 + 256) return false;
     deferred_guard_read(c, x);
     deferred_guard_read(c, res);
     deferred_guard_write(c, add);
@@ -1043,7 +1046,6 @@ bool mm_add_rms_norm(OpCtx & c, ggml_tensor * mm, const ggml_tensor * res, ggml_
     // place over the residual, into scratch (unless the GEMM splits: then only partials)
     ggml_tensor prod = *add;
     if (add->data == res->data) {
-        if (c.scratch->avail() < (size_t) n * N * 4 + 256) return false;
         prod.data = c.scratch->take((size_t) n * N * 4);
         prod.nb[1] = (size_t) n * 4; prod.nb[2] = prod.nb[3] = (size_t) n * N * 4;
     }

@@ -20,7 +20,11 @@
 //     is the f16 1024 + q (low nibbles), the high nibble in place OR 0x5400 is 64 + q;
 //     one v_pk_add removes the bias exactly, one v_pk_fma applies d*sc and -dmin*m —
 //     ~1.75 VALU per weight, hidden behind the MFMAs of the partner wave on the SIMD.
-//     Weights are scaled by 2^10 so d*sc stays a normal f16; the epilogue undoes it;
+//     Weights are scaled by ws = 2^10 so d*sc stays a normal f16; the epilogue undoes it.
+//     A row whose super-block scales would push a scaled weight past 2^15 (|w| > 32 at
+//     2^10: outlier rows of real checkpoints) lowers its lane's ws to a smaller power of two
+//     and rescales its accumulators once (m4_range, wave-uniform branch, never taken for
+//     ordinary weights);
 //   * epilogues: store (+ residual), SwiGLU of a gate/up pair (waves 0-1 gate rows,
 //     2-3 up rows of the same 64; combined through LDS), the f16 copy of the output for
 //     the next GEMM (act cache), and the MoE gather/scatter of grouped expert tiles.
@@ -152,12 +156,12 @@ __device__ __forceinline__ uint32_t m4_and_or(uint32_t x, uint32_t m, uint32_t b
 #endif
 }
 
-// dequantised scales of one lane's unit: lo / hi sub-block (d*sc, -dmin*m) x 2^10, f16;
+// dequantised scales of one lane's unit: lo / hi sub-block (d*sc, -dmin*m) x ws, f16;
 // Q5_K also the qh bit index of the two sub-blocks
 struct M4Scale { h2 slo, mlo, shi, mhi; int gb; };
 
 template <int QT>
-__device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, int j) {
+__device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, int j, float ws) {
     M4Scale s;
     const int hf = kc & 1, U = 2 * h + j;
     if constexpr (QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q5_K) {
@@ -170,8 +174,8 @@ __device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, i
         const uint32_t scw = hf == 0 ? (s0 & 0x3F3F3F3Fu) : ((s2 & 0x0F0F0F0Fu) | ((s0 >> 2) & 0x30303030u));
         const uint32_t mnw = hf == 0 ? (s1 & 0x3F3F3F3Fu) : (((s2 >> 4) & 0x0F0F0F0Fu) | ((s1 >> 2) & 0x30303030u));
         const uint32_t scp = scw >> (16 * (g & 1)), mnp = mnw >> (16 * (g & 1));
-        const float d = h2f((uint16_t) (dw(r.hd, 0) & 0xFFFF)) * M4_WSCALE;
-        const float dm = h2f((uint16_t) (dw(r.hd, 0) >> 16)) * M4_WSCALE;
+        const float d = h2f((uint16_t) (dw(r.hd, 0) & 0xFFFF)) * ws;
+        const float dm = h2f((uint16_t) (dw(r.hd, 0) >> 16)) * ws;
         const _Float16 a = (_Float16) (d * (float) (scp & 0xFF)), b = (_Float16) (d * (float) ((scp >> 8) & 0xFF));
         const _Float16 c = (_Float16) (-dm * (float) (mnp & 0xFF)), e = (_Float16) (-dm * (float) ((mnp >> 8) & 0xFF));
         s.slo = h2{a, a}; s.shi = h2{b, b}; s.mlo = h2{c, c}; s.mhi = h2{e, e};
@@ -179,7 +183,7 @@ __device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, i
     } else {
         // 16-wide groups: lo k = 128hf + 16U + i -> scale 8hf + U, hi (+64) -> 8hf + 4 + U
         const int slo = 8 * hf + U, shi = slo + 4;
-        const float d = h2f((uint16_t) r.d) * M4_WSCALE;
+        const float d = h2f((uint16_t) r.d) * ws;
         const int8_t vlo = (int8_t) (dw(r.sc, slo >> 2) >> (8 * (slo & 3)));
         const int8_t vhi = (int8_t) (dw(r.sc, shi >> 2) >> (8 * (shi & 3)));
         const _Float16 a = (_Float16) (d * (float) vlo), b = (_Float16) (d * (float) vhi);
@@ -188,6 +192,36 @@ __device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, i
         s.gb = 0;
     }
     return s;
+}
+
+// Range guard of one chunk: the largest scaled weight magnitude the chunk can produce is
+// ws x (Q4_K 15*63 d | 63 dmin, Q5_K 31*63 d | 63 dmin, Q6_K 32*128 d); it must stay below
+// 2^15 (f16 max 65504). A lane whose chunk exceeds it takes the largest power of two that
+// fits and rescales its accumulators by the ratio (its accumulators are all of its own
+// row, and the row's other lane (r + 32) reads the same super-block header, so both pick
+// the same ws). Scales only ever shrink, so a row rescales at most a few times.
+template <int QT, int TT>
+__device__ __forceinline__ void m4_range(const M4W<QT> & r, float & ws, f16v (&acc)[TT]) {
+    float need;
+    if constexpr (QT == GGML_TYPE_Q6_K) {
+        need = __builtin_fabsf(h2f((uint16_t) r.d)) * 4096.0f;
+    } else {
+        const float d = __builtin_fabsf(h2f((uint16_t) (dw(r.hd, 0) & 0xFFFF)));
+        const float dm = __builtin_fabsf(h2f((uint16_t) (dw(r.hd, 0) >> 16)));
+        need = __builtin_fmaxf(d * (QT == GGML_TYPE_Q4_K ? 945.0f : 1953.0f), dm * 63.0f);
+    }
+    const bool over = need * ws >= 32768.0f;
+    if (__builtin_amdgcn_ballot_w64(over)) {          // wave-uniform; ordinary weights never enter
+        int e;
+        (void) __builtin_frexpf(32768.0f / need, &e);
+        const float wn = over ? __builtin_ldexpf(1.0f, e - 1) : ws;
+        const float f = wn / ws;
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc[t][k] *= f;
+        ws = wn;
+    }
 }
 
 // B operand of MFMA step q of unit j (q 0,1: the low sub-block's positions 8q..8q+7 of
@@ -287,7 +321,8 @@ constexpr int M4_S = 4;            // activation ring stages (prefetch distance 
 // (it also retires the stage the previous chunk read, which the DMA then refills).
 template <int QT, int TT, int X>
 __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, const int (&cols)[TT],
-                                         uint4 * lds, int c0, int nc, f16v (&acc)[TT], unsigned long long * tr) {
+                                         uint4 * lds, int c0, int nc, f16v (&acc)[TT], float & ws,
+                                         unsigned long long * tr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     constexpr int NDMA = TT;                     // 1-KB LDS-DMA pieces per wave per chunk (32 TT rows / 8 waves / 4 rows)
     constexpr int TILE = 32 * TT * 16;           // uint4 per stage
@@ -327,8 +362,9 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
         h8 af[D + 1][TT];
 #pragma unroll
         for (int st = 0; st < D; ++st) lda(L, st >> 2, st & 3, af[st]);
+        if constexpr (!(X & 2)) m4_range<QT, TT>(rw, ws, acc);
         // the two units' scales once per chunk (they depend on j only, not on the step)
-        const M4Scale sj[2] = {m4_scales<QT>(rw, kc, h, 0), m4_scales<QT>(rw, kc, h, 1)};
+        const M4Scale sj[2] = {m4_scales<QT>(rw, kc, h, 0, ws), m4_scales<QT>(rw, kc, h, 1, ws)};
         if constexpr (X & 16) {
             // software-pipelined: step st+1's B operand is dequantised while step st's MFMAs
             // run, the schedule interleaving one MFMA, one LDS read and NV VALU instructions
@@ -463,13 +499,14 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
         cols[i] = EPI == 2 ? p.gather[slot0 + t] : t;
     }
     f16v acc[TT];
+    float ws = M4_WSCALE;                             // this lane's weight scale (m4_range)
     unsigned long long * tr = (blockIdx.x | blockIdx.y | blockIdx.z) == 0 ? p.trace : nullptr;
     MX_TRACE(tr, 0);
-    if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT, X>(p, wrow, cols, lds, c0, nc, acc, tr);
-    else m4_kloop<QTB, TT, X>(p, wrow, cols, lds, c0, nc, acc, tr);
+    if (!sg.isb || QTA == QTB) m4_kloop<QTA, TT, X>(p, wrow, cols, lds, c0, nc, acc, ws, tr);
+    else m4_kloop<QTB, TT, X>(p, wrow, cols, lds, c0, nc, acc, ws, tr);
 
     if (p.trace_blk && tid == 0 && bid < 65536) p.trace_blk[2 * bid + 1] = __builtin_amdgcn_s_memrealtime();
-    constexpr float inv = 1.0f / M4_WSCALE;
+    const float inv = 1.0f / ws;
     if constexpr (EPI == 1) {
         float * red = (float *) lds;                  // 4 waves x TT x 16 x 64 floats (<= the ring)
         m4_barrier();                                 // every wave is done with the ring
@@ -477,7 +514,7 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
 #pragma unroll
             for (int t = 0; t < TT; ++t)
 #pragma unroll
-                for (int e = 0; e < 16; ++e) red[(((wave - M4_WAVES / 2) * TT + t) * 16 + e) * 64 + lane] = acc[t][e];
+                for (int e = 0; e < 16; ++e) red[(((wave - M4_WAVES / 2) * TT + t) * 16 + e) * 64 + lane] = acc[t][e] * inv;
         }
         m4_barrier();
         if (wave >= M4_WAVES / 2) return;
@@ -486,7 +523,7 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int tok = tok0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
-                const float g = acc[t][e] * inv, u = red[((wave * TT + t) * 16 + e) * 64 + lane] * inv;
+                const float g = acc[t][e] * inv, u = red[((wave * TT + t) * 16 + e) * 64 + lane];
                 const float v = g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-g * 1.4426950408889634f)) * u;
                 if (tok < ntok && row < sg.M) {
                     sg.dst[(size_t) tok * sg.d_col + row] = v;
@@ -619,7 +656,9 @@ size_t mmq4_scratch(const ggml_tensor * dst) {
     if (!m4_kq(w->type) || x->ne[1] <= 8) return 0;
     const int64_t rows = mx_ceil_div(w->ne[1] + w->ne[1] / 2, 256) * 256;   // room for a q/k/v group
     const int ks = m4_ksplit(mx_ceil_div(x->ne[1], 128) * mx_ceil_div(rows, 256), (int) (w->ne[0] / M4_KC), x->ne[1], rows);
-    return ks > 1 ? (size_t) ks * x->ne[1] * rows * 4 + 256 : 0;
+    // + the product itself: mm_add_rms_norm keeps an unsplit product in scratch when the ADD
+    // runs in place over its residual, and must not squeeze the split-K planes out
+    return (ks > 1 ? (size_t) ks * x->ne[1] * rows * 4 + 256 : 0) + (size_t) w->ne[1] * x->ne[1] * 4 + 256;
 }
 
 template <int EPI>
@@ -655,6 +694,7 @@ static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int 
         const dim3 gr((unsigned) mx_ceil_div(a.part_ld, 256), (unsigned) a.N);
         k_mmq4_reduce<<<gr, 256, 0, c.st>>>(a);
     }
+    MX_KLOG("mmq4 launch epi=%d ks=%d planes=%d tiles=%d gx=%lld", EPI, a.ksplit, (int) taken, tiles_y, (long long) gx);
     return ok;
 }
 

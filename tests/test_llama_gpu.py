@@ -34,20 +34,26 @@ def test_prefill_matches_incremental_decode(pkg, tiny):
     s1.free(); s2.free()
 
 
-def test_prefill_qkv_epilogue_fusion(pkg, backend, tiny):
+@pytest.mark.parametrize("ks", [0, 2])
+def test_prefill_qkv_epilogue_fusion(pkg, backend, tiny, ks):
     """prefill fusions against node-by-node execution: q/k/v = the grouped GEMM + ONE
     k_qkv_pp_epi launch for ROPE(q), ROPE(k) and the two KV SET_ROWS (ops_qkv.hip
     qkv_prefill; off: g_tune[27] bit 128), and MUL_MAT -> ADD -> RMS_NORM -> MUL = the GEMM +
     ONE k_add_rms_norm pass (ops_mm.hip mm_add_rms_norm; off: bit 512). Same GEMMs, the
     same rope table and norm arithmetic (multiply-adds may contract differently in
     different kernels: last-bit differences), so the logits and the cache contents written
-    by the prompt agree (checked through a decode step that reads the cache)"""
+    by the prompt agree (checked through a decode step that reads the cache).
+    ks = 2 (g_tune[20]) forces the k_mmq4 split-K at these small widths (the cost model
+    alone never splits K <= 512), so the fused epilogues read the M4Split partial planes
+    (k_qkv_pp_epi's and k_add_rms_norm's SPLIT forms, the default at 8B widths) and are
+    compared with k_mmq4_reduce + the node-by-node kernels at the same 1e-9 bound"""
     rng = np.random.default_rng(7)
     toks = rng.integers(0, TINY["n_vocab"], 40).astype(np.int32)
     lib = pkg._lib.load()
     out = []
     for tune in (0, 128 | 512):
         lib.ggml_backend_mi355x_set_tune(27, tune)
+        lib.ggml_backend_mi355x_set_tune(20, ks)
         try:
             backend.klog(True)
             s = pkg.Session(tiny, n_ctx=256, flash_attn=True)
@@ -58,8 +64,14 @@ def test_prefill_qkv_epilogue_fusion(pkg, backend, tiny):
             s.free()
         finally:
             lib.ggml_backend_mi355x_set_tune(27, 0)
+            lib.ggml_backend_mi355x_set_tune(20, 0)
         assert any(l.startswith("qkv_pp ") for l in log) == (tune == 0), [l for l in log if "qkv" in l][:4]
         assert any(l.startswith("add_rms_norm ") for l in log) == (tune == 0), log[:8]
+        if ks and tune == 0:
+            assert all("ks=2" in l for l in log if l.startswith(("qkv_pp ", "add_rms_norm "))), \
+                [l for l in log if l.startswith(("qkv_pp ", "add_rms_norm "))][:4]
+        if ks:
+            assert any(l.startswith("mmq4 launch epi=0 ks=2") for l in log), [l for l in log if "mmq4" in l][:6]
         out.append((a, b))
     assert np.all(np.isfinite(out[0][0]))
     assert nmse(out[0][0], out[1][0]) < 1e-9

@@ -28,6 +28,13 @@ UNARY_OPS = ("ABS,SGN,NEG,STEP,TANH,ELU,RELU,SIGMOID,GELU,GELU_QUICK,SILU,HARDSW
 CHUNKS = [(op, None) for op in ["ADD", "MUL", "SCALE", "RMS_NORM", "ROPE", "SOFT_MAX", "SET_ROWS", "GET_ROWS", "CPY",
                                  "CONT", GLU_OPS, UNARY_OPS, "MUL_MAT_ID", "ARGSORT", "SUM_ROWS", "CLAMP", "DIV"]]
 CHUNKS += [("MUL_MAT", "type_a=(f32|f16|bf16),"), ("MUL_MAT", "type_a=(q|i|m|t)")]
+# the harness's fusion cases (run_whole_graph: the whole graph on the backend, so the
+# executor's fusions see these node chains): ROPE -> VIEW -> SET_ROWS (:2377, cases :7082),
+# RMS_NORM -> MUL -> ADD and ADD -> RMS_NORM (:3404, :3468, cases :7560-7586), MUL_MAT_ID
+# chains (:3920, cases :7790-7831), gate/up GLU GEMVs (:5420, cases :8282-8284) and the
+# top-k MoE router (:5322, cases :8297-8304)
+CHUNKS += [(op, None) for op in ["ROPE_SET_ROWS", "RMS_NORM_MUL_ADD", "ADD_RMS_NORM", "MUL_MAT_ID_FUSION",
+                                 "MUL_MAT_VEC_FUSION", "TOPK_MOE"]]
 CHUNKS += [("FLASH_ATTN_EXT", r"hsk=64,"), ("FLASH_ATTN_EXT", r"hsk=128,"), ("FLASH_ATTN_EXT", r"hsk=(40|72|80|96),"),
            ("FLASH_ATTN_EXT", r"hsk=(192|256|576),")]
 
