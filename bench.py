@@ -3,24 +3,30 @@
 
 Workload (BASELINE.json configs[1]): Llama-3-8B shapes (n_embd 4096, 32 layers, 32/8
 heads, n_ff 14336, vocab 128256) with Q4_K_M weights (Q4_K + Q6_K attn_v/ffn_down on
-the 16 use_more_bits layers + Q6_K output), synthetic random weights generated on the
-device (no checkpoints offline). A *step* is one tg128 run exactly as llama-bench's
-test_gen does it (tools/llama-bench/llama-bench.cpp:1991): reset the KV cache, then 128
-single-token decodes of random tokens, each followed by a device synchronise and the
-logits copy-back. value = generated tokens / wall time. pp512 (one 512-token prefill,
-test_prompt :1962) is reported beside it.
+the 16 use_more_bits layers + Q6_K output), synthetic random weights (no checkpoints
+offline).
 
-Multi-GPU (torchrun, one process per GPU, --mode pipeline, the default for N > 1): the
-layer split of SURVEY §8e, as llama-bench -sm layer measures it. Rank r owns layers
-[r*L/N, (r+1)*L/N) of ONE model; the hidden state of each token goes to rank r+1 by RCCL
-point-to-point send/recv over xGMI. The headline value is ONE sequence (llama-bench tg128:
-every token passes all N stages in turn), so the total work is fixed as N grows
-("strong") and the curve is expected flat to declining: layer split buys capacity, not
-decode speed. `pipelined_tok_s` reports N sequences in flight (one per
-pipeline slot, every GPU busy) beside it. --mode replicas runs a whole model per GPU.
---model picks the BASELINE.json config (llama3_8b, llama3_70b, mixtral_8x7b, tinyllama).
-Single GPU: `dropin` runs the reference's own libllama on this backend
-(GGML_BACKEND_PATH, -ngl 99) on the same GGUF shape — the drop-in throughput.
+Headline (`value`, round 4): the drop-in path the north star names — the reference's own
+libllama (oracle/_ref/ref-llama-bench: llama-bench's test_gen loop, tools/llama-bench/
+llama-bench.cpp:1991-2010) loading libggml-mi355x.so through GGML_BACKEND_PATH, -ngl 99,
+-fa 1, on a synthetic GGUF of that shape (tools/gguf_synth.py). A *step* is one tg128
+repetition (llama-bench -r K after its own untimed warmup run: W - 1 further untimed
+repetitions run first); value = K * 128 tokens / the sum of the K repetitions' times as
+llama-bench measures them (llama_decode + synchronize per token). This package's own
+runner (the same backend driven by mx_llama, device-side random weights) is reported
+beside it under `runner` (tg128, pp512, pp2048), as are the drop-in's -fa 0 / q8_0-KV /
+pp2048 / depth legs.
+
+Multi-GPU (torchrun, one process per GPU): libllama's own layer split, as llama-bench
+-sm layer -ts 1,..,1 measures it — rank 0 drives GPUs 0..N-1 through this backend
+(contiguous layer ranges, boundary activations by cpy_tensor_async peer copies over xGMI,
+pipeline parallelism on: src/llama-context.cpp:307-334); the other ranks only wait in a
+gloo barrier (no RCCL kernel resident on their GPUs during the measurement). ONE sequence
+passes all N devices in turn, so the total work is fixed ("strong") and the curve is
+expected flat to declining. --mode pipeline runs this package's own RCCL
+send/recv pipeline instead (reported as before), --mode replicas a whole model per GPU.
+--model picks the BASELINE.json config (llama3_8b, llama3_70b, mixtral_8x7b, tinyllama)
+for the runner modes.
 """
 import argparse
 import ctypes
@@ -43,7 +49,9 @@ MFMA_F16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no spars
 PP_FLOPS_PER_TOKEN = {"llama3_8b": 2 * 218103808 * 32}
 
 
-def dist_setup(n_gpus):
+def dist_setup(n_gpus, backend=None):
+    """backend: None = nccl (RCCL) when a GPU is visible, else gloo; "gloo" for the drop-in
+    layer-split headline (only rank 0's child process touches the GPUs)"""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -52,7 +60,7 @@ def dist_setup(n_gpus):
         import torch
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("MX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        backend = os.environ.get("MX_DIST_BACKEND") or backend or ("nccl" if torch.cuda.device_count() > 0 else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         tdist.init_process_group(backend=backend)
@@ -122,14 +130,17 @@ def roofline_glu(pkg, be, model, iters=256):
     ctx.free()
     achieved = bytes_per_launch / (us * 1e-6) / 1e9
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r02", "pmc_glu.json")   # scripts/pmc_roofline.sh
-    if not os.path.exists(pmc):
-        pmc = os.path.join(ROOT, "profiles", "r01", "pmc_glu.json")
-    if os.path.exists(pmc):
+    # scripts/pmc_roofline.sh (separate FETCH_SIZE / WRITE_SIZE passes of --roofline-only):
+    # the newest round's counter file for this exact launch
+    for rnd in ("r04", "r03", "r02", "r01"):
+        pmc = os.path.join(ROOT, "profiles", rnd, "pmc_glu.json")
+        if not os.path.exists(pmc):
+            continue
         try:
             rec = json.load(open(pmc))
             if rec.get("bytes_per_launch") == int(bytes_per_launch):
                 traffic, traffic_src = rec["hbm_bytes_per_launch"], os.path.relpath(pmc, ROOT)
+                break
         except Exception:  # noqa: BLE001
             pass
     return {"bound": "hbm", "kernel": f"k_gemv2 SwiGLU (ffn gate+up, {K}->{M} x2, cycled over {n_layer} layers)",
@@ -186,15 +197,16 @@ def cpu_baseline(args):
     threads = host_threads()
     try:
         gguf = bench_gguf()
-        r = subprocess.run([REF_BENCH, "-m", gguf, "-t", str(threads), "-p", str(args.cpu_pp), "-n", str(args.cpu_tg),
-                            "-r", str(args.cpu_reps)], capture_output=True, text=True, timeout=900)
+        r = subprocess.run([REF_BENCH, "-m", gguf, "-t", str(threads), "-ngl", "0", "-fa", "1", "-p", str(args.cpu_pp),
+                            "-n", str(args.cpu_tg), "-r", str(args.cpu_reps)], capture_output=True, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         res = json.loads(line)
         return {"value": res["tg_tok_s"], "unit": "tok/s", "cores": threads, "kind": "reference",
                 "pp_tok_s": res.get("pp_tok_s"), "tg_samples": res.get("tg_samples"), "pp_samples": res.get("pp_samples"),
                 "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-                "sample": f"reference CPU backend (libllama+ggml-cpu from /root/reference), same GGUF, "
-                          f"tg{args.cpu_tg} and pp{args.cpu_pp}, one warmup then {args.cpu_reps} repetitions each "
+                "sample": f"reference CPU backend (libllama+ggml-cpu from /root/reference), same GGUF, the bench's own "
+                          f"llama-bench flags at -ngl 0 -fa 1: tg{args.cpu_tg} and pp{args.cpu_pp}, one warmup then "
+                          f"{args.cpu_reps} repetitions each "
                           f"(llama-bench's loop), {threads} threads (the cgroup CPU quota of os.cpu_count() = "
                           f"{os.cpu_count()})"}
     except Exception as e:  # noqa: BLE001 — the GPU number stays valid without the baseline
@@ -211,15 +223,40 @@ def ref_bench(gguf, env, flags, timeout=900):
     return json.loads(line[-1]), r.stderr
 
 
-def dropin_bench(args):
+def tg_from_samples(samples, n_tok):
+    """whole-job rate of llama-bench repetitions: K * n_tok tokens over the summed times
+    (the samples are per-repetition tok/s), and the mean ms per repetition"""
+    secs = [n_tok / x for x in samples]
+    return len(samples) * n_tok / sum(secs), 1000.0 * sum(secs) / len(secs)
+
+
+def dropin_tg(args, env, flags, key):
+    """the timed drop-in tg: W - 1 untimed repetitions (llama-bench runs one warmup of its
+    own), then exactly K = --steps timed ones; returns a result dict or an error string"""
+    gguf = bench_gguf()
+    base = ["-t", "8", "-ngl", "99", "-p", 0, "-n", args.tg]
+    if args.warmup > 1:
+        ref_bench(gguf, env, base + flags + ["-r", args.warmup - 1])
+    t0 = time.perf_counter()
+    res, err = ref_bench(gguf, env, base + flags + ["-r", args.steps])
+    wall = time.perf_counter() - t0
+    if isinstance(res, str):
+        return res
+    value, ms = tg_from_samples(res["tg_samples"], args.tg)
+    st = [json.loads(x.split("stats ", 1)[1]) for x in err.splitlines() if "[mi355x] stats" in x]
+    return {"key": key, "tok_s": value, "ms_per_step": ms, "samples": res["tg_samples"], "avg_ts": res["tg_tok_s"],
+            "wall_s_incl_load": round(wall, 2), "executor": st[0] if st else None}
+
+
+def dropin_bench(args, skip=()):
     """The drop-in path as a user of the reference runs it: the reference's own libllama
     (oracle/_ref/ref-llama-bench, llama-bench's test_prompt / test_gen loop,
     tools/llama-bench/llama-bench.cpp:1962-2010, warmup + -r repetitions) loads
     libggml-mi355x.so through GGML_BACKEND_PATH with every layer offloaded (-ngl 99), on
-    the same Llama-3-8B Q4_K_M GGUF. Reports tg128 and pp512 at -fa 1 and -fa 0, at -fa 1
-    with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv), pp2048 (-b 2048 -ub 512,
-    BASELINE configs[2]), tg128 at depth (-d: llama-bench.cpp:2191-2226, the KV cache
-    filled with D tokens first) and the executor's counters per llama_decode."""
+    the same Llama-3-8B Q4_K_M GGUF. The extra legs beside the headline: tg128 at -fa 0
+    and with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv), pp512 at each, pp2048
+    (-b 2048 -ub 512, BASELINE configs[2]), tg128 at depth (-d: llama-bench.cpp:2191-2226,
+    the KV cache filled with D tokens first)."""
     if not os.path.exists(REF_BENCH) or args.no_dropin:
         return None
     out = {"how": "reference libllama (oracle/_ref/ref-llama-bench) + GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, "
@@ -234,6 +271,8 @@ def dropin_bench(args):
                 if (pp or tg) == 0:
                     continue
                 key = f"{test}_fa{fa}" + ("_q8kv" if ctk else "")
+                if key in skip:
+                    continue
                 runs.append((key, tg > 0, ["-fa", fa, "-p", pp, "-n", tg, "-c", max(256, pp + tg)] +
                              (["-ctk", ctk] if ctk else [])))
         if args.pp2048:
@@ -248,38 +287,36 @@ def dropin_bench(args):
                 continue
             out[f"{key}_tok_s"] = res["tg_tok_s"] if is_tg else res["pp_tok_s"]
             out[f"{key}_samples"] = res["tg_samples"] if is_tg else res["pp_samples"]
-            st = [json.loads(s.split("stats ", 1)[1]) for s in err.splitlines() if "[mi355x] stats" in s]
-            if st and is_tg and key == "tg128_fa1":
-                out[f"{key}_executor"] = st[0]
     except Exception as e:  # noqa: BLE001
         out["error"] = str(e)
     return out
 
 
-def dropin_layer_split(args, world):
+def dropin_layer_split(args, world, tg_leg=True):
     """N > 1: libllama's own layer split as llama-bench -sm layer measures it — ONE process
     (rank 0's child) drives the first N GPUs through this backend, contiguous layer ranges
     per device, boundary activations by cpy_tensor_async (hipMemcpyPeerAsync over xGMI),
-    pipeline parallelism on (src/llama-context.cpp:307-334). tg128 and pp512 at -fa 1."""
+    pipeline parallelism on (src/llama-context.cpp:307-334). The timed tg128 (-r K after
+    W untimed repetitions) is the N > 1 headline; pp512 at -fa 1 beside it."""
     if not os.path.exists(REF_BENCH) or args.no_dropin:
         return None
     vis = os.environ.get("HIP_VISIBLE_DEVICES")
     devs = vis.split(",")[:world] if vis else [str(i) for i in range(world)]
-    env = dict(os.environ, GGML_BACKEND_PATH=LIB, HIP_VISIBLE_DEVICES=",".join(devs))
-    out = {"how": f"reference libllama -sm layer -ts 1x{world} over HIP devices {','.join(devs)}, -ngl 99, -fa 1, "
-                  f"-r {args.dropin_reps}"}
+    env = dict(os.environ, GGML_BACKEND_PATH=LIB, HIP_VISIBLE_DEVICES=",".join(devs), GGML_MI355X_STATS="1")
+    ts = ",".join(["1"] * world)
+    split = ["-fa", "1", "-sm", "layer", "-ts", ts]
+    out = {"how": f"reference libllama -sm layer -ts {ts} over HIP devices {','.join(devs)}, -ngl 99, -fa 1",
+           "devices": devs}
     try:
+        if tg_leg:
+            out["tg"] = dropin_tg(args, env, split + ["-c", 256], "tg128_split")
         gguf = bench_gguf()
-        ts = ",".join(["1"] * world)
-        for key, is_tg, flags in (("tg128", True, ["-p", 0, "-n", args.tg, "-c", 256]),
-                                  ("pp512", False, ["-p", args.pp, "-n", 0, "-c", max(512, args.pp)])):
-            res, _ = ref_bench(gguf, env, ["-t", "8", "-ngl", "99", "-fa", "1", "-sm", "layer", "-ts", ts,
-                                           "-r", args.dropin_reps] + flags)
-            if isinstance(res, str):
-                out[key] = res
-                continue
-            out[f"{key}_tok_s"] = res["tg_tok_s"] if is_tg else res["pp_tok_s"]
-            out[f"{key}_samples"] = res["tg_samples"] if is_tg else res["pp_samples"]
+        res, _ = ref_bench(gguf, env, ["-t", "8", "-ngl", "99", "-p", args.pp, "-n", 0, "-c", max(512, args.pp),
+                                       "-r", args.dropin_reps] + split)
+        if isinstance(res, str):
+            out["pp512"] = res
+        else:
+            out["pp512_tok_s"], out["pp512_samples"] = res["pp_tok_s"], res["pp_samples"]
     except Exception as e:  # noqa: BLE001
         out["error"] = str(e)
     return out
@@ -382,6 +419,50 @@ class PipelineStage:
         self.model.free()
 
 
+def base_line(args, world, value, ms_per_step, scaling, workload, parallelism, recipe, label):
+    return {
+        "metric": METRIC,
+        "value": round(value, 2) if value else value,
+        "unit": "tok/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3) if ms_per_step else ms_per_step,
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "quantised weights (%s), int8 x int8 dot (v_dot4) + f32 accumulate" % recipe,
+        "data": "synthetic (random %s weights, random tokens)" % recipe,
+        "config": {"workload": workload, "model_shape": args.model, "recipe": recipe, "tg": args.tg, "pp": args.pp,
+                   "flash_attn": not args.no_fa, "parallelism": parallelism},
+    }
+
+
+def split_headline(args, world, rank, local, dist, run_split=None):
+    """N > 1 drop-in headline (libllama -sm layer): rank 0 runs the child over GPUs
+    0..N-1; every rank meets in gloo barriers around it (no collective kernel on any GPU).
+    Returns the JSON line on rank 0, None elsewhere. run_split is injectable (CPU tests)."""
+    run_split = run_split or dropin_layer_split
+    barrier(dist, local)
+    t0 = time.perf_counter()
+    split = run_split(args, world) if rank == 0 else None
+    barrier(dist, local)
+    wall = max_over_ranks(dist, time.perf_counter() - t0)
+    if rank != 0:
+        return None
+    tg = (split or {}).get("tg")
+    ok = isinstance(tg, dict)
+    line = base_line(args, world, tg["tok_s"] if ok else None, tg["ms_per_step"] if ok else None, "strong",
+                     f"Llama-3-8B Q4_K_M tg{args.tg} decode (llama-bench test_gen) through the reference libllama, "
+                     f"layer split over {world} GPUs", f"libllama -sm layer -ts {','.join(['1'] * world)} "
+                     "(cpy_tensor_async peer hand-off over xGMI), one sequence", "q4_k_m", "Llama-3-8B")
+    line["dropin_layer_split"] = split
+    line["wall_s_all_legs"] = round(wall, 2)
+    line["roofline"] = None
+    line["cpu_baseline"] = None
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -391,20 +472,21 @@ def main():
     ap.add_argument("--pp", type=int, default=512)
     ap.add_argument("--model", default="llama3_8b", choices=sorted(MODELS))
     ap.add_argument("--recipe", default=None)
-    ap.add_argument("--mode", default="auto", choices=["auto", "single", "pipeline", "replicas"],
-                    help="N>1: pipeline = layer split over the ranks (default), replicas = one model per GPU")
+    ap.add_argument("--mode", default="auto", choices=["auto", "dropin", "single", "pipeline", "replicas"],
+                    help="auto = dropin (the reference libllama on this backend; N>1: its -sm layer split) when "
+                         "oracle/_ref is built and --model llama3_8b, else the package runner (single / pipeline)")
     ap.add_argument("--seqs", type=int, default=0,
                     help="pipeline: sequences of the pipelined_tok_s extra (default = number of GPUs); the headline is 1")
     ap.add_argument("--no-fa", action="store_true", help="llama-bench -fa 0 graph (KQ mul_mat + softmax)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-dropin", action="store_true", help="skip the reference-libllama drop-in measurement")
-    ap.add_argument("--dropin-reps", type=int, default=5, help="llama-bench -r (SURVEY §8d: 5)")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the reference-libllama drop-in legs (runner headline)")
+    ap.add_argument("--dropin-reps", type=int, default=5, help="llama-bench -r of the extra legs (SURVEY §8d: 5)")
     ap.add_argument("--depths", type=lambda v: [int(x) for x in v.split(",") if x], default=[4096, 16384],
                     help="drop-in tg128 at these KV depths (llama-bench -d), comma list, '' for none")
     ap.add_argument("--no-pp2048", dest="pp2048", action="store_false", help="skip the pp2048 legs (BASELINE configs[2])")
-    ap.add_argument("--cpu-pp", type=int, default=64)
-    ap.add_argument("--cpu-tg", type=int, default=32)
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-pp", type=int, default=512)
+    ap.add_argument("--cpu-tg", type=int, default=128)
+    ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--skip-roofline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing (for scripts/pmc_roofline.sh's rocprofv3 --pmc passes)")
@@ -425,8 +507,20 @@ def main():
         model.free()
         return
 
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    dropin_ok = os.path.exists(REF_BENCH) and not args.no_dropin and args.model == "llama3_8b" and not args.no_fa
+    mode = args.mode
+    if mode == "auto":
+        mode = "dropin" if dropin_ok else ("pipeline" if world_env > 1 else "single")
+    if mode == "dropin" and world_env > 1:
+        world, rank, local, dist = dist_setup(args.gpus, backend="gloo")
+        line = split_headline(args, world, rank, local, dist)
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        dist.destroy_process_group()
+        return
     world, rank, local, dist = dist_setup(args.gpus)
-    mode = args.mode if args.mode != "auto" else ("pipeline" if world > 1 else "single")
+    runner_mode = "single" if mode == "dropin" else mode
     from mi355x_pkg import load_package
     pkg = load_package()
     shape_name, def_recipe, label = MODELS[args.model]
@@ -440,7 +534,7 @@ def main():
     rng = np.random.default_rng(42 + rank)
     n_vocab = shape["n_vocab"]
 
-    if mode == "pipeline":
+    if runner_mode == "pipeline":
         n_seq = args.seqs or world
         stage = PipelineStage(pkg, dist, rank, world, local, shape, recipe, not args.no_fa, n_ctx, n_seq)
         be, model = stage.be, stage.model
@@ -463,14 +557,14 @@ def main():
     be.synchronize()
     barrier(dist, local)
     dt = max_over_ranks(dist, time.perf_counter() - t0)
-    if mode == "pipeline":
+    if runner_mode == "pipeline":
         tokens = args.steps * tokens_per_step
     else:
         tokens = sum_over_ranks(dist, args.steps * tokens_per_step)
     tg_value = tokens / dt
 
     pipelined = None
-    if mode == "pipeline" and n_seq > 1:   # extra: N sequences in flight, one per stage
+    if runner_mode == "pipeline" and n_seq > 1:   # extra: N sequences in flight, one per stage
         stage.tg(rng, n_vocab, args.tg)
         barrier(dist, local)
         t2 = time.perf_counter()
@@ -482,7 +576,7 @@ def main():
     # pp512 beside it (not the headline value)
     pp_tok_s = None
     if args.pp > 0:
-        if mode == "pipeline":
+        if runner_mode == "pipeline":
             stage.pp(rng, n_vocab, args.pp)   # warm
             barrier(dist, local)
             t1 = time.perf_counter()
@@ -507,7 +601,7 @@ def main():
     # pp2048 (BASELINE configs[2]): llama-bench -p 2048 -b 2048 -ub 512, four 512-token
     # ubatches into a cache growing to 2048 cells; single GPU only
     pp2048_tok_s = None
-    if args.pp2048 and mode != "pipeline" and args.pp > 0:
+    if args.pp2048 and runner_mode != "pipeline" and args.pp > 0:
         sess.free()
         sess = pkg.Session(model, n_ctx=2304, n_ubatch=512, flash_attn=not args.no_fa)
         toks = rng.integers(0, n_vocab, size=2048, dtype=np.int32)
@@ -522,53 +616,58 @@ def main():
 
     stats = be.stats()
     # weights one decoded token reads (all stages together)
-    decode_bytes = int(sum_over_ranks(dist, model.decode_bytes())) if mode == "pipeline" else model.decode_bytes()
+    decode_bytes = int(sum_over_ranks(dist, model.decode_bytes())) if runner_mode == "pipeline" else model.decode_bytes()
     roof = None if (args.skip_roofline or shape.get("n_expert")) else roofline_glu(pkg, be, model)
     cpu = cpu_baseline(args) if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
-    dropin = dropin_bench(args) if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
-    barrier(dist, local)
-    split_leg = dropin_layer_split(args, world) if (rank == 0 and world > 1 and args.model == "llama3_8b") else None
+    head_dropin = None
+    if mode == "dropin" and rank == 0:
+        env = dict(os.environ, GGML_BACKEND_PATH=LIB, GGML_MI355X_STATS="1")
+        head_dropin = dropin_tg(args, env, ["-fa", 1, "-c", 256], "tg128_fa1")
+    dropin = dropin_bench(args, skip=("tg128_fa1",) if mode == "dropin" else ()) \
+        if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
     barrier(dist, local)
 
     if rank == 0:
-        per_gpu_bytes_s = decode_bytes * tg_value / world
         par = {"single": "single", "replicas": f"replicas x{world}",
-               "pipeline": f"layer split x{world} (RCCL p2p hidden-state hand-off), one sequence (llama-bench -sm layer)"}[mode]
-        out = {
-            "metric": METRIC,
-            "value": round(tg_value, 2),
-            "unit": "tok/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * dt / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "strong" if mode == "pipeline" else "weak",
-            "vs_baseline": None,
-            "dtype": "quantised weights (%s), int8 x int8 dot (v_dot4) + f32 accumulate" % recipe,
-            "data": "synthetic (random %s weights generated on device, random tokens)" % recipe,
-            "config": {"workload": f"{label} {recipe.upper()} tg{args.tg} decode (llama-bench test_gen)",
-                       "model_shape": args.model, "recipe": recipe, "tg": args.tg, "pp": args.pp,
-                       "flash_attn": not args.no_fa, "parallelism": par},
-            "pp512_tok_s": round(pp_tok_s, 1) if pp_tok_s else None,
-            "pp2048_tok_s": round(pp2048_tok_s, 1) if pp2048_tok_s else None,
-            "pp_roofline": ({"bound": "mfma", "achieved": round(pp_tok_s * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world, 1),
+               "pipeline": f"layer split x{world} (RCCL p2p hidden-state hand-off), one sequence (llama-bench -sm layer)"}[runner_mode]
+        runner = {"how": "this package's runner (mx_llama: the same backend, device-side random weights) "
+                         f"-> {par}, {args.warmup} warmup + {args.steps} timed tg steps",
+                  "tg128_tok_s": round(tg_value, 2), "ms_per_step": round(1000.0 * dt / args.steps, 3),
+                  "pp512_tok_s": round(pp_tok_s, 1) if pp_tok_s else None,
+                  "pp2048_tok_s": round(pp2048_tok_s, 1) if pp2048_tok_s else None,
+                  "executor": stats, "pipelined": pipelined}
+        if isinstance(head_dropin, dict):
+            out = base_line(args, world, head_dropin["tok_s"], head_dropin["ms_per_step"], "weak",
+                            f"{label} {recipe.upper()} tg{args.tg} decode (llama-bench test_gen) through the reference "
+                            "libllama (GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, -fa 1)", "single", recipe, label)
+            out["headline"] = head_dropin
+            hv = head_dropin["tok_s"]
+        else:
+            # runner headline (no reference build, another model, or the drop-in failed)
+            out = base_line(args, world, tg_value, 1000.0 * dt / args.steps, "strong" if runner_mode == "pipeline" else "weak",
+                            f"{label} {recipe.upper()} tg{args.tg} decode (llama-bench test_gen), package runner", par,
+                            recipe, label)
+            if head_dropin is not None:
+                out["headline_dropin_error"] = head_dropin
+            hv = tg_value
+        pp_ref = (dropin or {}).get("pp512_fa1_tok_s") if isinstance(head_dropin, dict) else pp_tok_s
+        out.update({
+            "pp512_tok_s": round(pp_ref, 1) if pp_ref else None,
+            "pp_roofline": ({"bound": "mfma", "achieved": round(pp_ref * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world, 1),
                              "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
-                             "frac": round(pp_tok_s * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world / MFMA_F16_PEAK_TFS, 4),
+                             "frac": round(pp_ref * PP_FLOPS_PER_TOKEN[args.model] / 1e12 / world / MFMA_F16_PEAK_TFS, 4),
                              "flops_per_token": PP_FLOPS_PER_TOKEN[args.model]}
-                            if pp_tok_s and args.model in PP_FLOPS_PER_TOKEN else None),
+                            if pp_ref and args.model in PP_FLOPS_PER_TOKEN else None),
             "decode_bytes_per_token": decode_bytes,
-            "decode_roofline": {"achieved_GBs": round(per_gpu_bytes_s / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
-                                "frac": round(per_gpu_bytes_s / 1e9 / HBM_PEAK_GBS, 4)},
+            "decode_roofline": {"achieved_GBs": round(decode_bytes * hv / world / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
+                                "frac": round(decode_bytes * hv / world / 1e9 / HBM_PEAK_GBS, 4)},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "runner": runner,
             "dropin": dropin,
-            "dropin_layer_split": split_leg,
-            "pipelined": pipelined,
-            "executor": stats,
-        }
+        })
         print(json.dumps(out), flush=True)
-    if mode == "pipeline":
+    if runner_mode == "pipeline":
         stage.free()
     else:
         sess.free()

@@ -6,6 +6,8 @@
 #include <string>
 #include <vector>
 #include <unordered_map>
+#include <initializer_list>
+#include <utility>
 
 namespace mx {
 
@@ -219,6 +221,10 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 // FLASH_ATTN_EXT -> RESHAPE -> MUL_MAT(wo) -> ADD(residual) of one decode token (ops_attn_o.hip)
 int fuse_attn_oproj(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 bool t_overlaps_ext(const ggml_tensor * a, const ggml_tensor * b);
+// no output of a fused launch overlaps its inputs or another output, except the named
+// element-wise in-place (output, input) pairs at the same start (exec.cpp)
+bool fused_io_ok(std::initializer_list<const ggml_tensor *> outs, std::initializer_list<const ggml_tensor *> ins,
+                 std::initializer_list<std::pair<const ggml_tensor *, const ggml_tensor *>> inplace = {});
 int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 // the executor's guard for a node about to run (deferred norms it reads or overwrites)
 void deferred_guard_node_ext(OpCtx & c, const ggml_tensor * n);

@@ -102,6 +102,30 @@ static bool t_overlaps(const ggml_tensor * a, const ggml_tensor * b) {
 }
 bool t_overlaps_ext(const ggml_tensor * a, const ggml_tensor * b) { return t_overlaps(a, b); }
 
+// General output-overlap guard of a fused launch (round 4). ggml-alloc hands a node the
+// memory of tensors that died earlier in node order (and runs ADD/MUL/SOFT_MAX/ROPE in
+// place), so an unfused chain may legally write a later member's output over an input an
+// earlier member already consumed; one fused grid reads and writes in no such order (two
+// allocator-aliasing bugs came from exactly this: the MoE chain, r02, and the prefill q/k/v
+// epilogue, r03). A fusion runs only if no output overlaps an input it reads or another
+// output — except the (output, input) pairs the caller names as element-wise in place:
+// the same start address, every element read before it is written by the same thread.
+bool fused_io_ok(std::initializer_list<const ggml_tensor *> outs, std::initializer_list<const ggml_tensor *> ins,
+                 std::initializer_list<std::pair<const ggml_tensor *, const ggml_tensor *>> inplace) {
+    for (const ggml_tensor * o : outs) {
+        if (!o) continue;
+        for (const ggml_tensor * o2 : outs)
+            if (o2 && o2 != o && t_overlaps(o, o2)) return false;
+        for (const ggml_tensor * in : ins) {
+            if (!in || !t_overlaps(o, in)) continue;
+            bool ok = false;
+            for (const auto & pr : inplace) ok = ok || (pr.first == o && pr.second == in && o->data == in->data);
+            if (!ok) return false;
+        }
+    }
+    return true;
+}
+
 XStage xstage_of(Stream * s, const ggml_tensor * x) {
     for (const DeferredNorm & d : s->deferred)
         if (x->data == d.mul->data && mx_nelements(x) == mx_nelements(d.mul) && mx_is_contiguous(x)) {
@@ -236,6 +260,11 @@ static bool try_fuse_rms_mul(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     const ggml_tensor * w = mul->src[0] == norm ? mul->src[1] : (mul->src[1] == norm ? mul->src[0] : nullptr);
     if (!w || w->type != GGML_TYPE_F32 || w->ne[0] != norm->ne[0] || !mx_is_contiguous_rows(w)) return false;
     if (!mx_are_same_shape(mul, norm)) return false;
+    // one row per workgroup, read whole before it is written: in place over x is safe, any
+    // other overlap is not
+    const ggml_tensor * x = norm->src[0];
+    const bool same_rows = mx_are_same_shape(mul, x) && mul->nb[1] == x->nb[1] && mul->nb[2] == x->nb[2] && mul->nb[3] == x->nb[3];
+    if (!fused_io_ok({mul}, {x, w}, {{mul, same_rows ? x : nullptr}})) return false;
     // the norm output must be consumed only by the MUL (it is a graph-internal temporary)
     if (uses[norm] != 1 || (norm->flags & GGML_TENSOR_FLAG_OUTPUT)) return false;
     act_cache_invalidate(c.s, mul);
@@ -258,6 +287,10 @@ static int try_fuse_mm_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     if (add->op != GGML_OP_ADD) return 0;
     const ggml_tensor * res = add->src[0] == mm ? add->src[1] : (add->src[1] == mm ? add->src[0] : nullptr);
     if (!res || res == mm || uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    // the epilogue reads each residual element and writes the sum from the same thread: in
+    // place (same start and strides) is safe, a shifted overlap is not
+    const bool same = res->nb[1] == add->nb[1] && res->nb[2] == add->nb[2] && res->nb[3] == add->nb[3];
+    if (!fused_io_ok({add}, {res}, {{add, same ? res : nullptr}})) return 0;
     act_cache_invalidate(c.s, add);
     if (mmvq_small_batch_ok(mm)) return mmvq_fused_add(c, mm, res, add) ? 2 : 0;
     if (i + 3 < g->n_nodes) {

@@ -747,6 +747,11 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         if (n != sm && n != kqv && n != out && !nf_view(n)) return 0;
         if (nf_view(n) && nf_base(n) == kqv && n != pm) return 0;   // another reader of kqv
     }
+    // the output may sit exactly over q (the allocator reuses the dead q's memory): element
+    // (d, h, t) of both is at (t H + h) D + d when q's strides are the permuted contiguous
+    // ones, and each workgroup reads its q rows before it writes the same rows
+    const bool q_same = q->nb[1] == (size_t) H * D * 4 && q->nb[2] == (size_t) D * 4;
+    if (!fused_io_ok({out}, {q, k, v, m}, {{out, q_same ? q : nullptr}})) return 0;
     for (const ggml_tensor * t : {(const ggml_tensor *) kq, (const ggml_tensor *) sm, (const ggml_tensor *) kqv})
         for (int j = last + 1; j < g->n_nodes; ++j)
             for (int s2 = 0; s2 < GGML_MAX_SRC; ++s2)

@@ -272,3 +272,103 @@ def test_dropin_kl_divergence(ggufs, tmp_path, shape, recipe, ctk):
         print(f"kld {shape} {recipe} ctk={ctk} inc={inc}: mean {kld.mean():.3e} p99 {np.percentile(kld, 99):.3e} "
               f"max {kld.max():.3e} top1 {top:.3f}")
         assert kld.mean() < 5e-4 and kld.max() < 5e-3 and top >= 0.90, (kld.mean(), kld.max(), top)
+
+
+def parse_seq_state(blob):
+    """a llama_state_seq_get_data blob (src/llama-kv-cache.cpp:1648-1867): returns the
+    bit-exact part (stream / cell counts, every cell's position and sequence ids, the
+    per-layer type / row-size headers) and the K / V payloads (one uint8 array per layer
+    and kind)"""
+    o = 0
+
+    def take(n):
+        nonlocal o
+        b = blob[o:o + n]
+        o += n
+        return b
+
+    u32 = lambda: int(np.frombuffer(take(4), np.uint32)[0])   # noqa: E731
+    exact, payload = [], []
+    n_stream = u32()
+    exact.append(("n_stream", n_stream))
+    for _ in range(n_stream):
+        cells = u32()
+        exact.append(("cells", cells))
+        if cells == 0:
+            continue
+        for _ in range(cells):
+            pos = int(np.frombuffer(take(4), np.int32)[0])
+            ns = u32()
+            exact.append(("cell", pos, tuple(np.frombuffer(take(4 * ns), np.int32).tolist())))
+        v_trans, n_layer = u32(), u32()
+        exact.append(("v_trans", v_trans, "n_layer", n_layer))
+        for _ in range(n_layer):
+            kt = int(np.frombuffer(take(4), np.int32)[0])
+            row = int(np.frombuffer(take(8), np.uint64)[0])
+            exact.append(("k", kt, row))
+            payload.append((kt, take(cells * row)))
+        for _ in range(n_layer):
+            vt = int(np.frombuffer(take(4), np.int32)[0])
+            if not v_trans:
+                row = int(np.frombuffer(take(8), np.uint64)[0])
+                exact.append(("v", vt, row))
+                payload.append((vt, take(cells * row)))
+            else:
+                el, nv = u32(), u32()
+                exact.append(("vt", vt, el, nv))
+                payload.append((vt, take(cells * el * nv)))
+    assert o == len(blob), (o, len(blob))
+    return exact, payload
+
+
+@pytest.mark.parametrize("fa,ctk", [(1, None), (0, None), (1, 8)])
+def test_dropin_kv_state(ggufs, tmp_path, fa, ctk):
+    """KV state save / restore through this backend (SURVEY §5 checkpoint/resume):
+    llama_state_seq_get_data / set_data and llama_state_save_file / load_file
+    (src/llama-context.cpp:3416-3431) read and write the raw KV rows through get_tensor /
+    set_tensor. oracle/state_probe.cpp (built against the reference libllama) prefills a
+    prompt on a GPU context, saves, and continues; then restores into fresh GPU contexts,
+    a CPU context, and the CPU's own state into a GPU context. Bit-exact: the GPU state
+    read back after a restore, the continued logits after either restore (seq blob and
+    state file), and the cell occupancy (positions, sequence ids, row headers) against the
+    reference CPU backend's state; the K/V rows themselves (computed by two backends) and
+    the cross-backend continuations within the whole-graph bound. fa 0 stores V
+    transposed; ctk 8 is the q8_0 cache."""
+    probe = os.path.join(ROOT, "oracle", "_ref", "state-probe")
+    if not os.path.exists(probe):
+        pytest.skip("oracle/_ref/state-probe not built")
+    rng = np.random.default_rng(40 + fa)
+    rng.integers(0, 1000, 37).astype(np.int32).tofile(tmp_path / "p.i32")
+    rng.integers(0, 1000, 6).astype(np.int32).tofile(tmp_path / "g.i32")
+    cmd = [probe, "-m", ggufs[("small", "q4_k_m")], "-fa", str(fa), "--prompt", str(tmp_path / "p.i32"),
+           "--gen", str(tmp_path / "g.i32"), "--out", str(tmp_path)] + (["-ctk", str(ctk)] if ctk else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, GGML_BACKEND_PATH=LIB))
+    assert r.returncode == 0, r.stderr[-2000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    n = info["blob_bytes"]
+    assert n > 0 and info["set_b"] == n and info["set_d"] == n and info["set_e"] == n, info
+    assert info["saved"] == 1 and info["loaded"] == 1 and info["file_tokens"] == 37, info
+    blob = {k: np.fromfile(tmp_path / f"blob_{k}.bin", np.uint8) for k in "abc"}
+    lg = {k: np.fromfile(tmp_path / f"logits_{k}.f32", np.float32).reshape(6, -1) for k in "abcdef"}
+    # GPU -> GPU: the state survives set_tensor / get_tensor bit for bit, and so does the
+    # continuation (seq blob and whole-context state file)
+    assert np.array_equal(blob["b"], blob["a"])
+    assert np.array_equal(lg["b"].view(np.uint32), lg["a"].view(np.uint32))
+    assert np.array_equal(lg["f"].view(np.uint32), lg["a"].view(np.uint32))
+    # KV indexing bit-exact against the reference CPU backend's own state
+    ea, pa = parse_seq_state(blob["a"])
+    ec, pc = parse_seq_state(blob["c"])
+    assert ea == ec
+    assert sum(1 for e in ea if e[0] == "cell") == 37
+    for (ta, xa), (tc, xc) in zip(pa, pc):
+        if ta == 1:     # f16 rows: values within the whole-graph bound
+            assert nmse(xa.view(np.float16).astype(np.float64), xc.view(np.float16).astype(np.float64)) < TOL
+        elif ta == 8:   # q8_0 rows: dequantise (f16 scale + 32 int8)
+            def deq(x):
+                b = x.reshape(-1, 34)
+                return (b[:, :2].copy().view(np.float16).astype(np.float64) * b[:, 2:].view(np.int8).astype(np.float64))
+            assert nmse(deq(xa), deq(xc)) < TOL
+    # across backends: the GPU state continued on the CPU, the CPU state on the GPU
+    assert nmse(lg["a"], lg["c"]) < TOL
+    assert nmse(lg["d"], lg["a"]) < TOL
+    assert nmse(lg["e"], lg["c"]) < TOL

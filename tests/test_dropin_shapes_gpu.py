@@ -64,6 +64,11 @@ def l70b(gguf_dir):
 
 
 @pytest.fixture(scope="module")
+def l70b8(gguf_dir):
+    return make_gguf(gguf_dir, "llama3_70b_8l", "q4_k_m")
+
+
+@pytest.fixture(scope="module")
 def mixtral(gguf_dir):
     return make_gguf(gguf_dir, "mixtral_2l", "q5_k_m")
 
@@ -231,6 +236,31 @@ def test_llama3_70b_width_pp512(l70b, tmp_path, fa):
     assert k["mmq3g"] + k["mmq4 glu"] == 2, k
     assert any(ln.startswith("mmq4 glu") and "M=28672" in ln and "K=8192" in ln for ln in klog), k
     assert k["fa_mma2" if fa else "attn_nofa_mma"] == 2, k
+
+
+@pytest.mark.parametrize("incremental", [False, True])
+def test_llama3_70b_width_layer_split_8(l70b8, tmp_path, incremental):
+    """BASELINE configs[3] in miniature: an eight-layer GGUF at the Llama-3-70B widths,
+    libllama -sm layer -ts 1,1,1,1,1,1,1,1 over eight logical devices of the one MI355X
+    (GGML_MI355X_VIRTUAL_DEVICES=8): one layer per device (src/llama-model.cpp:2599-2609),
+    pipeline parallelism on, every one of the seven boundary activations handed over by
+    be_cpy_async on its peer-copy branch (GGML_MI355X_FORCE_PEER=1, the branch eight real
+    GPUs take). Logits against the reference CPU backend: incremental decode at the
+    whole-graph bound, a 40-token prefill at the 70B-width prefill bound (per-node
+    attribution: profiles/r04/attrib_llama3_70b_2l_fa1.txt)."""
+    toks = np.random.default_rng(35).integers(0, 128000, 6 if incremental else 40)
+    cpu, _, _ = run_ref(tmp_path, l70b8, toks, 0, 1, incremental=incremental)
+    gpu, log, klog = run_ref(tmp_path, l70b8, toks, 99, 1, incremental=incremental,
+                             extra=["-sm", "layer", "-ts", ",".join(["1"] * 8)],
+                             env_extra={"GGML_MI355X_VIRTUAL_DEVICES": "8", "GGML_MI355X_FORCE_PEER": "1"})
+    assert "MI355X7" in log, log[-2000:]
+    assert np.all(np.isfinite(gpu))
+    err = nmse(gpu, cpu)
+    assert err < (TOL if incremental else TOL_70B_PP), err
+    cp = [ln for ln in klog if ln.startswith("cpy_async")]
+    assert cp and all("peer=1" in ln for ln in cp), cp[:8]
+    for i in range(7):
+        assert any(f"MI355X{i} -> MI355X{i + 1} " in ln for ln in cp), (i, cp[:10])
 
 
 def test_llama3_8b_width_pp2048(l8b, tmp_path):

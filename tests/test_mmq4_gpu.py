@@ -17,6 +17,8 @@ Outlier rows: k_mmq4 dequantises weights into f16 MFMA operands scaled by 2^10; 
 whose scaled values would pass the f16 range (|w| > 32 at 2^10) lowers its row's scale
 (m4_range). The outlier cases put |w| up to ~200 in whole rows, in the LAST super-block of
 a row (the rescale happens after accumulation started) and in the first one."""
+import os
+
 import numpy as np
 import pytest
 
@@ -74,8 +76,17 @@ def run(pkg, be, build, tune=()):
     return res, log
 
 
+# MX_TEST_NO_KLOG=1: numeric checks only (running these cases against an older build whose
+# kernel-choice log lacks the launch lines, profiles/r04/mmq4_outlier_old_vs_new.txt)
+NO_KLOG = os.environ.get("MX_TEST_NO_KLOG") == "1"
+
+
 def launch_lines(log):
     return [l for l in log if l.startswith("mmq4 launch ")]
+
+
+def klog_has(log, pred):
+    return NO_KLOG or any(pred(l) for l in log)
 
 
 @pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K"])
@@ -97,8 +108,8 @@ def test_mmq4_plain(pkg, backend, orc, tname, ks, outlier):
         return [ctx.mul_mat(tw, tx)], [(tw, w), (tx, x)]
 
     (y,), log = run(pkg, backend, build, [(20, ks)])
-    assert any(l.startswith(f"mmq4 qt={tid} ") for l in log), log
-    assert launch_lines(log) == [l for l in launch_lines(log) if f"epi=0 ks={ks} " in l] and launch_lines(log), log
+    assert klog_has(log, lambda l: l.startswith(f"mmq4 qt={tid} ")), log
+    assert NO_KLOG or (launch_lines(log) and all(f"epi=0 ks={ks} " in l for l in launch_lines(log))), log
     check(y.reshape(N, M), orc.mul_mat(tid, w, rb, x, exact=True), rows_out)
 
 
@@ -121,8 +132,8 @@ def test_mmq4_residual(pkg, backend, orc, tname, ks):
         return [ctx.add(ctx.mul_mat(tw, tx), tr)], [(tw, w), (tx, x), (tr, r)]
 
     (y,), log = run(pkg, backend, build, [(20, ks)])
-    assert any(l.startswith(f"mmq4 qt={tid} ") and "res=1" in l for l in log), log
-    assert any(f"epi=0 ks={ks} " in l for l in launch_lines(log)), log
+    assert klog_has(log, lambda l: l.startswith(f"mmq4 qt={tid} ") and "res=1" in l), log
+    assert klog_has(launch_lines(log), lambda l: f"epi=0 ks={ks} " in l), log
     check(y.reshape(N, M), orc.mul_mat(tid, w, rb, x, exact=True) + r, rows_out)
 
 
@@ -152,8 +163,8 @@ def test_mmq4_group(pkg, backend, orc, types, ks):
         return outs, [(tx, x)] + [(tw, w) for tw, (w, _) in zip(tws, ws)]
 
     ys, log = run(pkg, backend, build, [(20, ks)])
-    assert any(l.startswith(f"mmq4 group n={len(types)} ") for l in log), log
-    assert any(f"epi=0 ks={ks} " in l for l in launch_lines(log)), log
+    assert klog_has(log, lambda l: l.startswith(f"mmq4 group n={len(types)} ")), log
+    assert klog_has(launch_lines(log), lambda l: f"epi=0 ks={ks} " in l), log
     for y, t, M, (w, rb), ro in zip(ys, types, Ms, ws, outs_rows):
         check(y.reshape(N, M), orc.mul_mat(NAMES[t], w, rb, x, exact=True), ro)
 
@@ -180,8 +191,8 @@ def test_mmq4_glu(pkg, backend, orc, tname, N):
         return [ctx.swiglu_split(gate, up)], [(tg, wg), (tu, wu), (tx, x)]
 
     (y,), log = run(pkg, backend, build)
-    assert any(l.startswith(f"mmq4 glu qt={tid} ") for l in log), log
-    assert any("epi=1 " in l for l in launch_lines(log)), log
+    assert klog_has(log, lambda l: l.startswith(f"mmq4 glu qt={tid} ")), log
+    assert klog_has(launch_lines(log), lambda l: "epi=1 " in l), log
     g = orc.mul_mat(tid, wg, rb, x, exact=True)
     u = orc.mul_mat(tid, wu, rb, x, exact=True)
     check(y.reshape(N, M), orc.swiglu(g, u), rows_out)
@@ -211,8 +222,8 @@ def test_mmq4_moe(pkg, backend, orc, tname):
         return [ctx.mul_mat_id(tw, tx, ti)], [(tw, w), (tx, x), (ti, ids)]
 
     (y,), log = run(pkg, backend, build)
-    assert any(l.startswith(f"mmq4 moe qt={tid} ") for l in log), log
-    assert any("epi=2 " in l for l in launch_lines(log)), log
+    assert klog_has(log, lambda l: l.startswith(f"mmq4 moe qt={tid} ")), log
+    assert klog_has(launch_lines(log), lambda l: "epi=2 " in l), log
     y = y.reshape(T, used, M)
     for e in range(E):
         sel = np.argwhere(ids == e)

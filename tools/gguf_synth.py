@@ -38,6 +38,10 @@ SHAPES = {
     # layer 1 (use_more_bits) attn_v / ffn_down Q6_K
     "llama3_70b_2l": dict(n_vocab=128256, n_embd=8192, n_layer=2, n_head=64, n_head_kv=8, n_ff=28672,
                           n_ctx=8192, rope_base=500000.0, rule70b=True),
+    # eight layers at 70B widths: one per device of an 8-way layer split (-sm layer -ts 1x8,
+    # BASELINE configs[3]); use_more_bits layers 0, 3, 6, 7 carry the Q6_K attn_v / ffn_down
+    "llama3_70b_8l": dict(n_vocab=128256, n_embd=8192, n_layer=8, n_head=64, n_head_kv=8, n_ff=28672,
+                          n_ctx=8192, rope_base=500000.0, rule70b=True),
     "mixtral_8x7b": dict(n_vocab=32000, n_embd=4096, n_layer=32, n_head=32, n_head_kv=8, n_ff=14336,
                          n_ctx=32768, rope_base=1e6, n_expert=8, n_expert_used=2),
     "mixtral_2l": dict(n_vocab=32000, n_embd=4096, n_layer=2, n_head=32, n_head_kv=8, n_ff=14336,
