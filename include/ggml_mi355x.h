@@ -54,9 +54,15 @@ extern "C" {
 double ggml_backend_mi355x_time_mmvq(ggml_backend_t backend, const struct ggml_tensor * const * w,
                                      const struct ggml_tensor * const * w2, int n_w,
                                      const struct ggml_tensor * x, struct ggml_tensor * dst, int iters);
-/* Launch-geometry overrides for tuning sweeps (0 = built-in choice):
- * idx 0/1 = GEMV lanes-per-row / units-per-lane, 2/3 = the same for the fused SwiGLU GEMV. */
+/* Tuning knobs for A/B runs and sweeps (0 = the built-in choice; every knob is documented
+ * at its g_tune[idx] use in the sources, e.g. 17 prefill GEMM choice, 20 forced split-K,
+ * 23 FA weight-prefetch MB). The same knobs can be set for a whole process through
+ * GGML_MI355X_TUNE="idx=val,idx=val". Timing variants and debug masks only act in an A/B
+ * variant build (ggml_backend_mi355x_ab_variants). */
 void ggml_backend_mi355x_set_tune(int idx, int value);
+/* 1 when this library is an A/B variant build (MX_AB_VARIANTS: the experiment-only code
+ * paths the tuning knobs reach), 0 for the product library */
+int ggml_backend_mi355x_ab_variants(void);
 /* Debug: phase timestamps (s_memtime) of the first workgroup of the instrumented kernels,
  * recorded while tune index 6 is set: slot s (0 decode flash-attn, 1 GEMV, 2 QKV) at
  * out[s*128 + wave*8 + phase]. Read-and-clear; returns n or -1. */

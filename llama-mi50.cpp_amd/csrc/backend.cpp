@@ -728,3 +728,5 @@ namespace mx { unsigned g_tune_gen = 0; }   // part of every cgraph signature (e
 extern "C" void ggml_backend_mi355x_set_tune(int idx, int value) {
     if (idx >= 0 && idx < 32 && mx::g_tune[idx] != value) { mx::g_tune[idx] = value; ++mx::g_tune_gen; }
 }
+
+extern "C" int ggml_backend_mi355x_ab_variants(void) { return MX_AB_VARIANTS; }

@@ -130,13 +130,13 @@ XStage xstage_of(Stream * s, const ggml_tensor * x) {
     for (const DeferredNorm & d : s->deferred)
         if (x->data == d.mul->data && mx_nelements(x) == mx_nelements(d.mul) && mx_is_contiguous(x)) {
             XStage xs{(const float *) d.norm->src[0]->data, (const float *) d.w->data, mx_op_param<float>(d.norm, 0), 1};
-            xs.dbg = g_tune[11];
+            xs.dbg = MX_AB_VARIANTS ? g_tune[11] : 0;
             xs.xcd = g_tune[15] != 1;
             xs.drain = g_tune[14] == 1;
             return xs;
         }
     XStage xs{(const float *) x->data, nullptr, 0.0f, 0};
-    xs.dbg = g_tune[11];
+    xs.dbg = MX_AB_VARIANTS ? g_tune[11] : 0;
     xs.xcd = g_tune[15] != 1;
     xs.drain = g_tune[14] == 1;
     if (const ActQ * a = act_cache_find(s, x)) {

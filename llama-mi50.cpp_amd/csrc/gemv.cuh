@@ -656,9 +656,9 @@ __device__ __forceinline__ void gemv_rows_staged(const char * const (&rows)[NM],
                 if constexpr (xs_norm(MODE)) asm volatile("" : "+v"(sr.w[h][j]));
             }
     }
-    if (!(xs.dbg & 1)) stage_finish<NT, MODE, UPL * NM * w2_loads<QT>()>(xs, K, a, red, sr);
+    if (!MX_DBG(xs.dbg & 1)) stage_finish<NT, MODE, UPL * NM * w2_loads<QT>()>(xs, K, a, red, sr);
     fence();                                  // older than the staged x: already landed
-    if (xs.dbg & 2) {                         // timing experiment: consume the loads only
+    if (MX_DBG(xs.dbg & 2)) {                         // timing experiment: consume the loads only
         for (int it = 0; it < n_iter; ++it) {
             if (it) w2_load_batch<QT, UPL, NM>(rows, it * STEP + sub, LPR, units, r);
             const int * wv = (const int *) &r[0][0];

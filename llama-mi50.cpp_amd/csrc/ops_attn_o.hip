@@ -29,6 +29,14 @@
 #include "backend.h"
 #include "gemv.cuh"
 
+#if !MX_AB_VARIANTS
+// product build: the fused form is an A/B experiment (measured slower), the
+// chain runs as the decode attention + the output-projection GEMV
+namespace mx {
+int fuse_attn_oproj(OpCtx &, ggml_cgraph *, int, const UseCount &) { return 0; }
+}  // namespace mx
+#else
+
 namespace mx {
 
 struct AoArgs {
@@ -652,3 +660,4 @@ int fuse_attn_oproj(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
 }
 
 }  // namespace mx
+#endif  // MX_AB_VARIANTS

@@ -472,6 +472,12 @@ constexpr int FD_LONG_NI = 8;
 constexpr int FD_LONG_MAXSPLIT = 32768;   // the combine's split weights in LDS (128 KB): 4M keys at D 128
 static FdCfg fd_cfg(int D, int Gt, int64_t n_kv) {
     const int cs16 = 16 * FD_NI * (64 / (D / 8)), cs4 = 4 * FD_NI * (64 / (D / 8));
+    // g_tune[1] = NI (2 / 4, experiment): short caches too take the LONG geometry — chunks of
+    // 4 NI 64/(D/8) keys, one per workgroup, G = g_tune[29] (default 1) heads, plus the combine
+    if (g_tune[1] && D == 128 && n_kv <= cs16 && n_kv > 4 * g_tune[1] * (64 / (D / 8))) {   // >= 2 splits
+        const int g = g_tune[29] ? std::min(g_tune[29], Gt) : 1;
+        return {g, 4, (int) mx_ceil_div(n_kv, 4 * g_tune[1] * (64 / (D / 8))), true};
+    }
     if (g_tune[10] == 2 || (g_tune[10] != 3 && n_kv <= cs16)) return {1, 16, (int) mx_ceil_div(n_kv, cs16), false};
     if (g_tune[10] == 3) return {Gt, 4, (int) std::min<int64_t>(FD_MAXSPLIT, mx_ceil_div(n_kv, cs4)), false};
     // sweeps: g_tune[28] keys rows per lane (4 / 8 / 16), g_tune[29] heads per workgroup (D 128, f16)
@@ -536,12 +542,13 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
             (void) attr; \
             k_fattn_dec2_combine<DD, GG><<<gc, 256, lds, c.st>>>(a); \
             return; }
-        const int ni = D == 128 && g_tune[28] ? g_tune[28] : FD_LONG_NI;
+        const int ni = D == 128 && g_tune[1] && a.n_kv <= 16 * FD_NI * (64 / (D / 8)) && a.n_kv > 4 * g_tune[1] * (64 / (D / 8)) ? g_tune[1] :
+                       D == 128 && g_tune[28] ? g_tune[28] : FD_LONG_NI;
         if (ni != FD_LONG_NI && !kq) {   // sweep geometries (f16, D 128)
 #define FS(NI_, GG) if (ni == NI_ && f.G == GG) { \
                 k_fattn_dec2<128, GG, 4, false, NI_, true><<<grid, 256, 0, c.st>>>(a); \
                 k_fattn_dec2_combine<128, GG><<<gc, 256, lds, c.st>>>(a); return; }
-            FS(4, 1) FS(4, 2) FS(4, 4) FS(16, 1) FS(16, 2) FS(16, 4)
+            FS(2, 1) FS(2, 2) FS(4, 1) FS(4, 2) FS(4, 4) FS(16, 1) FS(16, 2) FS(16, 4)
 #undef FS
         }
         FL(128, 1) FL(128, 2) FL(128, 4) FL(64, 1) FL(64, 2) FL(64, 4)

@@ -8,6 +8,20 @@
 namespace mx {
 
 int g_tune[32] = {0};
+// GGML_MI355X_TUNE="i=v,i=v": the same knobs for processes that load the backend without
+// calling ggml_backend_mi355x_set_tune (the reference libllama in drop-in A/B runs)
+static const bool g_tune_env = [] {
+    if (const char * e = getenv("GGML_MI355X_TUNE")) {
+        for (const char * p = e; *p;) {
+            int i = 0, v = 0, n = 0;
+            if (sscanf(p, "%d=%d%n", &i, &v, &n) != 2) break;
+            if (i >= 0 && i < 32) g_tune[i] = v;
+            p += n;
+            while (*p == ',' || *p == ' ') ++p;
+        }
+    }
+    return true;
+}();
 bool g_gemv2 = getenv("GGML_MI355X_GEMV_V1") == nullptr;
 
 struct G2Args {

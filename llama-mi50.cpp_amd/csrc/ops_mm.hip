@@ -526,7 +526,7 @@ constexpr int MM3_CPR = MM3_BK / 8;             // 16-byte chunks per LDS row
 __device__ __forceinline__ void mmq_tile_xy(const MmqArgs & p, int & bx, int & by) {
     const int gx = (int) gridDim.x, n = gx * (int) gridDim.y;
     int id = (int) blockIdx.x + gx * (int) blockIdx.y;
-    if ((p.dbg & 32) && n % 8 == 0) id = (id % 8) * (n / 8) + id / 8;
+    if (MX_DBG(p.dbg & 32) && n % 8 == 0) id = (id % 8) * (n / 8) + id / 8;
     bx = id % gx; by = id / gx;
 }
 
@@ -548,7 +548,7 @@ __device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, int64
     const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
     const char * wbase = p.w + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
     const _Float16 * xbase = p.x + ch * p.N * p.kp;
-    const int64_t nk = (p.dbg & 16) ? 2 : p.K / MM3_BK;
+    const int64_t nk = MX_DBG(p.dbg & 16) ? 2 : p.K / MM3_BK;
     // this thread's weight unit: half kh (wave-uniform) of row ur's super-block, chunk uc
     const int ur = (tid & 255) >> 2, uc = tid & 3;
 
@@ -569,9 +569,9 @@ __device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, int64
             const int unit = tid + NT * it;
             const int t = unit / MM3_CPR, chn = unit % MM3_CPR;
             const int64_t tok = min(tok0 + t, p.N - 1);
-            ra[it] = *(const uint4 *) (xbase + ((p.dbg & 4) ? 8 * chn : tok * p.kp + k0 + 8 * chn));
+            ra[it] = *(const uint4 *) (xbase + (MX_DBG(p.dbg & 4) ? 8 * chn : tok * p.kp + k0 + 8 * chn));
         }
-        raw_load<QT>(p, wbase, (p.dbg & 1) ? row0 : row0 + ur, (p.dbg & 1) ? 0 : k0 + 128 * kh, uc, rw[0]);
+        raw_load<QT>(p, wbase, MX_DBG(p.dbg & 1) ? row0 : row0 + ur, MX_DBG(p.dbg & 1) ? 0 : k0 + 128 * kh, uc, rw[0]);
     };
     auto store = [&](const uint4 (&ra)[NA], const RawW<QT> (&rw)[1], int64_t kt) {
         const int64_t k0 = min(kt, nk - 1) * MM3_BK;
@@ -581,14 +581,14 @@ __device__ __forceinline__ void mmq3_tile(const MmqArgs & p, int64_t row0, int64
             const int t = unit / MM3_CPR, chn = unit % MM3_CPR;
             lds_a[swzn<MM3_CPR>(t, chn)] = tok0 + t < p.N ? ra[it] : make_uint4(0, 0, 0, 0);
         }
-        if (!(p.dbg & 8)) raw_store<QT, MM3_CPR>(rw[0], (int) (k0 + 128 * kh), row0 + ur < p.M, ur, uc, lds_b, 16 * kh);
+        if (!MX_DBG(p.dbg & 8)) raw_store<QT, MM3_CPR>(rw[0], (int) (k0 + 128 * kh), row0 + ur < p.M, ur, uc, lds_b, 16 * kh);
     };
 
     const int r = lane & 31, hsel = lane >> 5;
     auto mfma_step = [&]() {
 #pragma unroll
         for (int kq = 0; kq < MM3_BK / 2; kq += 16) {
-            if (p.dbg & 2) break;
+            if (MX_DBG(p.dbg & 2)) break;
             const int chn = (kh * (MM3_BK / 2) + kq) / 8 + hsel;
             half8 a[2], b[TM];
 #pragma unroll
@@ -900,7 +900,7 @@ static void mmq_run_ex(OpCtx & c, ggml_tensor * dst, ggml_tensor * out, const gg
     if (res) { p.res = (const float *) res->data; p.r_col = res->nb[1] / 4; }
     p.M = w->ne[1]; p.N = x->ne[1]; p.K = w->ne[0]; p.ne12 = x->ne[2];
     p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
-    p.dbg = g_tune[13];
+    p.dbg = MX_AB_VARIANTS ? g_tune[13] : 0;
     const bool kq = w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
     if (kq && !g_mmq_v1 && p.K % 256 == 0 && mmq4_mul_mat(c, w, x, xa, kp, out, res)) return;
     if (kq && !g_mmq_v1 && p.K % 256 == 0) {
@@ -1089,7 +1089,7 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, 
         return true;
     }
     p.dst = (float *) glu->data; p.d_col = glu->nb[1] / 4;
-    p.M = wg->ne[1]; p.N = x->ne[1]; p.K = wg->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = g_tune[13];
+    p.M = wg->ne[1]; p.N = x->ne[1]; p.K = wg->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = MX_AB_VARIANTS ? g_tune[13] : 0;
     // the down projection reads this output: write its f16 copy too (claimed after the
     // input conversion above, which used the same slot)
     p.h = mmq_act_claim(c, glu->data, glu->ne[0], glu->ne[1], glu->nb[1]);
@@ -1128,7 +1128,7 @@ bool mmq_group_run(OpCtx & c, ggml_tensor * const * mms, int n) {
     MmqArgs p{};
     p.x = mmq_act(c, x, kp); p.kp = kp;
     if (mmq4_group(c, mms, n, p.x, kp)) return true;
-    p.N = x->ne[1]; p.K = x->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = g_tune[13];
+    p.N = x->ne[1]; p.K = x->ne[0]; p.ne12 = 1; p.r2 = 1; p.r3 = 1; p.dbg = MX_AB_VARIANTS ? g_tune[13] : 0;
     MmqSegs sg{};
     sg.n = n;
     sg.tb0[0] = 0;

@@ -332,7 +332,7 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
     auto dma = [&](int i) {
-        if (p.dbg & 4) return;
+        if (MX_DBG(p.dbg & 4)) return;
         const int st = (i % M4_S) * TILE, kc = c0 + i;
 #pragma unroll
         for (int d = 0; d < NDMA; ++d) {
@@ -407,7 +407,7 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
             for (int t = 0; t < TT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], b, acc[t], 0, 0, 0);
         }
     };
-    auto wl = [&](int i, M4W<QT> & rw) { m4_load<QT>(wrow, (p.dbg & 8) ? c0 : c0 + i, h, rw); };
+    auto wl = [&](int i, M4W<QT> & rw) { m4_load<QT>(wrow, MX_DBG(p.dbg & 8) ? c0 : c0 + i, h, rw); };
     M4W<QT> r0, r1, r2;
     // prologue: ring stages 0 .. S-2, weights of chunks 0 and 1
 #pragma unroll
@@ -601,7 +601,7 @@ static void m4_kernel_x(hipStream_t st, const M4Args & a, dim3 g) {
 
 template <int QTA, int QTB, int TT, int EPI>
 static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
-    if constexpr (QTA == QTB && TT == 4 && EPI < 2 && QTA != GGML_TYPE_Q5_K) {
+    if constexpr (MX_AB_VARIANTS && QTA == QTB && TT == 4 && EPI < 2 && QTA != GGML_TYPE_Q5_K) {
         switch (g_tune[31]) {   // timing experiments (X bits above), the prefill GEMM shapes only
             case 1: return m4_kernel_x<QTA, QTB, TT, EPI, 1 | M4_XDEF>(st, a, g);
             case 2: return m4_kernel_x<QTA, QTB, TT, EPI, 2 | (M4_XDEF & 8)>(st, a, g);
@@ -663,7 +663,7 @@ size_t mmq4_scratch(const ggml_tensor * dst) {
 
 template <int EPI>
 static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int nz, int tt) {
-    a.dbg = g_tune[19];
+    a.dbg = MX_AB_VARIANTS ? g_tune[19] : 0;
     a.trace = mx_trace_slot(3);
     a.trace_blk = mx_trace_blocks();
     const int nk = a.K / M4_KC;

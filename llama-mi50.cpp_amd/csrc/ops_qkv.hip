@@ -103,8 +103,8 @@ __global__ __launch_bounds__(BAL ? 448 : 256) void k_qkv_rope_store(QkvArgs p) {
     const float v = acc[0];   // row sum: in lane sub == L-1 (every lane of the row for L <= 16)
     const float pv = __shfl_xor(v, LA, 64);
     if (sub != L - 1 || !valid) return;
-    if (p.xs.dbg & 4) { if (m == 0) p.q_out[row] = v; return; }
-    if ((p.xs.dbg & 8) && m > 0) return;
+    if (MX_DBG(p.xs.dbg & 4)) { if (m == 0) p.q_out[row] = v; return; }
+    if (MX_DBG(p.xs.dbg & 8) && m > 0) return;
     if (m == 2) {
         if (p.vq8f) { p.vq8f[row] = v; return; }
         const uint16_t h = f2h(v);
@@ -499,7 +499,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     // default geometry, the norm / f32 / q8 sources a 448-thread block stages in one pass.
     // Opt-in (g_tune[30] = 1): measured 7.12 vs 6.71 us alone (opbench attn_in) and within
     // the noise in tg128 (584 vs 582 tok/s), profiles/r03/qkv_balanced_ab.txt
-    const bool bal = g_tune[30] == 1 && cfg == 5 && wq->ne[1] % 16 == 0 && wq->ne[1] == 4 * wk->ne[1] && wq->ne[1] == 4 * wv->ne[1] &&
+    const bool bal = MX_AB_VARIANTS && g_tune[30] == 1 && cfg == 5 && wq->ne[1] % 16 == 0 && wq->ne[1] == 4 * wk->ne[1] && wq->ne[1] == 4 * wv->ne[1] &&
                      p.K <= 16 * 448 && (mode == XS_NORM || mode == XS_Q8 || mode == XS_F32);
     if (bal) {
         void (*kb)(QkvArgs) = nullptr;

@@ -653,6 +653,8 @@ def test_attn_oproj_decode_chain(pkg, backend, orc, n_kv, H, Hkv, M, mask_tail, 
         return [y], [(tq, q), (tk, k), (tv, v), (tm, m16), (tw, w), (tr, r)]
 
     lib = pkg._lib.load()
+    if not lib.ggml_backend_mi355x_ab_variants():
+        pytest.skip("ops_attn_o.hip is an A/B experiment: built only with -DMX_AB_VARIANTS=1 (scripts/build_variants.sh)")
     lib.ggml_backend_mi355x_set_tune(27, 16 if v1 else 64)
     try:
         backend.klog(True)
