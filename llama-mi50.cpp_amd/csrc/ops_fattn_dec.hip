@@ -94,7 +94,7 @@ __device__ __forceinline__ float kr_max(float v) {
 // (the looping split form paid one memory round trip per 64-key chunk: 34.5 us at 16k
 // keys), any number of splits; the (O, max, sum) partials are merged by
 // k_fattn_dec2_combine, a parallel second launch (one workgroup per query head).
-template <int D, int G, int NW, bool KQ = false, int NI = FD_NI, bool LONG = false>
+template <int D, int G, int NW, bool KQ = false, int NI = FD_NI, bool LONG = false, int CPW = 1>
 __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     constexpr int NT = 64 * NW;
     constexpr int LPK = D / 8;            // lanes per key row
@@ -190,59 +190,58 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[h][i] = 0.f;
     }
-    for (int ci = 0; ci < cpb; ++ci) {
-        const int ch = split * cpb + ci;
-        if (ch >= nch) break;                                 // workgroup-uniform
+    // one chunk's loads, unconditional (clamped: a load under a branch costs a wait at
+    // the join): mask, K rows, V rows — coalesced, LPK lanes per row
+    struct Chunk { uint16_t mraw[NI]; uint4 kr[NI], vr[NI]; uint16_t kd[NI], vd[NI]; };
+    auto load = [&](int ch, Chunk & b) {
         const int key0 = ch * CS + wave * KPW + kq;
-        // every load of the chunk first, unconditional (clamped: a load under a branch
-        // costs a wait at the join): mask, K rows, V rows — coalesced, LPK lanes per row
-        uint16_t mraw[NI];
-        uint4 kr[NI], vr[NI];
-        uint16_t kd[NI], vd[NI];                              // KQ: block scales
 #pragma unroll
-        for (int t = 0; t < NI; ++t) mraw[t] = mrow[min(key0 + t * KPI, p.n_kv - 1)];
+        for (int t = 0; t < NI; ++t) b.mraw[t] = mrow[min(key0 + t * KPI, p.n_kv - 1)];
         if constexpr (KQ) {
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
                 const size_t ko = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1;
                 const uint2 w = ldu8(kb + ko);
-                kr[t] = make_uint4(w.x, w.y, 0, 0);
-                kd[t] = ld_u16(kb - lofs + dofs + ko);
+                b.kr[t] = make_uint4(w.x, w.y, 0, 0);
+                b.kd[t] = ld_u16(kb - lofs + dofs + ko);
             }
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
                 const size_t vo = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1;
                 const uint2 w = ldu8(vb + vo);
-                vr[t] = make_uint4(w.x, w.y, 0, 0);
-                vd[t] = ld_u16(vb - lofs + dofs + vo);
+                b.vr[t] = make_uint4(w.x, w.y, 0, 0);
+                b.vd[t] = ld_u16(vb - lofs + dofs + vo);
             }
         } else {
 #pragma unroll
-            for (int t = 0; t < NI; ++t) kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
+            for (int t = 0; t < NI; ++t) b.kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
 #pragma unroll
-            for (int t = 0; t < NI; ++t) vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
+            for (int t = 0; t < NI; ++t) b.vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        if (ci == 0) MX_TRACE(tr, 1);
+    };
+    // scores and the online softmax of one loaded chunk (keys past n_kv count as masked:
+    // a chunk wholly past the cache contributes nothing)
+    auto process = [&](int ch, const Chunk & b, bool first) {
+        const int key0 = ch * CS + wave * KPW + kq;
         float mk[NI];
 #pragma unroll
-        for (int t = 0; t < NI; ++t) mk[t] = key0 + t * KPI < p.n_kv ? (p.mask ? h2f(mraw[t]) : 0.f) : -INFINITY;
+        for (int t = 0; t < NI; ++t) mk[t] = key0 + t * KPI < p.n_kv ? (p.mask ? h2f(b.mraw[t]) : 0.f) : -INFINITY;
         // scores: q·k over the row's LPK lanes (DPP), one per (head, key) in every lane of the row
         float s[G][NI];
-        if (ci == 0) { asm volatile("" :: "v"(kr[0].x), "v"(vr[0].x), "v"(vr[NI - 1].w)); MX_TRACE(tr, 2); }
+        if (first) { asm volatile("" :: "v"(b.kr[0].x), "v"(b.vr[0].x), "v"(b.vr[NI - 1].w)); MX_TRACE(tr, 2); }
 #pragma unroll
         for (int t = 0; t < NI; ++t) {
 #pragma unroll
             for (int h = 0; h < G; ++h) {
                 float acc;
                 if constexpr (KQ) {
-                    const int si = dot4_i8((int) kr[t].y, qq8[h][1], dot4_i8((int) kr[t].x, qq8[h][0], 0));
-                    acc = (float) si * (qd[h] * h2f(kd[t]));
+                    const int si = dot4_i8((int) b.kr[t].y, qq8[h][1], dot4_i8((int) b.kr[t].x, qq8[h][0], 0));
+                    acc = (float) si * (qd[h] * h2f(b.kd[t]));
                 } else {
-                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[h][0], 0.f, false);
-                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[h][1], acc, false);
-                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[h][2], acc, false);
-                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[h][3], acc, false);
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, b.kr[t].x), qh[h][0], 0.f, false);
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, b.kr[t].y), qh[h][1], acc, false);
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, b.kr[t].z), qh[h][2], acc, false);
+                    acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, b.kr[t].w), qh[h][3], acc, false);
                 }
                 acc = dpp_sum_group<LPK>(acc);
                 // log2 domain (v_exp_f32 below): s = (q·k·scale + mask) · log2(e)
@@ -269,13 +268,13 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
                 if constexpr (KQ) {
-                    const float dv = h2f(vd[t]);
-                    const uint32_t vw[2] = {vr[t].x, vr[t].y};
+                    const float dv = h2f(b.vd[t]);
+                    const uint32_t vw[2] = {b.vr[t].x, b.vr[t].y};
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
                         o[h][i] += pr[t] * (dv * (float) (int8_t) ((vw[i >> 2] >> (8 * (i & 3))) & 0xFF));
                 } else {
-                    const uint32_t vw[4] = {vr[t].x, vr[t].y, vr[t].z, vr[t].w};
+                    const uint32_t vw[4] = {b.vr[t].x, b.vr[t].y, b.vr[t].z, b.vr[t].w};
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         o[h][2 * i] += pr[t] * h2f((uint16_t) (vw[i] & 0xFFFF));
@@ -283,6 +282,32 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
                     }
                 }
             }
+        }
+    };
+    if constexpr (LONG && CPW > 1) {
+        // round 4: CPW chunks per workgroup, double-buffered — chunk c+1's loads are in
+        // flight while chunk c computes (the one-chunk form left every workgroup's compute
+        // exposed after its single round trip, and 4x the splits for the combine)
+        Chunk bf[2];
+        load(min(split * CPW, nch - 1), bf[0]);
+#pragma unroll
+        for (int ci = 0; ci < CPW; ++ci) {
+            // (compiler memory barrier: the next chunk's loads are issued here, not hoisted
+            // above the previous chunk's processing — two register buffers, not CPW)
+            asm volatile("" ::: "memory");
+            if (ci + 1 < CPW) load(min(split * CPW + ci + 1, nch - 1), bf[(ci + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            process(split * CPW + ci, bf[ci & 1], ci == 0);
+        }
+    } else {
+        for (int ci = 0; ci < cpb; ++ci) {
+            const int ch = split * cpb + ci;
+            if (ch >= nch) break;                                 // workgroup-uniform
+            Chunk b;
+            load(ch, b);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ci == 0) MX_TRACE(tr, 1);
+            process(ch, b, ci == 0);
         }
     }
 #pragma unroll
@@ -467,10 +492,10 @@ bool fa_dec2_ok(const ggml_tensor * dst) {
 // LONG: 4-wave workgroups over min(Gt, 2) query heads (K/V read once per workgroup for
 // those heads, from L2 by the group's other workgroup), 8 key rows per lane per chunk —
 // 128 keys (64 KB of f16 K/V at D 128) in flight per workgroup, one chunk each.
-struct FdCfg { int G, NW, nsplit; bool lng; };
+struct FdCfg { int G, NW, nsplit; bool lng; int cpw = 1; };
 constexpr int FD_LONG_NI = 8;
 constexpr int FD_LONG_MAXSPLIT = 32768;   // the combine's split weights in LDS (128 KB): 4M keys at D 128
-static FdCfg fd_cfg(int D, int Gt, int64_t n_kv) {
+static FdCfg fd_cfg(int D, int Gt, int64_t n_kv, int64_t rows) {   // rows = Hkv x n_q x sequences
     const int cs16 = 16 * FD_NI * (64 / (D / 8)), cs4 = 4 * FD_NI * (64 / (D / 8));
     // g_tune[1] = NI (2 / 4, experiment): short caches too take the LONG geometry — chunks of
     // 4 NI 64/(D/8) keys, one per workgroup, G = g_tune[29] (default 1) heads, plus the combine
@@ -486,13 +511,22 @@ static FdCfg fd_cfg(int D, int Gt, int64_t n_kv) {
     // vs 18.5; profiles/r03/opbench_fa_long_sweep.txt)
     const int g = D == 128 && g_tune[29] ? std::min(g_tune[29], Gt) : std::min(Gt, 2);
     const int csl = 4 * ni * (64 / (D / 8));
-    return {g, 4, (int) mx_ceil_div(n_kv, csl), true};
+    const int64_t nch = mx_ceil_div(n_kv, csl);
+    // round 4: CPW chunks per workgroup (double-buffered) once one chunk each would give more
+    // than ~512 workgroups (two per CU): 16k keys at D 128 = 128 chunks x 16 slots -> CPW 4.
+    // g_tune[2] forces CPW (1 / 2 / 4 / 8)
+    int cpw = 1;
+    if (g_tune[2] == 1 || g_tune[2] == 2 || g_tune[2] == 4 || g_tune[2] == 8) cpw = g_tune[2];
+    else if (ni == FD_LONG_NI && g <= 2)
+        while (cpw < 4 && mx_ceil_div(nch, 2 * cpw) * rows * (Gt / g) >= 512) cpw *= 2;   // (CPW 8 spills)
+    if (ni != FD_LONG_NI || g > 2) cpw = 1;                   // (instantiated for the default NI, G <= 2)
+    return {g, 4, (int) mx_ceil_div(nch, cpw), true, cpw};
 }
 
 size_t fa_dec2_scratch(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0], * k = dst->src[1];
     const int64_t D = k->ne[0];
-    const FdCfg f = fd_cfg((int) D, (int) (q->ne[2] / k->ne[2]), k->ne[1]);
+    const FdCfg f = fd_cfg((int) D, (int) (q->ne[2] / k->ne[2]), k->ne[1], k->ne[2] * q->ne[1] * q->ne[3]);
     return (size_t) (q->ne[1] * q->ne[3] * q->ne[2]) * (f.lng ? f.nsplit : std::min(f.nsplit, FD_MAXSPLIT)) * (D + 2) * sizeof(float) + 256;
 }
 
@@ -509,7 +543,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     a.ns_kv = (int) k->ne[3];
     a.scale = mx_op_param<float>(dst, 0);
     const int D = (int) k->ne[0], Gt = a.H / a.Hkv;
-    const FdCfg f = fd_cfg(D, Gt, a.n_kv);
+    const FdCfg f = fd_cfg(D, Gt, a.n_kv, (int64_t) a.Hkv * a.n_q * q->ne[3]);
     MX_ASSERT(f.lng ? f.nsplit <= 65535 : f.nsplit <= FD_MAXSPLIT);
     a.nsplit = f.nsplit;
     a.part = (float *) c.scratch->take(fa_dec2_scratch(dst));
@@ -529,14 +563,16 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     } else a.pf_n = 0;
     const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
     const bool kq = k->type == GGML_TYPE_Q8_0;
-    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u long=%d", D, f.G, f.NW, f.nsplit, a.n_kv, a.H, a.Hkv,
-            (int) kq, pf_rows, (int) f.lng);
+    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u long=%d cpw=%d", D, f.G, f.NW, f.nsplit, a.n_kv,
+            a.H, a.Hkv, (int) kq, pf_rows, (int) f.lng, f.cpw);
     if (f.lng) {
         const unsigned gc = gx * (unsigned) f.G;                     // one combine workgroup per query head
         const size_t lds = (size_t) f.nsplit * sizeof(float);
-#define FL(DD, GG) if (D == DD && f.G == GG) { \
-            if (kq) k_fattn_dec2<DD, GG, 4, true, FD_LONG_NI, true><<<grid, 256, 0, c.st>>>(a); \
-            else k_fattn_dec2<DD, GG, 4, false, FD_LONG_NI, true><<<grid, 256, 0, c.st>>>(a); \
+#define FLC(DD, GG, CP) if (f.cpw == CP) { \
+            if (kq) k_fattn_dec2<DD, GG, 4, true, FD_LONG_NI, true, CP><<<grid, 256, 0, c.st>>>(a); \
+            else k_fattn_dec2<DD, GG, 4, false, FD_LONG_NI, true, CP><<<grid, 256, 0, c.st>>>(a); }
+#define FLW(DD, GG, CPWS) if (D == DD && f.G == GG) { \
+            CPWS \
             static const bool attr = [] { HIP_CHECK(hipFuncSetAttribute((const void *) k_fattn_dec2_combine<DD, GG>, \
                 hipFuncAttributeMaxDynamicSharedMemorySize, FD_LONG_MAXSPLIT * (int) sizeof(float))); return true; }(); \
             (void) attr; \
@@ -551,8 +587,12 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
             FS(2, 1) FS(2, 2) FS(4, 1) FS(4, 2) FS(4, 4) FS(16, 1) FS(16, 2) FS(16, 4)
 #undef FS
         }
-        FL(128, 1) FL(128, 2) FL(128, 4) FL(64, 1) FL(64, 2) FL(64, 4)
-#undef FL
+#define CPW4(DD, GG) FLC(DD, GG, 2) else FLC(DD, GG, 4) else FLC(DD, GG, 8) else FLC(DD, GG, 1)
+        FLW(128, 1, CPW4(128, 1)) FLW(128, 2, CPW4(128, 2)) FLW(128, 4, FLC(128, 4, 1))
+        FLW(64, 1, CPW4(64, 1)) FLW(64, 2, CPW4(64, 2)) FLW(64, 4, FLC(64, 4, 1))
+#undef CPW4
+#undef FLW
+#undef FLC
         MX_ABORT("fattn dec2 long D=%d G=%d", D, f.G);
     }
 #define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { \

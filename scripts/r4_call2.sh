@@ -11,3 +11,5 @@ timeout -k 10 600 bash scripts/r4_attrib.sh > /dev/null 2>&1; echo "attrib rc=$?
 timeout -k 10 600 python bench.py > gpurun_out/r4_bench1.json 2> gpurun_out/r4_bench1.err; echo "bench rc=$?"; tail -c 1500 gpurun_out/r4_bench1.json
 OUT=gpurun_out/fa256 timeout -k 10 300 bash scripts/opbench.sh --only fa_256 --ab 0=0 1=4 1=2 1=4,29=2 1=2,29=2 0=0 > gpurun_out/r4_fa256_ab.txt 2>&1; echo "fa ab rc=$?"; grep -E "==|fattn" gpurun_out/fa256/report.txt | head -40
 AB="0=0 1=4 1=2 1=4,29=2" PASSES=2 timeout -k 10 400 bash scripts/ab_dropin.sh > gpurun_out/r4_ab_dropin_fa.txt 2>&1; echo "dropin ab rc=$?"; cat gpurun_out/r4_ab_dropin_fa.txt
+OUT=gpurun_out/falong timeout -k 10 300 bash scripts/opbench.sh --only fa_4096 fa_16384 fa_32768 --ab 2=1 0=0 2=2 2=4 2=8 2=1 > gpurun_out/r4_falong_ab.txt 2>&1; echo "fa long ab rc=$?"; grep -E "==|fattn" gpurun_out/falong/report.txt | head -60
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_ops_gpu.py -k "flash_attn" > gpurun_out/r4_fa_tests.log 2>&1; echo "fa tests rc=$?"; tail -3 gpurun_out/r4_fa_tests.log
