@@ -77,6 +77,7 @@ struct ActCacheEntry {
 
 struct GraphCache {
     std::vector<uint64_t> key;    // signature of the captured cgraph
+    unsigned buf_gen = 0;         // g_buf_gen at capture (a row split's slice streams' buffers)
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     int hits = 0;
@@ -131,6 +132,7 @@ struct Stream {
     int32_t rope_params[11] = {};
     bool use_graphs = true;
     bool use_fusion = true;
+    bool split_graph = false;        // the graph holds row-split weights: only fusions without a split matrix
     std::string name;
     ggml_backend backend{};
     ggml_abort_callback abort_cb = nullptr;

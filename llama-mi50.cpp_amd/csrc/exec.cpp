@@ -14,6 +14,7 @@
 #include "gemv.h"
 
 #include <algorithm>
+#include <atomic>
 #include <unordered_map>
 
 namespace mx {
@@ -101,6 +102,7 @@ static bool t_overlaps(const ggml_tensor * a, const ggml_tensor * b) {
     return a && b && a->data && b->data && overlaps(a->data, mx_nbytes(a), b->data, mx_nbytes(b));
 }
 bool t_overlaps_ext(const ggml_tensor * a, const ggml_tensor * b) { return t_overlaps(a, b); }
+bool split_graph_capturable(int main_hip);   // split.cpp
 
 // General output-overlap guard of a fused launch (round 4). ggml-alloc hands a node the
 // memory of tensors that died earlier in node order (and runs ADD/MUL/SOFT_MAX/ROPE in
@@ -298,8 +300,7 @@ static int try_fuse_mm_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
         const ggml_tensor * w = mul->op == GGML_OP_MUL ? (mul->src[0] == norm ? mul->src[1] : (mul->src[1] == norm ? mul->src[0] : nullptr)) : nullptr;
         if (norm->op == GGML_OP_RMS_NORM && norm->src[0] == add && w && uses[norm] == 1 && mx_are_same_shape(mul, norm) &&
             !((norm->flags | mul->flags) & GGML_TENSOR_FLAG_OUTPUT)) {
-            act_cache_invalidate(c.s, mul);
-            if (mm_add_rms_norm(c, mm, res, add, norm, w, mul)) return 4;
+            if (mm_add_rms_norm(c, mm, res, add, norm, w, mul)) return 4;   // (invalidates mul's cached forms itself)
         }
     }
     return mmq_fused_add(c, mm, res, add) ? 2 : 0;
@@ -470,6 +471,11 @@ static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q, bo
     for (int r = 1; r < s->pf_n; ++r) if (s->pf_take[r] != s->gpf_off) s->gpf_node = nullptr;   // one offset for all
 }
 
+// bumped whenever any stream's scratch / activation buffers move: a captured graph whose
+// row-split slices ran on other streams (their buffers are not the capturing stream's)
+// must not replay over freed memory
+static std::atomic<unsigned> g_buf_gen{0};
+
 static void run_nodes(Stream * s, ggml_cgraph * g) {
     OpCtx c{s, s->stream, &s->scratch};
     static thread_local UseMap uses;
@@ -494,7 +500,11 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i, n->src[0]->ne[1], false);
         else if (n->op == GGML_OP_MUL_MAT && n->src[0]->type == GGML_TYPE_F16 && n->src[1]->ne[1] == 1) fa_prefetch_plan(s, g, i, 1, true);
         s->gpf_armed = s->gpf_node && n == s->gpf_node;
-        if (s->use_fusion) {
+        if (s->use_fusion && s->split_graph) {
+            // row-split weights: the fusions that touch no MUL_MAT (split or not: a split
+            // slice runs on its device's own stream, which no deferred norm reaches)
+            if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
+        } else if (s->use_fusion) {
             const int i0 = i;
             if (n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }
             if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
@@ -544,6 +554,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
 // grow a stream's scratch arena, activation ring and f16 slots to the given sizes
 // (never inside a capture)
 static void stream_reserve(Stream * s, size_t need, size_t slot, size_t f16need) {
+    if (slot > s->act_slot || f16need > s->f16.cap || need > s->scratch.cap) ++g_buf_gen;
     if (slot > s->act_slot) {
         HIP_CHECK(hipStreamSynchronize(s->stream));
         if (s->act.base) HIP_CHECK(hipFree(s->act.base));
@@ -594,13 +605,14 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         same = graph_signature_same(g, gc.key);   // gc.key now holds g's signature
         const auto t1 = std::chrono::steady_clock::now();
         s->us_sig += std::chrono::duration<double, std::micro>(t1 - t0).count();
-        if (gc.exec && same) {
+        if (gc.exec && same && gc.buf_gen == g_buf_gen.load()) {
             HIP_CHECK(hipGraphLaunch(gc.exec, s->stream));
             s->us_launch += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
             s->n_graph_replay++;
             return;
         }
-        if (!same) {   // a different graph: the capture of the previous one is stale
+        if (!same || (gc.exec && gc.buf_gen != g_buf_gen.load())) {   // a different graph (or moved buffers): the capture is stale
+            same = false;
             gc.hits = 0;
             if (gc.exec) { HIP_CHECK(hipGraphExecDestroy(gc.exec)); gc.exec = nullptr; }
             if (gc.graph) { HIP_CHECK(hipGraphDestroy(gc.graph)); gc.graph = nullptr; }
@@ -619,26 +631,29 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     }
     stream_reserve(s, need, slot, f16need);   // a reallocation clears gc.key: no capture of old buffers replays
 
-    // row-split weights (split.cpp): every device works on the node, which no single-stream
-    // capture can hold, and the fusions assume one device — eager and unfused
+    // row-split weights (split.cpp): every device works on the node, the slices fork off
+    // onto the devices' own streams and join back by events; only the fusions without a
+    // MUL_MAT apply. Captured like any graph when the slice devices are this GPU (the fork /
+    // join events pull the slice streams into the capture), eager across GPUs.
     bool split = false;
     for (int i = 0; i < g->n_nodes && !split; ++i) split = g->nodes[i]->op == GGML_OP_MUL_MAT && tensor_is_split(g->nodes[i]->src[0]);
-    if (split) {
+    s->split_graph = split;
+    if (split && !split_graph_capturable(s->device)) {
         gc.key.clear();   // never captured: the next sighting must not count as a repeat
-        const bool f = s->use_fusion;
-        s->use_fusion = false;
         run_nodes(s, g);
-        s->use_fusion = f;
+        s->split_graph = false;
         return;
     }
-    if (!graphs || !same || gc.key.empty()) { run_nodes(s, g); return; }   // first sighting: eager
+    if (!graphs || !same || gc.key.empty()) { run_nodes(s, g); s->split_graph = false; return; }   // first sighting: eager
     // second sighting of the same signature: capture and launch
     HIP_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
     run_nodes(s, g);
+    s->split_graph = false;
     hipGraph_t graph = nullptr;
     HIP_CHECK(hipStreamEndCapture(s->stream, &graph));
     HIP_CHECK(hipGraphInstantiate(&gc.exec, graph, nullptr, nullptr, 0));
     gc.graph = graph;
+    gc.buf_gen = g_buf_gen.load();
     HIP_CHECK(hipGraphLaunch(gc.exec, s->stream));
 }
 

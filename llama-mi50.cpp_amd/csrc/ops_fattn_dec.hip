@@ -512,13 +512,15 @@ static FdCfg fd_cfg(int D, int Gt, int64_t n_kv, int64_t rows) {   // rows = Hkv
     const int g = D == 128 && g_tune[29] ? std::min(g_tune[29], Gt) : std::min(Gt, 2);
     const int csl = 4 * ni * (64 / (D / 8));
     const int64_t nch = mx_ceil_div(n_kv, csl);
-    // round 4: CPW chunks per workgroup (double-buffered) once one chunk each would give more
-    // than ~512 workgroups (two per CU): 16k keys at D 128 = 128 chunks x 16 slots -> CPW 4.
-    // g_tune[2] forces CPW (1 / 2 / 4 / 8)
+    // round 4 experiment, g_tune[2] = CPW (2 / 4 / 8): CPW chunks per workgroup, double-
+    // buffered (chunk c+1's loads in flight while chunk c computes). Measured slower than one
+    // chunk per workgroup at every length (opbench, profiles/r04/fa_long_cpw_ab.txt: 16k keys
+    // 17.4 / 19.3 / 21.5 / 47 us for CPW 1 / 2 / 4 / 8; drop-in tg128 at depth 16384 354 -> 319
+    // tok/s with CPW 4): with all chunks of all workgroups resident at once the loads are
+    // already in flight together, and a second register buffer halves the waves per SIMD.
     int cpw = 1;
-    if (g_tune[2] == 1 || g_tune[2] == 2 || g_tune[2] == 4 || g_tune[2] == 8) cpw = g_tune[2];
-    else if (ni == FD_LONG_NI && g <= 2)
-        while (cpw < 4 && mx_ceil_div(nch, 2 * cpw) * rows * (Gt / g) >= 512) cpw *= 2;   // (CPW 8 spills)
+    (void) rows;
+    if (g_tune[2] == 2 || g_tune[2] == 4 || g_tune[2] == 8) cpw = g_tune[2];
     if (ni != FD_LONG_NI || g > 2) cpw = 1;                   // (instantiated for the default NI, G <= 2)
     return {g, 4, (int) mx_ceil_div(nch, cpw), true, cpw};
 }

@@ -1032,8 +1032,15 @@ bool mm_add_rms_norm(OpCtx & c, ggml_tensor * mm, const ggml_tensor * res, ggml_
     if (!rows16(add) || !rows16(res) || !rows16(mul) || !mx_are_same_shape(add, mm) || N > INT32_MAX) return false;
     if (n % 4 || n < 128 || n > 4 * 256 * 8) return false;
     if (w->type != GGML_TYPE_F32 || mx_nelements(w) != n || !mx_is_contiguous(w) || (uintptr_t) w->data % 16) return false;
-    // the norm rows are written while other rows' sums are still being read
-    if (t_overlaps_ext(mul, add) || t_overlaps_ext(mul, res) || t_overlaps_ext(mul, w) || t_overlaps_ext(mul, x)) return false;
+    // The norm rows are written while other rows' sums are still being read: mul must not
+    // overlap add or w, and res only exactly (the workgroup of row t reads res row t before
+    // it writes mul row t — block_sum's barriers). x is consumed by the GEMM (through its f16
+    // copy) before this pass starts, so mul may reuse x's memory: libllama's allocator places
+    // the norm there (x, the SwiGLU or attention output, dies at the GEMM) — refusing that
+    // overlap had kept the fusion off in every drop-in prefill (r03 drop-in pp512 profile:
+    // 62 k_mmq4_reduce + 62 k_rms_norm_v4 launches per ubatch, profiles/r04/).
+    const bool mul_on_res = mul->data == res->data && mul->nb[1] == res->nb[1];
+    if (t_overlaps_ext(mul, add) || (!mul_on_res && t_overlaps_ext(mul, res)) || t_overlaps_ext(mul, w)) return false;
     if (add->data != res->data && t_overlaps_ext(add, res)) return false;
     // every refusal comes before the deferred-norm guards act (mmq4_scratch sizes the arena
     // for this product and the split-K planes together)
@@ -1053,6 +1060,7 @@ bool mm_add_rms_norm(OpCtx & c, ggml_tensor * mm, const ggml_tensor * res, ggml_
     g_m4_split = &sp;
     mmq_run_ex(c, mm, &prod, nullptr);
     g_m4_split = nullptr;
+    act_cache_invalidate(c.s, mul);   // (after the GEMM: mul may lie over x, whose f16 copy it read)
     const float eps = mx_op_param<float>(norm, 0);
     _Float16 * h = mmq_act_claim(c, mul->data, n, N, mul->nb[1]);
     const int vpt = (int) mx_ceil_div(n / 4, 256);

@@ -11,10 +11,12 @@
 //
 // MI355X form: one process drives all devices (as the reference does for -sm row); each
 // device runs its slice with the same kernels as an unsplit MUL_MAT (decode GEMV, prefill
-// GEMM) on an auxiliary stream of its own; src1 goes to the devices by peer copy over
-// xGMI (peer access is enabled between all pairs at registry init), the slices come back
-// by 2D peer copies, events order everything against the main stream. Split graphs run
-// eagerly and unfused (a capture cannot span devices).
+// GEMM) on an auxiliary stream of its own, reading src1 where it lies on the main device and
+// writing its rows of dst there directly (peer access over xGMI is enabled between all
+// pairs at registry init; without it: peer copies in and out); events fork the slices off
+// the main stream and join them back. Graphs with split weights keep the fusions that
+// involve no split matrix, and are captured into one hipGraph when the slice devices are
+// the main GPU (virtual devices), eager otherwise (split_graph_capturable).
 // GGML_MI355X_VIRTUAL_DEVICES=N exposes the GPUs N times over (tests: a row split over
 // two logical devices of one MI355X exercises every path but the xGMI link itself).
 #include "backend.h"
@@ -164,17 +166,19 @@ ggml_backend_buffer_type_t split_buffer_type(int main_device, const float * tens
 }
 
 // ---- MUL_MAT with a split src0
-// Staging buffers and events per (main device, slice device): a split buffer type with
-// another main device, or a second context, gets state created on its own devices.
+// Staging buffers and events per (main stream, slice device): two contexts on the same main
+// device (two main streams) never share a slice's staging buffers or events (a
+// second context's peer copy could overwrite the no-peer gather buffer before the first
+// one's scatter had read it).
 struct SliceState {
-    void * x = nullptr; size_t xcap = 0;        // src1 copy on the slice device
-    void * y = nullptr; size_t ycap = 0;        // the slice's partial dst on the slice device
+    void * x = nullptr; size_t xcap = 0;        // no-peer path: src1 copy on the slice device
+    void * y = nullptr; size_t ycap = 0;        // no-peer path: the slice's partial dst there
     void * g = nullptr; size_t gcap = 0;        // no-peer gather: the partial dst staged on main
     hipEvent_t ev_main = nullptr;               // main stream -> slice stream (created on main)
     hipEvent_t ev_done = nullptr;               // slice stream -> main stream (created on slice)
 };
 static std::mutex g_split_mu;
-static std::map<std::pair<int, int>, SliceState> g_slices;   // (main logical, slice logical)
+static std::map<std::pair<const Stream *, int>, SliceState> g_slices;   // (main stream, slice logical)
 
 static void * grow(void *& p, size_t & cap, int hip, size_t bytes) {
     if (bytes > cap) {
@@ -186,8 +190,8 @@ static void * grow(void *& p, size_t & cap, int hip, size_t bytes) {
     return p;
 }
 
-static SliceState & slice_state(int main_l, int d) {
-    SliceState & st = g_slices[{main_l, d}];
+static SliceState & slice_state(const Stream * main, int main_l, int d) {
+    SliceState & st = g_slices[{main, d}];
     if (!st.ev_main) {
         HIP_CHECK(hipSetDevice(mx_dev_hip(main_l)));
         HIP_CHECK(hipEventCreateWithFlags(&st.ev_main, hipEventDisableTiming));
@@ -195,6 +199,20 @@ static SliceState & slice_state(int main_l, int d) {
         HIP_CHECK(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
     }
     return st;
+}
+
+// A split graph may be captured into one hipGraph (exec.cpp) when every slice device is
+// the main device's GPU (virtual devices): the fork / join events make the slice streams
+// part of the capture. Across GPUs a capture would have to span devices, which this
+// backend does not rely on: those graphs run eagerly. GGML_MI355X_SPLIT_GRAPHS=0 turns
+// the capture off, =2 tries it across GPUs as well (experiment).
+bool split_graph_capturable(int main_hip) {
+    static const int mode = [] { const char * v = getenv("GGML_MI355X_SPLIT_GRAPHS"); return v ? atoi(v) : 1; }();
+    if (mode == 0) return false;
+    if (mode == 2) return true;
+    for (int d = 0; d < mx_dev_count(); ++d)
+        if (mx_dev_hip(d) != main_hip) return false;
+    return true;
 }
 
 // GGML_MI355X_FORCE_PEER=1 (tests): take the cross-device copy branches even when two
@@ -224,47 +242,69 @@ void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) {
     for (int d = 0; d < mx_dev_count(); ++d) {
         const int64_t rows = e->hi[d] - e->lo[d];
         if (rows == 0) continue;
-        SliceState & st = slice_state(main_l, d);
-        Stream * ds = mx_aux_stream(d);
-        const int hip = ds->device;
+        SliceState & st = slice_state(c.s, main_l, d);
+        const int hip = mx_dev_hip(d);
         const bool cross = hip != main_hip || force;
-        const bool direct = !cross || mx_peer_enabled(hip, main_hip);   // slice device writes main's dst itself
-        HIP_CHECK(hipSetDevice(main_hip));
-        HIP_CHECK(hipEventRecord(st.ev_main, c.st));
-        HIP_CHECK(hipSetDevice(hip));
-        HIP_CHECK(hipStreamWaitEvent(ds->stream, st.ev_main, 0));
-        // the slice's operands on device d: src1 by peer copy, the partial dst
-        void * xd = grow(st.x, st.xcap, hip, xb);
-        void * yd = grow(st.y, st.ycap, hip, (size_t) rows * N * 4);
-        HIP_CHECK(hipSetDevice(hip));
-        if (!cross) HIP_CHECK(hipMemcpyAsync(xd, x->data, xb, hipMemcpyDeviceToDevice, ds->stream));
-        else HIP_CHECK(hipMemcpyPeerAsync(xd, hip, x->data, main_hip, xb, ds->stream));
+        const bool direct = !cross || mx_peer_enabled(hip, main_hip);   // slice device reaches main's memory itself
+        // a slice on the main GPU itself (virtual devices) runs on the main stream: no fork /
+        // join (each is a cross-queue barrier in a captured graph); other GPUs' slices (and
+        // GGML_MI355X_FORCE_PEER runs) fork onto the slice device's stream
+        const bool local = !cross && direct;
+        Stream * ds = local ? c.s : mx_aux_stream(d);
+        if (!local) {
+            HIP_CHECK(hipSetDevice(main_hip));
+            HIP_CHECK(hipEventRecord(st.ev_main, c.st));
+            HIP_CHECK(hipSetDevice(hip));
+            HIP_CHECK(hipStreamWaitEvent(ds->stream, st.ev_main, 0));
+        }
         ggml_tensor ws = *w, xs = *x, ys = *dst;
         ws.ne[1] = rows; ws.nb[2] = ws.nb[3] = ws.nb[1] * rows; ws.data = e->data[d]; ws.buffer = nullptr; ws.extra = nullptr;
         ws.view_src = nullptr;
-        xs.data = xd; xs.buffer = nullptr; xs.view_src = nullptr;
-        ys.ne[0] = rows; ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[1] * ys.ne[1]; ys.nb[3] = ys.nb[2] * ys.ne[2];
-        ys.data = yd; ys.buffer = nullptr; ys.view_src = nullptr;
+        xs.buffer = nullptr; xs.view_src = nullptr;
+        ys.ne[0] = rows; ys.buffer = nullptr; ys.view_src = nullptr;
         ys.src[0] = &ws; ys.src[1] = &xs;
+        void * yd = nullptr;
+        if (direct) {
+            // round 4: the slice kernel reads src1 where it lies and writes its rows of every
+            // column straight into dst (over xGMI when the devices differ: peer access is on
+            // between them) — no staging copies, one kernel per device and matrix
+            ys.data = (char *) dst->data + e->lo[d] * 4;
+            if (N == 1) { ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[3] = ys.nb[1]; }   // one column: contiguous
+        } else {
+            // no peer access (GGML_MI355X_NO_PEER or no link): src1 by peer copy to the slice
+            // device, the partial dst there, one contiguous peer copy back into a staging
+            // buffer on main, scattered into dst on the main stream
+            void * xd = grow(st.x, st.xcap, hip, xb);
+            yd = grow(st.y, st.ycap, hip, (size_t) rows * N * 4);
+            HIP_CHECK(hipSetDevice(hip));
+            // (one GPU: a plain device copy — a peer copy between a device and itself is not
+            // captured into a graph, it runs once at capture time)
+            if (hip == main_hip) HIP_CHECK(hipMemcpyAsync(xd, x->data, xb, hipMemcpyDeviceToDevice, ds->stream));
+            else HIP_CHECK(hipMemcpyPeerAsync(xd, hip, x->data, main_hip, xb, ds->stream));
+            xs.data = xd;
+            ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[1] * ys.ne[1]; ys.nb[3] = ys.nb[2] * ys.ne[2];
+            ys.data = yd;
+        }
+        if (local) {   // the main stream's buffers are sized for the graph's nodes, this slice included
+            c.scratch->reset();
+            op_mul_mat(c, &ys);
+            continue;
+        }
         stream_reserve_node(ds, &ys);
         OpCtx dc{ds, ds->stream, &ds->scratch};
         ds->scratch.reset();
         act_cache_reset(ds);
+        HIP_CHECK(hipSetDevice(hip));
         op_mul_mat(dc, &ys);
         if (direct) {
-            // the slice's rows of every column straight into dst on the main device (a 2D
-            // copy over xGMI when the devices differ: peer access is on between them)
-            HIP_CHECK(hipMemcpy2DAsync((char *) dst->data + e->lo[d] * 4, dst->nb[1], yd, (size_t) rows * 4, (size_t) rows * 4, N,
-                                       hipMemcpyDeviceToDevice, ds->stream));
             HIP_CHECK(hipEventRecord(st.ev_done, ds->stream));
             HIP_CHECK(hipSetDevice(main_hip));
             HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));
         } else {
-            // no peer access (GGML_MI355X_NO_PEER or no link): one contiguous peer copy of
-            // the partial dst into a staging buffer on main, scattered into dst there
             void * gm = grow(st.g, st.gcap, main_hip, (size_t) rows * N * 4);
             HIP_CHECK(hipSetDevice(hip));
-            HIP_CHECK(hipMemcpyPeerAsync(gm, main_hip, yd, hip, (size_t) rows * N * 4, ds->stream));
+            if (hip == main_hip) HIP_CHECK(hipMemcpyAsync(gm, yd, (size_t) rows * N * 4, hipMemcpyDeviceToDevice, ds->stream));
+            else HIP_CHECK(hipMemcpyPeerAsync(gm, main_hip, yd, hip, (size_t) rows * N * 4, ds->stream));
             HIP_CHECK(hipEventRecord(st.ev_done, ds->stream));
             HIP_CHECK(hipSetDevice(main_hip));
             HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));

@@ -13,3 +13,7 @@ OUT=gpurun_out/fa256 timeout -k 10 300 bash scripts/opbench.sh --only fa_256 --a
 AB="0=0 1=4 1=2 1=4,29=2" PASSES=2 timeout -k 10 400 bash scripts/ab_dropin.sh > gpurun_out/r4_ab_dropin_fa.txt 2>&1; echo "dropin ab rc=$?"; cat gpurun_out/r4_ab_dropin_fa.txt
 OUT=gpurun_out/falong timeout -k 10 300 bash scripts/opbench.sh --only fa_4096 fa_16384 fa_32768 --ab 2=1 0=0 2=2 2=4 2=8 2=1 > gpurun_out/r4_falong_ab.txt 2>&1; echo "fa long ab rc=$?"; grep -E "==|fattn" gpurun_out/falong/report.txt | head -60
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_ops_gpu.py -k "flash_attn" > gpurun_out/r4_fa_tests.log 2>&1; echo "fa tests rc=$?"; tail -3 gpurun_out/r4_fa_tests.log
+OUT=gpurun_out/prof_pp512 RUN="-p 512 -n 0 -c 512" timeout -k 10 300 bash scripts/prof_dropin.sh > /dev/null 2>&1; echo "prof pp rc=$?"; python tools/trace_gaps.py gpurun_out/prof_pp512/run_kernel_trace.csv --gap-us 100 | head -30
+OUT=gpurun_out/prof_tg128 timeout -k 10 300 bash scripts/prof_dropin.sh > /dev/null 2>&1; echo "prof tg rc=$?"; python tools/trace_gaps.py gpurun_out/prof_tg128/run_kernel_trace.csv --gap-us 30 | head -30
+timeout -k 10 600 bash scripts/r4_rowsplit.sh > gpurun_out/r4_rowsplit.txt 2>&1; echo "rowsplit rc=$?"; cat gpurun_out/r4_rowsplit.txt
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_dropin_gpu.py -k "split" > gpurun_out/r4_split_tests.log 2>&1; echo "split tests rc=$?"; grep -E "PASSED|FAILED|^E " gpurun_out/r4_split_tests.log | head

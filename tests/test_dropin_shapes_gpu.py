@@ -167,6 +167,10 @@ def test_llama3_8b_width_pp512(l8b, tmp_path, fa):
     k = kinds(klog)
     assert k["mmq3g"] + k["mmq4 glu"] == 2, k     # fused gate/up/SwiGLU per layer
     assert k["mmq3m"] + k["mmq4 group"] == 2, k   # q/k/v in one launch per layer
+    # GEMM -> ADD -> RMS_NORM -> MUL as the GEMM + one k_add_rms_norm pass under libllama's
+    # allocator (the norm reuses the dead GEMM input's memory): layer 0's two sites and the
+    # last layer's down projection + output norm (its attention output meets a GET_ROWS)
+    assert k["add_rms_norm"] >= 3, k
     if fa:
         assert k["fa_mma2"] == 2, k
     else:   # the KQ -> softmax -> KQV chain as one transposed-V flash launch per layer
