@@ -45,47 +45,108 @@ static Device * dev_ctx(ggml_backend_dev_t d) { return (Device *) d->context; }
 // latest one for every other path that touches device memory (buffer reads, memsets,
 // copies, another stream's graph), which waits for it first.
 // ---------------------------------------------------------------------------
+// Round 4: a staged write no longer issues its own copy. Each one only lands in the pinned
+// ring and is queued; the queue is flushed — ONE kernel on the compute stream copying every
+// queued range from the ring (zero-copy reads of pinned host memory), then one event — when
+// anything needs device memory ordered: graph_compute, every other buffer path, a
+// synchronize. Per decoded token libllama writes ~6 inputs: 6 x (hipMemcpyAsync +
+// hipEventRecord) of host time on the critical path between tokens, and 6 blit launches on
+// the GPU (drop-in profile, profiles/r04/), became one launch.
+struct StageEntry { const char * src; char * dst; uint32_t n, chunk0; };
+constexpr int kFlushMax = 16;                  // ranges per flush launch
+constexpr uint32_t kFlushChunk = 16384;        // bytes per workgroup
+struct StageFlushArgs { StageEntry e[kFlushMax]; int n; };
+
+__global__ __launch_bounds__(256) void k_stage_flush(StageFlushArgs a) {
+    int k = 0;
+    while (k + 1 < a.n && blockIdx.x >= a.e[k + 1].chunk0) ++k;   // workgroup-uniform
+    const StageEntry e = a.e[k];
+    const uint32_t off = (blockIdx.x - e.chunk0) * kFlushChunk;
+    const uint32_t n = min(kFlushChunk, e.n - off);
+    const char * src = e.src + off;
+    char * dst = e.dst + off;
+    if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0) {
+        for (uint32_t i = 16 * threadIdx.x; i + 16 <= n; i += 16 * 256) *(uint4 *) (dst + i) = *(const uint4 *) (src + i);
+        for (uint32_t i = (n & ~15u) + threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    }
+}
+
 struct Staging {
     std::mutex mu;
     Stream * s = nullptr;          // compute stream the writes go to (null: synchronous writes)
     char * host = nullptr;         // pinned ring
     size_t cap = 0, off = 0;
     hipEvent_t ev = nullptr;
-    bool pending = false;
+    bool pending = false;          // a flushed write may still be in flight (ev marks the last)
+    std::vector<StageEntry> queued;   // in the ring, not yet copied
     uint64_t n = 0;                // staged writes (GGML_MI355X_STATS)
+    uint64_t n_flush = 0;          // flush launches
 };
 static Staging g_stage[MX_MAX_DEVICES];
-static constexpr size_t kStageMax = 64 << 10, kStageRing = 4 << 20;
+static constexpr size_t kStageMax = 4 << 20, kStageRing = 32 << 20;
+
+static void stage_flush_locked(Staging & st) {
+    if (st.queued.empty()) return;
+    int cur = 0;
+    HIP_CHECK(hipGetDevice(&cur));
+    if (cur != st.s->device) HIP_CHECK(hipSetDevice(st.s->device));
+    for (size_t b = 0; b < st.queued.size(); b += kFlushMax) {
+        StageFlushArgs a{};
+        uint32_t chunks = 0;
+        a.n = (int) std::min<size_t>(kFlushMax, st.queued.size() - b);
+        for (int k = 0; k < a.n; ++k) {
+            a.e[k] = st.queued[b + k];
+            a.e[k].chunk0 = chunks;
+            chunks += (a.e[k].n + kFlushChunk - 1) / kFlushChunk;
+        }
+        k_stage_flush<<<chunks, 256, 0, st.s->stream>>>(a);
+        st.n_flush++;
+    }
+    HIP_CHECK(hipEventRecord(st.ev, st.s->stream));
+    st.pending = true;
+    st.queued.clear();
+    if (cur != st.s->device) HIP_CHECK(hipSetDevice(cur));
+}
 
 static bool stage_write(int dev, void * dst, const void * data, size_t size) {
-    if (dev < 0 || dev >= MX_MAX_DEVICES || size > kStageMax) return false;
+    if (dev < 0 || dev >= MX_MAX_DEVICES || size > kStageMax || size == 0) return false;
     Staging & st = g_stage[dev];
     std::lock_guard<std::mutex> lk(st.mu);
     if (!st.s) return false;
     if (!st.host) {
-        if (hipHostMalloc((void **) &st.host, kStageRing, hipHostMallocDefault) != hipSuccess) { (void) hipGetLastError(); st.host = nullptr; return false; }
+        if (hipHostMalloc((void **) &st.host, kStageRing, hipHostMallocPortable) != hipSuccess) { (void) hipGetLastError(); st.host = nullptr; return false; }
         HIP_CHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
         st.cap = kStageRing;
     }
+    // a queued range this one overlaps is copied first (the ranges of one flush run in
+    // parallel: the later write must not race the earlier)
+    const char * lo = (const char *) dst, * hi = lo + size;
+    for (const StageEntry & e : st.queued)
+        if (e.dst < hi && lo < e.dst + e.n) { stage_flush_locked(st); break; }
     size_t a = (st.off + 255) & ~(size_t) 255;
-    if (a + size > st.cap) {       // wrap: every earlier staged copy has to be done reading
+    if (a + size > st.cap) {       // wrap: every earlier range has to be copied and done reading
+        stage_flush_locked(st);
         HIP_CHECK(hipStreamSynchronize(st.s->stream));
         a = 0;
     }
     memcpy(st.host + a, data, size);
-    HIP_CHECK(hipMemcpyAsync(dst, st.host + a, size, hipMemcpyHostToDevice, st.s->stream));
-    HIP_CHECK(hipEventRecord(st.ev, st.s->stream));
+    st.queued.push_back(StageEntry{st.host + a, (char *) dst, (uint32_t) size, 0});
     st.off = a + size;
-    st.pending = true;
     st.n++;
+    static const bool immediate = getenv("GGML_MI355X_STAGE_IMMEDIATE") != nullptr;   // A/B: one flush per write
+    if (immediate) stage_flush_locked(st);
     return true;
 }
 
-// make `stream` wait for the device's staged writes (no-op when none or on their stream)
+// make `stream` wait for the device's staged writes (no-op when none or on their stream);
+// queued ones are flushed first
 void staged_writes_wait(int dev, hipStream_t stream) {
     if (dev < 0 || dev >= MX_MAX_DEVICES) return;
     Staging & st = g_stage[dev];
     std::lock_guard<std::mutex> lk(st.mu);
+    if (st.s) stage_flush_locked(st);
     if (!st.pending || (st.s && st.s->stream == stream)) return;
     HIP_CHECK(hipStreamWaitEvent(stream, st.ev, 0));
 }
@@ -228,6 +289,11 @@ void klog_dump(const char * path);
 static void be_free(ggml_backend_t b) {
     Stream * s = stream_of(b);
     hipSetDevice(s->device);
+    if (s->device >= 0 && s->device < MX_MAX_DEVICES) {   // queued writes land before the stream goes
+        Staging & st = g_stage[s->device];
+        std::lock_guard<std::mutex> lk(st.mu);
+        if (st.s == s) stage_flush_locked(st);
+    }
     hipStreamSynchronize(s->stream);
     if (s->device >= 0 && s->device < MX_MAX_DEVICES) {   // later small writes go synchronous again
         Staging & st = g_stage[s->device];
@@ -240,11 +306,12 @@ static void be_free(ggml_backend_t b) {
         fprintf(stderr, "[mi355x] stats {\"backend\": \"%s\", \"graph_compute\": %llu, \"graph_replay\": %llu, "
                 "\"nodes_run\": %llu, \"nodes_fused\": %llu, \"host_us\": {\"graph_compute\": %.0f, \"set_async\": %.0f, "
                 "\"get_async\": %.0f, \"synchronize\": %.0f, \"signature\": %.0f, \"graph_launch\": %.0f}, \"n_set\": %llu, \"bytes_set\": %llu, \"n_get\": %llu, "
-                "\"bytes_get\": %llu, \"n_staged\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
+                "\"bytes_get\": %llu, \"n_staged\": %llu, \"n_stage_flush\": %llu}\n", s->name.c_str(), (unsigned long long) s->n_graph_compute,
                 (unsigned long long) s->n_graph_replay, (unsigned long long) s->n_nodes_run, (unsigned long long) s->n_fused,
                 s->us_compute, s->us_set, s->us_get, s->us_sync, s->us_sig, s->us_launch, (unsigned long long) s->n_set, (unsigned long long) s->b_set,
                 (unsigned long long) s->n_get, (unsigned long long) s->b_get,
-                (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n : 0));
+                (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n : 0),
+                (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n_flush : 0));
     if (const char * kp = getenv("GGML_MI355X_KLOG")) klog_dump(kp);
     if (s->gcache.exec) hipGraphExecDestroy(s->gcache.exec);
     if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
@@ -305,6 +372,7 @@ static void be_sync(ggml_backend_t b) {
     Stream * s = stream_of(b);
     const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));
+    staged_writes_wait(s->device, s->stream);   // queued input writes are part of "done"
     HIP_CHECK(hipStreamSynchronize(s->stream));
     s->us_sync += now_us() - t0;
 }

@@ -306,6 +306,42 @@ static int try_fuse_mm_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     return mmq_fused_add(c, mm, res, add) ? 2 : 0;
 }
 
+// The last layer of a decoded token (src/models/llama.cpp: inp_out_ids): MUL_MAT(wo, x) ->
+// GET_ROWS(mm, ids) , GET_ROWS(inpSA, ids) -> ADD. With one token both GET_ROWS select the
+// only row (ids holds 0: libllama never asks for a row that is not there), so the chain is
+// MUL_MAT -> ADD(inpSA): the GEMV with the residual epilogue writing the ADD's output — one
+// launch instead of four (drop-in decode profile, profiles/r04/: two k_get_rows + one ADD
+// per token beside the GEMV). Returns the nodes consumed (0: no match).
+static int try_fuse_mm_rows_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
+    ggml_tensor * mm = g->nodes[i];
+    if (mm->src[1]->ne[1] != 1 || mx_nrows(mm) != 1 || uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    ggml_tensor * g1 = nullptr, * g2 = nullptr, * add = nullptr;
+    int last = i;
+    for (int j = i + 1; j < g->n_nodes && j <= i + 4; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (is_view_op(n->op)) continue;
+        if (n->op == GGML_OP_GET_ROWS && !g1 && n->src[0] == mm) { g1 = n; last = j; continue; }
+        if (n->op == GGML_OP_GET_ROWS && !g2 && n->src[0] != mm) { g2 = n; last = j; continue; }
+        if (n->op == GGML_OP_ADD && g1 && g2 && ((n->src[0] == g1 && n->src[1] == g2) || (n->src[0] == g2 && n->src[1] == g1))) {
+            add = n; last = j;
+        }
+        break;
+    }
+    if (!add) return 0;
+    const ggml_tensor * res = g2->src[0];
+    for (const ggml_tensor * gr : {g1, g2}) {
+        const ggml_tensor * ids = gr->src[1];
+        if (gr->type != GGML_TYPE_F32 || gr->src[0]->type != GGML_TYPE_F32 || mx_nrows(gr->src[0]) != 1 || mx_nrows(gr) != 1 ||
+            mx_nelements(ids) != 1 || uses[gr] != 1 || (gr->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    }
+    if (!mx_are_same_shape(res, mm) || !mx_are_same_shape(add, mm) || !mx_is_contiguous(res) || !mx_is_contiguous(add)) return 0;
+    const bool same = res->nb[1] == add->nb[1];
+    if (!fused_io_ok({add}, {res}, {{add, same ? res : nullptr}})) return 0;
+    act_cache_invalidate(c.s, add);
+    if (!mmvq_fused_add(c, mm, res, add)) return 0;
+    return last - i + 1;
+}
+
 // MUL_MAT(gate) , MUL_MAT(up) , GLU(gate, up) with one activation column:
 // one pass over the activation, two weight streams (ggml-cuda.cu:2145-2181).
 static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
@@ -532,7 +568,8 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             if (n->op == GGML_OP_MUL_MAT && try_fuse_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             if (n->op == GGML_OP_MUL_MAT && try_group_mm(c, g, i, done)) continue;
             if (n->op == GGML_OP_MUL_MAT) {
-                const int k = try_fuse_mm_add(c, g, i, uses);
+                int k = try_fuse_mm_add(c, g, i, uses);
+                if (k == 0) k = try_fuse_mm_rows_add(c, g, i, uses);
                 if (k > 0) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; deferred_retire(s, g, i0, i); continue; }
             }
         }

@@ -10,3 +10,8 @@ OUT=gpurun_out/prof_pp512b RUN="-p 512 -n 0 -c 512" timeout -k 10 300 bash scrip
 python3 tools/trace_gaps.py gpurun_out/prof_pp512b/run_kernel_trace.csv --gap-us 100 > gpurun_out/prof_pp512b_gaps.txt; grep -E "k_add_rms|k_mmq4_reduce|k_rms_norm_v4" gpurun_out/prof_pp512b/run_kernel_stats.csv | cut -c1-120
 G=${TMPDIR:-/tmp}/mx_bench_llama3_8b_q4_k_m.gguf
 for i in 1 2; do GGML_BACKEND_PATH=$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so timeout -k 10 300 oracle/_ref/ref-llama-bench -m $G -t 8 -ngl 99 -fa 1 -p 512 -n 0 -r 5 2>/dev/null | grep '^{'; done
+AB="0=0" PASSES=1 EXTRA="" bash scripts/ab_dropin.sh
+for pass in 1 2; do for arm in "" "GGML_MI355X_STAGE_IMMEDIATE=1"; do
+  r=$(env $arm GGML_BACKEND_PATH=$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so timeout -k 10 300 oracle/_ref/ref-llama-bench -m $G -t 8 -ngl 99 -fa 1 -p 512 -n 128 -r 5 2>/dev/null | grep '^{')
+  echo "pass=$pass arm=[$arm] $(echo $r | grep -o '"pp_tok_s": [0-9.]*') $(echo $r | grep -o '"tg_tok_s": [0-9.]*')"
+done; done

@@ -138,10 +138,10 @@ def test_llama3_8b_width_decode(l8b, tmp_path, fa):
     # lm_head: libllama marks result_norm an output, so the norm is not deferred; its
     # fused RMS_NORM+MUL kernel emits the q8 copy the lm_head GEMV stages
     assert k["gemv2 epi=0 mode=2 M=128256 q8o=0"] == n, k
-    # O projection: + residual in the epilogue, except in the last layer, where
-    # libllama's inp_out_ids GET_ROWS sits between the projection and the ADD
-    assert k["gemv2 epi=2 mode=0 M=4096 q8o=0"] == n * (L - 1), k
-    assert k["gemv2 epi=0 mode=0 M=4096 q8o=0"] == n, k
+    # O projection: + residual in the epilogue in every layer (in the last one across
+    # libllama's one-row inp_out_ids GET_ROWS pair: exec.cpp try_fuse_mm_rows_add)
+    assert k["gemv2 epi=2 mode=0 M=4096 q8o=0"] == n * L, k
+    assert k["gemv2 epi=0 mode=0 M=4096 q8o=0"] == 0, k
     if fa:
         assert k["fattn_dec2"] + k["fattn_dec"] == n * L, k
     assert k["mmvq1"] == 0, k                                  # no first-generation fallback GEMV
@@ -168,9 +168,9 @@ def test_llama3_8b_width_pp512(l8b, tmp_path, fa):
     assert k["mmq3g"] + k["mmq4 glu"] == 2, k     # fused gate/up/SwiGLU per layer
     assert k["mmq3m"] + k["mmq4 group"] == 2, k   # q/k/v in one launch per layer
     # GEMM -> ADD -> RMS_NORM -> MUL as the GEMM + one k_add_rms_norm pass under libllama's
-    # allocator (the norm reuses the dead GEMM input's memory): layer 0's two sites and the
-    # last layer's down projection + output norm (its attention output meets a GET_ROWS)
-    assert k["add_rms_norm"] >= 3, k
+    # allocator (the norm reuses the dead GEMM input's memory): layer 0's two sites (the last
+    # layer's attention output meets libllama's inp_out_ids GET_ROWS first)
+    assert k["add_rms_norm"] >= 2, k
     if fa:
         assert k["fa_mma2"] == 2, k
     else:   # the KQ -> softmax -> KQV chain as one transposed-V flash launch per layer
@@ -249,18 +249,23 @@ def test_llama3_70b_width_layer_split_8(l70b8, tmp_path, incremental):
     (GGML_MI355X_VIRTUAL_DEVICES=8): one layer per device (src/llama-model.cpp:2599-2609),
     pipeline parallelism on, every one of the seven boundary activations handed over by
     be_cpy_async on its peer-copy branch (GGML_MI355X_FORCE_PEER=1, the branch eight real
-    GPUs take). Logits against the reference CPU backend: incremental decode at the
-    whole-graph bound, a 40-token prefill at the 70B-width prefill bound (per-node
-    attribution: profiles/r04/attrib_llama3_70b_2l_fa1.txt)."""
+    GPUs take). Logits against the same backend on one device (incremental decode and a
+    40-token prefill)."""
     toks = np.random.default_rng(35).integers(0, 128000, 6 if incremental else 40)
-    cpu, _, _ = run_ref(tmp_path, l70b8, toks, 0, 1, incremental=incremental)
+    one, _, _ = run_ref(tmp_path, l70b8, toks, 99, 1, incremental=incremental, tag="one")
     gpu, log, klog = run_ref(tmp_path, l70b8, toks, 99, 1, incremental=incremental,
                              extra=["-sm", "layer", "-ts", ",".join(["1"] * 8)],
                              env_extra={"GGML_MI355X_VIRTUAL_DEVICES": "8", "GGML_MI355X_FORCE_PEER": "1"})
     assert "MI355X7" in log, log[-2000:]
     assert np.all(np.isfinite(gpu))
-    err = nmse(gpu, cpu)
-    assert err < (TOL if incremental else TOL_70B_PP), err
+    # the split must not change the arithmetic: against the same backend on one device (the
+    # per-layer kernels are the same; the boundaries only copy). The one-device path itself
+    # is pinned to the reference CPU backend at these widths by the two-layer tests; over
+    # eight random-weight layers the two backends' small per-node differences (the CPU's
+    # q8_K activation rounding, profiles/r04/attrib_llama3_70b_2l_fa1.txt) grow by the
+    # attention's amplification to NMSE ~1e-2, so the CPU is not the bound here.
+    err = nmse(gpu, one)
+    assert err < 1e-6, err
     cp = [ln for ln in klog if ln.startswith("cpy_async")]
     assert cp and all("peer=1" in ln for ln in cp), cp[:8]
     for i in range(7):
@@ -367,12 +372,10 @@ def test_runner_launch_mix_equals_dropin(pkg, backend, l8b, tmp_path):
     per_tok = collections.Counter({kk: v // len(toks) for kk, v in theirs.items()})
     hot = [kk for kk in set(ours) | set(per_tok) if kk.startswith(("gemv2", "qkv", "fattn"))]
     assert hot, ours
-    # the two graphs differ only where libllama's graph differs: inp_out_ids GET_ROWS after
-    # the last layer's attention (O projection without residual fusion). The lm_head reads
-    # the RMS_NORM+MUL+q8 launch's q8 copy in both (exec.cpp never defers a norm into a
-    # 128256-row grid)
-    ours_adj = collections.Counter(ours)
-    ours_adj["gemv2 epi=2 mode=0 M=4096 q8o=0"] -= 1
-    ours_adj["gemv2 epi=0 mode=0 M=4096 q8o=0"] += 1
+    # libllama's graph has the inp_out_ids GET_ROWS pair after the last layer's attention;
+    # for one token exec.cpp folds MUL_MAT -> GET_ROWS x2 -> ADD into the residual GEMV
+    # (round 4), so the hot launches are the same kernels, the same number of times. The
+    # lm_head reads the RMS_NORM+MUL+q8 launch's q8 copy in both (exec.cpp never defers a
+    # norm into a 128256-row grid)
     for kk in hot:
-        assert per_tok[kk] == ours_adj[kk], (kk, per_tok, ours)
+        assert per_tok[kk] == ours[kk], (kk, per_tok, ours)
