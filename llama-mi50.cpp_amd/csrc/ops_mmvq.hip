@@ -350,9 +350,24 @@ bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, 
     if (res->type != GGML_TYPE_F32 || add->type != GGML_TYPE_F32 || !mx_are_same_shape(res, mm) || !mx_are_same_shape(add, mm)) return false;
     if (res->nb[0] != 4 || add->nb[0] != 4 || w->ne[2] != 1 || w->ne[3] != 1) return false;
     XStage xs;
-    if (g_gemv2 && gemv2_ok(w, x, add) && mx_is_contiguous(res) && gemv2_stage(c, x, {add}, {res}, &xs)) {
-        gemv2_launch(c, w, nullptr, xs, (float *) add->data, (const float *) res->data);
-        return true;
+    if (g_gemv2 && gemv2_ok(w, x, add) && mx_is_contiguous(res)) {
+        if (gemv2_stage(c, x, {add}, {res}, &xs)) {
+            gemv2_launch(c, w, nullptr, xs, (float *) add->data, (const float *) res->data);
+            return true;
+        }
+        // the output lies over x (libllama's allocator hands the dead input's memory to the
+        // ADD: the last layer's MUL_MAT -> GET_ROWS -> ADD chain): quantise x into the
+        // activation cache first, then stream the GEMV from that q8 copy — no workgroup reads
+        // x while another writes the output (gemv2_stage refused exactly that)
+        if (!xs.norm) {
+            quantize_activations(c, x);
+            xs = xstage_of(c.s, x);
+            if (xs.q8 && !xs.norm) {
+                gemv2_launch(c, w, nullptr, xs, (float *) add->data, (const float *) res->data);
+                act_cache_invalidate(c.s, add);
+                return true;
+            }
+        }
     }
     ActQ a = quantize_activations(c, x);
     MmvArgs p = mmv_args(w, x, add);
