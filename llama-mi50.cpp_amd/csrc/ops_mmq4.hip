@@ -54,7 +54,10 @@ constexpr int M4_KC = 128;        // K per chunk (half a super-block)
 #ifndef MX_M4_PIPE
 #define MX_M4_PIPE 1
 #endif
-constexpr int M4_XDEF = (MX_M4_Q6V2 ? 8 : 0) | (MX_M4_PIPE ? 16 : 0);
+#ifndef MX_M4_2STAGE      // two-chunk stages (round 4): glu 181 -> 159, down Q6_K 114 -> 100 us
+#define MX_M4_2STAGE 1    // (same-box opbench, profiles/r04/mmq4_two_chunk_stages_ab.txt)
+#endif
+constexpr int M4_XDEF = (MX_M4_Q6V2 ? 8 : 0) | (MX_M4_PIPE ? 16 : 0) | (MX_M4_2STAGE ? 32 : 0);
 #ifndef MX_M4_LDA
 #define MX_M4_LDA 1               // MFMA steps the LDS activation reads run ahead (1 or 2)
 #endif
@@ -409,14 +412,47 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
     };
     auto wl = [&](int i, M4W<QT> & rw) { m4_load<QT>(wrow, MX_DBG(p.dbg & 8) ? c0 : c0 + i, h, rw); };
     M4W<QT> r0, r1, r2;
-    // prologue: ring stages 0 .. S-2, weights of chunks 0 and 1
+    // prologue: ring stages 0 .. S-2 (two-chunk stages: chunks 0 and 1), weights of chunks 0 and 1
 #pragma unroll
-    for (int i = 0; i < M4_S - 1; ++i) if (i < nc) dma(i);
+    for (int i = 0; i < ((X & 32) ? 2 : M4_S - 1); ++i) if (i < nc) dma(i);
     __builtin_amdgcn_sched_barrier(0);
     wl(0, r0);
     if (nc > 1) wl(1, r1);
     __builtin_amdgcn_sched_barrier(0);
     MX_TRACE(tr, 1);
+    if constexpr (X & 32) {
+        // round 4 (X bit 32, the default; g_tune[3] = 2 restores one-chunk stages): two-chunk
+        // stages — the ring's four chunk slots
+        // are filled two at a time, one counted wait + barrier per PAIR of chunks (the
+        // per-chunk wait + barrier was 44 of 203 us of the glu, profiles/r03/
+        // mmq4_decomposition.txt); prefetch distance two chunks instead of three. Loop
+        // unrolled by six (weight register sets rotate by three, stages by two).
+        auto iter2 = [&](int i, bool even, const M4W<QT> & rc, M4W<QT> & rn) {
+            if (even) {
+                // issued after DMA(i), DMA(i+1) (at i - 2): the weights of chunks i and i+1
+                if (i + 3 < nc) m4_wait_vm<2 * NW>();
+                else m4_wait_vm<0>();
+                m4_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 2 < nc) dma(i + 2);
+                if (i + 3 < nc) dma(i + 3);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 2 < nc) wl(i + 2, rn);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(rc, i);
+        };
+        for (int i = 0; i < nc; i += 6) {
+            iter2(i, true, r0, r2);
+            if (i + 1 < nc) iter2(i + 1, false, r1, r0);
+            if (i + 2 < nc) iter2(i + 2, true, r2, r1);
+            if (i + 3 < nc) iter2(i + 3, false, r0, r2);
+            if (i + 4 < nc) iter2(i + 4, true, r1, r0);
+            if (i + 5 < nc) iter2(i + 5, false, r2, r1);
+        }
+        MX_TRACE(tr, 6);
+        return;
+    }
     auto iter = [&](int i, const M4W<QT> & rc, M4W<QT> & rn) {
         // instructions issued after DMA(i): >= DMA(i+1), DMA(i+2) and two chunks of weight
         // loads in steady state; the last chunks drain everything
@@ -601,6 +637,8 @@ static void m4_kernel_x(hipStream_t st, const M4Args & a, dim3 g) {
 
 template <int QTA, int QTB, int TT, int EPI>
 static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
+    if constexpr (QTA == QTB && TT == 4 && EPI < 2)
+        if (g_tune[3] == 2) return m4_kernel_x<QTA, QTB, TT, EPI, M4_XDEF & ~32>(st, a, g);   // one-chunk stages (A/B)
     if constexpr (MX_AB_VARIANTS && QTA == QTB && TT == 4 && EPI < 2 && QTA != GGML_TYPE_Q5_K) {
         switch (g_tune[31]) {   // timing experiments (X bits above), the prefill GEMM shapes only
             case 1: return m4_kernel_x<QTA, QTB, TT, EPI, 1 | M4_XDEF>(st, a, g);
