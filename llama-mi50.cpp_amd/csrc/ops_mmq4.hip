@@ -57,7 +57,11 @@ constexpr int M4_KC = 128;        // K per chunk (half a super-block)
 #ifndef MX_M4_2STAGE      // two-chunk stages (round 4): glu 181 -> 159, down Q6_K 114 -> 100 us
 #define MX_M4_2STAGE 1    // (same-box opbench, profiles/r04/mmq4_two_chunk_stages_ab.txt)
 #endif
-constexpr int M4_XDEF = (MX_M4_Q6V2 ? 8 : 0) | (MX_M4_PIPE ? 16 : 0) | (MX_M4_2STAGE ? 32 : 0);
+#ifndef MX_M4_5SLOT       // five-slot (160 KB) ring with two-chunk stages: glu 164.8 -> 159.0,
+#define MX_M4_5SLOT 1     // down Q6_K 105 -> 102 us (profiles/r04/mmq4_five_slot_ab.txt)
+#endif
+constexpr int M4_XDEF = (MX_M4_Q6V2 ? 8 : 0) | (MX_M4_PIPE ? 16 : 0) | (MX_M4_2STAGE ? 32 : 0) |
+                        (MX_M4_2STAGE && MX_M4_5SLOT ? 64 : 0);
 #ifndef MX_M4_LDA
 #define MX_M4_LDA 1               // MFMA steps the LDS activation reads run ahead (1 or 2)
 #endif
@@ -316,6 +320,7 @@ __device__ __forceinline__ void m4_barrier() {   // LDS reads/writes of this wav
 
 constexpr int M4_WAVES = 8;        // waves per workgroup (two per SIMD)
 constexpr int M4_S = 4;            // activation ring stages (prefetch distance M4_S - 1 chunks)
+template <int X> __host__ __device__ constexpr int m4_slots() { return (X & 64) ? 5 : M4_S; }   // X 64: 160 KB ring
 
 // The K loop of one wave over chunks [c0, c0 + nc): its lane's row `wrow`, tokens
 // [tok0, tok0 + 32 TT) of the workgroup's activation ring (cols: activation column of
@@ -336,7 +341,7 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
         for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
     auto dma = [&](int i) {
         if (MX_DBG(p.dbg & 4)) return;
-        const int st = (i % M4_S) * TILE, kc = c0 + i;
+        const int st = (i % m4_slots<X>()) * TILE, kc = c0 + i;
 #pragma unroll
         for (int d = 0; d < NDMA; ++d) {
             const int trow = (wave * NDMA + d) * 4 + (lane >> 4);
@@ -358,7 +363,7 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
         }
     };
     auto compute = [&](const M4W<QT> & rw, int i) {
-        const uint4 * L = lds + (i % M4_S) * TILE;
+        const uint4 * L = lds + (i % m4_slots<X>()) * TILE;
         const int kc = c0 + i;
         // activation fragments MX_M4_LDA steps ahead (ring of MX_M4_LDA + 1 register sets)
         constexpr int D = (X & 16) ? 2 : MX_M4_LDA;
@@ -414,7 +419,7 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
     M4W<QT> r0, r1, r2;
     // prologue: ring stages 0 .. S-2 (two-chunk stages: chunks 0 and 1), weights of chunks 0 and 1
 #pragma unroll
-    for (int i = 0; i < ((X & 32) ? 2 : M4_S - 1); ++i) if (i < nc) dma(i);
+    for (int i = 0; i < ((X & 64) ? 3 : (X & 32) ? 2 : M4_S - 1); ++i) if (i < nc) dma(i);
     __builtin_amdgcn_sched_barrier(0);
     wl(0, r0);
     if (nc > 1) wl(1, r1);
@@ -428,7 +433,17 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
         // mmq4_decomposition.txt); prefetch distance two chunks instead of three. Loop
         // unrolled by six (weight register sets rotate by three, stages by two).
         auto iter2 = [&](int i, bool even, const M4W<QT> & rc, M4W<QT> & rn) {
-            if (even) {
+            if (even && (X & 64)) {
+                // five slots: chunks i+3, i+4 go into the slots of i-2, i-1 (done before this
+                // barrier); issued after DMA(i+1) (at i - 2): DMA(i+2) and the weights of
+                // chunks i and i+1
+                if (i + 2 < nc) m4_wait_vm<NDMA + 2 * NW>();
+                else m4_wait_vm<0>();
+                m4_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + 3 < nc) dma(i + 3);
+                if (i + 4 < nc) dma(i + 4);
+            } else if (even) {
                 // issued after DMA(i), DMA(i+1) (at i - 2): the weights of chunks i and i+1
                 if (i + 3 < nc) m4_wait_vm<2 * NW>();
                 else m4_wait_vm<0>();
@@ -626,7 +641,7 @@ static bool m4_plain_ok(int64_t K) { return m4_all() || K >= 8192; }
 
 template <int QTA, int QTB, int TT, int EPI, int X = M4_XDEF>
 static void m4_kernel_x(hipStream_t st, const M4Args & a, dim3 g) {
-    constexpr int lds = M4_S * 32 * TT * 256;
+    constexpr int lds = m4_slots<X>() * 32 * TT * 256;
     static const bool attr = [] {
         HIP_CHECK(hipFuncSetAttribute((const void *) k_mmq4<QTA, QTB, TT, EPI, X>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         return true;
@@ -637,8 +652,12 @@ static void m4_kernel_x(hipStream_t st, const M4Args & a, dim3 g) {
 
 template <int QTA, int QTB, int TT, int EPI>
 static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
-    if constexpr (QTA == QTB && TT == 4 && EPI < 2)
-        if (g_tune[3] == 2) return m4_kernel_x<QTA, QTB, TT, EPI, M4_XDEF & ~32>(st, a, g);   // one-chunk stages (A/B)
+    // A/B: g_tune[3] = 2 the round-3 loop (one wait + barrier per chunk, four slots), 4 the
+    // four-slot two-chunk stages
+    if constexpr (QTA == QTB && TT == 4 && EPI < 2) {
+        if (g_tune[3] == 2) return m4_kernel_x<QTA, QTB, TT, EPI, M4_XDEF & ~(32 | 64)>(st, a, g);
+        if (g_tune[3] == 4) return m4_kernel_x<QTA, QTB, TT, EPI, (M4_XDEF & ~64) | 32>(st, a, g);
+    }
     if constexpr (MX_AB_VARIANTS && QTA == QTB && TT == 4 && EPI < 2 && QTA != GGML_TYPE_Q5_K) {
         switch (g_tune[31]) {   // timing experiments (X bits above), the prefill GEMM shapes only
             case 1: return m4_kernel_x<QTA, QTB, TT, EPI, 1 | M4_XDEF>(st, a, g);
