@@ -303,6 +303,11 @@ def dropin_layer_split(args, world, tg_leg=True):
     vis = os.environ.get("HIP_VISIBLE_DEVICES")
     devs = vis.split(",")[:world] if vis else [str(i) for i in range(world)]
     env = dict(os.environ, GGML_BACKEND_PATH=LIB, HIP_VISIBLE_DEVICES=",".join(devs), GGML_MI355X_STATS="1")
+    if os.environ.get("MX_BENCH_VIRTUAL") == "1":
+        # rehearsal on a one-GPU box: N logical devices of GPU 0 (GGML_MI355X_VIRTUAL_DEVICES),
+        # every layer boundary on the peer-copy branch — the control flow of the real N-GPU run
+        devs = [devs[0]]
+        env.update(HIP_VISIBLE_DEVICES=devs[0], GGML_MI355X_VIRTUAL_DEVICES=str(world), GGML_MI355X_FORCE_PEER="1")
     ts = ",".join(["1"] * world)
     split = ["-fa", "1", "-sm", "layer", "-ts", ts]
     out = {"how": f"reference libllama -sm layer -ts {ts} over HIP devices {','.join(devs)}, -ngl 99, -fa 1",

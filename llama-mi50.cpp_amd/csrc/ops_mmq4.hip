@@ -32,6 +32,8 @@
 #include "mm.h"
 #include "gemv.h"
 
+#include <type_traits>
+
 namespace mx {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -625,6 +627,265 @@ __global__ void k_mmq4_reduce(M4Args p) {
 }
 
 // ---------------------------------------------------------------------------
+// k_mmq5: the gate/up/SwiGLU GEMM on 256-token tiles, one wave per SIMD (round 4).
+// In k_mmq4 a wave multiplies one dequantised 32-row B fragment into 4 token tiles: ~6
+// VALU per MFMA, which with the partner wave's share overfills the MFMA's issue gaps (at
+// most ~5 single-issue fillers hide per v_mfma_f32_32x32x16, MI355X_MICROARCH.md constants
+// table), and every MFMA reads its own activation fragment from LDS. Here a wave holds 32
+// gate rows AND the same 32 up rows (two B fragments) x 256 tokens (eight token tiles):
+// per 16-deep step 16 MFMAs on 8 LDS reads and 2 dequantisations (~2-3 VALU per MFMA);
+// 256 accumulators (512-register wave), and the SwiGLU pairs gate and up inside the lane
+// that holds both (no LDS exchange). Four waves = 128 row pairs x 256 tokens per
+// workgroup; a 2 x 64 KB activation ring (one wait + barrier per 128-deep chunk, DMA one
+// chunk ahead), weights two chunks ahead in three register sets. Token tiles of one row
+// tile go to one XCD (they read the same weight rows: one HBM read per L2).
+// ---------------------------------------------------------------------------
+#ifndef M5TT_
+#define M5TT_ 8
+#endif
+#ifndef M5_SCHED
+#define M5_SCHED 1
+#endif
+constexpr int M5_WAVES = 4, M5_TT = M5TT_, M5_BT = 32 * M5_TT;
+constexpr int M5_TILE = M5_BT * 16;                  // uint4 per ring slot (64 KB)
+constexpr int M5_NDMA = M5_BT / 4 / M5_WAVES;        // 1-KB LDS-DMA pieces per wave per chunk
+constexpr int M5_LDS = 2 * M5_TILE * 16;
+constexpr int M5_XDEF = M4_XDEF;   // (| 128: interleaved issue, g_tune[3] = 16; measured slower)
+
+// m4_load with the chunk-dependent part of every address uniform (base + kc offsets) and
+// the lane's part a 32-bit offset (row, k-slice h)
+template <int QT>
+__device__ __forceinline__ void m5_load(const char * base, uint32_t wo, int kc, int h, M4W<QT> & r) {
+    const int sb = kc >> 1, hf = kc & 1;
+    const uint32_t qo = wo + 32u * (uint32_t) h;
+    if constexpr (QT == GGML_TYPE_Q4_K) {
+        const char * b = base + (size_t) sb * 144;
+        r.hd = *(const int4 *) (b + wo);
+        r.q0 = *(const int4 *) (b + 16 + 64 * hf + qo);
+        r.q1 = *(const int4 *) (b + 32 + 64 * hf + qo);
+    } else {
+        static_assert(QT == GGML_TYPE_Q5_K, "k_mmq5: Q4_K / Q5_K");
+        const char * b = base + (size_t) sb * 176;
+        r.hd = *(const int4 *) (b + wo);
+        r.h0 = *(const int4 *) (b + 16 + wo);
+        r.h1 = *(const int4 *) (b + 32 + wo);
+        r.q0 = *(const int4 *) (b + 48 + 64 * hf + qo);
+        r.q1 = *(const int4 *) (b + 64 + 64 * hf + qo);
+    }
+}
+
+// largest scaled weight magnitude of a Q4_K / Q5_K super-block per unit of scale (its
+// d / dmin header dword), and the weight scale a row whose maximum is `need` takes
+template <int QT>
+__device__ __forceinline__ float m5_need(uint32_t dd) {
+    const float d = __builtin_fabsf(h2f((uint16_t) (dd & 0xFFFF)));
+    const float dm = __builtin_fabsf(h2f((uint16_t) (dd >> 16)));
+    return __builtin_fmaxf(d * (QT == GGML_TYPE_Q4_K ? 945.0f : 1953.0f), dm * 63.0f);
+}
+__device__ __forceinline__ float m5_ws(float need) {
+    if (need * M4_WSCALE < 32768.0f) return M4_WSCALE;
+    int e;
+    (void) __builtin_frexpf(32768.0f / need, &e);
+    return __builtin_ldexpf(1.0f, e - 1);
+}
+
+template <int QT, int X = M5_XDEF>
+__global__ __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(1, 1)))
+void k_mmq5_glu(M4Args p) {
+    extern __shared__ __align__(16) uint4 lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const M4Seg & sg = p.seg[0];
+    const int T = (p.N + M5_BT - 1) / M5_BT, R = (sg.M + 127) / 128, L = (int) blockIdx.x;
+    int rt, tt;
+    if ((R & 7) == 0) { const int k = L >> 3; rt = (k / T) * 8 + (L & 7); tt = k % T; }   // XCD = L mod 8
+    else { rt = L / T; tt = L % T; }
+    const int tok0 = tt * M5_BT, ntok = p.N;
+    const int row = rt * 128 + wave * 32 + r;
+    const int rr = row < sg.M ? row : sg.M - 1;
+    // 32-bit lane offsets from uniform bases (global loads in saddr form: no 64-bit
+    // address arithmetic per load; x < 4 GiB and a weight matrix < 4 GiB by the host check)
+    uint32_t xo[M5_NDMA];
+#pragma unroll
+    for (int d = 0; d < M5_NDMA; ++d) {
+        const int trow = (wave * M5_NDMA + d) * 4 + (lane >> 4);
+        const int t = tok0 + trow < ntok ? tok0 + trow : ntok - 1;
+        xo[d] = (uint32_t) t * (uint32_t) p.kp * 2u + 16u * (uint32_t) ((lane & 15) ^ (trow & 15));
+    }
+    const uint32_t wo = (uint32_t) rr * (uint32_t) sg.w_row;
+    f16v acc[2][M5_TT];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int t = 0; t < M5_TT; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[f][t][e] = 0.f;
+    const int nc = p.K / M4_KC;
+    // weight scales of the row pair, fixed for the whole K loop: the largest power of two
+    // <= 2^10 that keeps every scaled weight of the row below 2^15 (the lane pair of a row
+    // scans alternate super-blocks' d / dmin; k_mmq4's m4_range reaches the same scale
+    // chunk by chunk, rescaling its accumulators — 256 accumulators do not leave registers
+    // for that)
+    float ng = 0.f, nu = 0.f;
+    {
+        constexpr int BS = QT == GGML_TYPE_Q4_K ? 144 : 176;
+        const int nsb = p.K / 256;
+        for (int s0 = 0; s0 < nsb; s0 += 16) {
+            uint32_t vg[8], vu[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int sb = s0 + 2 * k + h;
+                vg[k] = sb < nsb ? *(const uint32_t *) (sg.w + (size_t) sb * BS + wo) : 0u;
+                vu[k] = sb < nsb ? *(const uint32_t *) (p.w2 + (size_t) sb * BS + wo) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                ng = __builtin_fmaxf(ng, m5_need<QT>(vg[k]));
+                nu = __builtin_fmaxf(nu, m5_need<QT>(vu[k]));
+            }
+        }
+        ng = __builtin_fmaxf(ng, __shfl_xor(ng, 32));
+        nu = __builtin_fmaxf(nu, __shfl_xor(nu, 32));
+    }
+    const float ws0 = m5_ws(ng), ws1 = m5_ws(nu);
+    constexpr int NW = m4_loads<QT>();
+    constexpr int NV = QT == GGML_TYPE_Q4_K ? 2 : 3;   // VALU per MFMA in the step schedule
+    auto dma_part = [&](int i, int d0, int nd) {
+        const int st = (i & 1) * M5_TILE;
+        const char * xb = (const char *) p.x + (size_t) i * (2 * M4_KC);
+#pragma unroll
+        for (int d = d0; d < d0 + nd; ++d)
+            __builtin_amdgcn_global_load_lds((const void *) (xb + xo[d]), (m4_lds_t) (lds + st + (wave * M5_NDMA + d) * 64), 16, 0, 0);
+    };
+    auto dma = [&](int i) {
+        if (MX_DBG(p.dbg & 4)) return;
+        dma_part(i, 0, M5_NDMA);
+    };
+    auto lda = [&](const uint4 * Ls, int j, int q, h8 (&a)[M5_TT]) {
+        const int ci = m4_ci<QT>(h, j, q) ^ (r & 15);
+#pragma unroll
+        for (int t = 0; t < M5_TT; ++t) {
+            const uint4 av = Ls[(32 * t + r) * 16 + ci];
+            __builtin_memcpy(&a[t], &av, 16);
+        }
+    };
+    // X bit 128 (g_tune[3] = 16; glu 151 -> 159 us, so not the default): chunk i + 1's activation DMA (4 pieces in each of steps 0-3)
+    // and chunk i + 2's weights (step 4) are issued between the MFMAs of chunk i — with one
+    // wave per SIMD a burst of them at the chunk head left the matrix pipe idle while they
+    // issued (~60-185 cycles per LDS-DMA piece, MI355X_MICROARCH.md). Past the end the
+    // loads are clamped to the last chunk (into the free slot / register set: no branch in
+    // the MFMA loop).
+    auto compute = [&](int i, const M4W<QT> & wg, const M4W<QT> & wu, M4W<QT> & ng, M4W<QT> & nu) {
+        const uint4 * Ls = lds + (i & 1) * M5_TILE;
+        h8 af[2][M5_TT];
+        lda(Ls, 0, 0, af[0]);
+        const M4Scale sg_[2] = {m4_scales<QT>(wg, i, h, 0, ws0), m4_scales<QT>(wg, i, h, 1, ws0)};
+        const M4Scale su_[2] = {m4_scales<QT>(wu, i, h, 0, ws1), m4_scales<QT>(wu, i, h, 1, ws1)};
+        h8 bg[2], bu[2];
+        bg[0] = m4_deq<QT, X>(wg, sg_[0], h, 0, 0);
+        bu[0] = m4_deq<QT, X>(wu, su_[0], h, 0, 0);
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+            h8 (&cur)[M5_TT] = af[st & 1];
+            if constexpr (X & 128) {
+                if (st < 4) dma_part(i + 1 < nc ? i + 1 : nc - 1, 4 * st, 4);
+                if (st == 4) {
+                    const int kw = i + 2 < nc ? i + 2 : nc - 1;
+                    m5_load<QT>(sg.w, wo, kw, h, ng); m5_load<QT>(p.w2, wo, kw, h, nu);
+                }
+            }
+            if (st + 1 < 8) {
+                const int j = (st + 1) >> 2, q = (st + 1) & 3;
+                lda(Ls, j, q, af[(st + 1) & 1]);
+                if constexpr (X & 2) {   // timing only: raw weight bits as the B operand
+                    const int4 a = j ? wg.q1 : wg.q0, b = j ? wu.q1 : wu.q0;
+                    __builtin_memcpy(&bg[(st + 1) & 1], &a, 16);
+                    __builtin_memcpy(&bu[(st + 1) & 1], &b, 16);
+                } else {
+                    bg[(st + 1) & 1] = m4_deq<QT, X>(wg, sg_[j], h, j, q);
+                    bu[(st + 1) & 1] = m4_deq<QT, X>(wu, su_[j], h, j, q);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < M5_TT; ++t) acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], bg[st & 1], acc[0][t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < M5_TT; ++t) acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], bu[st & 1], acc[1][t], 0, 0, 0);
+#if M5_SCHED
+#pragma unroll
+            for (int t = 0; t < M5_TT; ++t) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if ((X & 128) && ((st < 4 && t < 4) || (st == 4 && t < 2 * NW)))
+                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    };
+    M4W<QT> ga, ua, gb, ub, gc, uc;
+    dma(0);
+    __builtin_amdgcn_sched_barrier(0);
+    m5_load<QT>(sg.w, wo, 0, h, ga); m5_load<QT>(p.w2, wo, 0, h, ua);
+    if (nc > 1) { m5_load<QT>(sg.w, wo, 1, h, gb); m5_load<QT>(p.w2, wo, 1, h, ub); }
+    __builtin_amdgcn_sched_barrier(0);
+    // issued after DMA(i): the weights of chunk i + 1 (2 NW loads, at least); the wait also
+    // retires the weights of chunk i (issued before DMA(i))
+    auto iter = [&](int i, const M4W<QT> & cg, const M4W<QT> & cu, M4W<QT> & ng, M4W<QT> & nu) {
+        if constexpr (!(X & 1)) {
+            if (i + 1 < nc) m4_wait_vm<2 * NW>();
+            else m4_wait_vm<0>();
+            m4_barrier();   // DMA(i) of every wave landed; chunk i - 1's slot is free
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(X & 128)) {
+            if (i + 1 < nc) dma(i + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 2 < nc) {
+                const int kw = MX_DBG(p.dbg & 8) ? 0 : i + 2;
+                m5_load<QT>(sg.w, wo, kw, h, ng); m5_load<QT>(p.w2, wo, kw, h, nu);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        compute(i, cg, cu, ng, nu);
+    };
+    for (int i = 0; i < nc; i += 3) {
+        iter(i, ga, ua, gc, uc);
+        if (i + 1 < nc) iter(i + 1, gb, ub, ga, ua);
+        if (i + 2 < nc) iter(i + 2, gc, uc, gb, ub);
+    }
+    m4_wait_vm<0>();   // (the clamped loads past the end)
+    const float inv0 = 1.0f / ws0, inv1 = 1.0f / ws1;
+    if (row >= sg.M) return;
+    // raw buffer stores: the lane's 32-bit byte offset (the host checks both outputs
+    // < 4 GiB), no address arithmetic beyond one add per store, and the tokens past N
+    // dropped by the descriptor's range (num_records = N rows of the output) instead of a
+    // branch per store
+    const uint32_t lo = ((uint32_t) (tok0 + 4 * h) * (uint32_t) sg.d_col + (uint32_t) row) * 4u;
+    const uint32_t lh = ((uint32_t) (tok0 + 4 * h) * (uint32_t) p.h_col + (uint32_t) row) * 2u;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(sg.dst, 0, (int) ((uint32_t) ntok * (uint32_t) sg.d_col * 4u), 0x00020000);
+    auto store = [&](auto with_h) {
+        const __amdgpu_buffer_rsrc_t rh = with_h ? __builtin_amdgcn_make_buffer_rsrc(p.h, 0, (int) ((uint32_t) ntok * (uint32_t) p.h_col * 2u), 0x00020000) : rd;
+#pragma unroll
+        for (int t = 0; t < M5_TT; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const uint32_t tu = 32 * t + (e & 3) + 8 * (e >> 2);
+                const float g = acc[0][t][e] * inv0, u = acc[1][t][e] * inv1;
+                const float v = g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-g * 1.4426950408889634f)) * u;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rd, (int) (lo + tu * (uint32_t) sg.d_col * 4u), 0, 0);
+                if constexpr (decltype(with_h)::value) {
+                    const _Float16 hv = (_Float16) v;
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, hv), rh, (int) (lh + tu * (uint32_t) p.h_col * 2u), 0, 0);
+                }
+            }
+    };
+    if (p.h) store(std::true_type{});
+    else store(std::false_type{});
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static bool m4_kq(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
@@ -798,6 +1059,16 @@ bool mmq4_group(OpCtx & c, ggml_tensor * const * mms, int n, const _Float16 * xa
     return m4_dispatch<0>(c, a, ta, tb, tiles, 1, tt);
 }
 
+template <int QT, int X>
+static void m5_launch(hipStream_t st, const M4Args & a, dim3 g) {
+    static const bool attr = [] {
+        HIP_CHECK(hipFuncSetAttribute((const void *) k_mmq5_glu<QT, X>, hipFuncAttributeMaxDynamicSharedMemorySize, M5_LDS));
+        return true;
+    }();
+    (void) attr;
+    k_mmq5_glu<QT, X><<<g, 64 * M5_WAVES, M5_LDS, st>>>(a);
+}
+
 // silu(Wg·x) * (Wu·x) into glu (+ its f16 copy h for the down projection)
 bool mmq4_glu_ok(const ggml_tensor * wg, const ggml_tensor * wu, const ggml_tensor * x, const ggml_tensor * glu) {
     if (!mmq4_on() || !m4_weight_ok(wg, x->ne[0]) || !m4_weight_ok(wu, x->ne[0]) || wg->type != wu->type) return false;
@@ -814,6 +1085,31 @@ void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const g
     a.h = h; a.h_col = h_col;
     const int tiles = (int) mx_ceil_div(wg->ne[1], 16 * M4_WAVES), tt = m4_tt();
     MX_KLOG("mmq4 glu qt=%d tt=%d M=%lld N=%d K=%d", (int) wg->type, tt, (long long) wg->ne[1], a.N, a.K);
+    // k_mmq5 (256-token tiles) from 256 tokens on; g_tune[3] = 8 keeps k_mmq4
+    if (a.N >= M5_BT && g_tune[3] != 8 && wg->type == GGML_TYPE_Q4_K &&
+        (size_t) a.N * a.kp * 2 < (1ull << 32) && (size_t) wg->ne[1] * wg->nb[1] < (1ull << 32) &&
+        (size_t) a.N * glu->nb[1] < (1ull << 32) && (size_t) a.N * (size_t) h_col * 2 < (1ull << 32)) {
+        const int R = (int) mx_ceil_div(wg->ne[1], 128), T = (int) mx_ceil_div(a.N, M5_BT);
+        a.ksplit = 1;
+        const dim3 g((unsigned) (R * T));
+        if constexpr (MX_AB_VARIANTS) {
+            // timing experiments (results wrong): g_tune[31] 1 no wait + barrier, 2 no
+            // dequantisation; g_tune[19] 4 no activation DMA, 8 weights of chunk 0 only
+            a.dbg = g_tune[19];
+            switch (g_tune[31]) {
+                case 1: m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 1>(c.st, a, g); break;
+                case 2: m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 2>(c.st, a, g); break;
+                case 3: m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 3>(c.st, a, g); break;
+                default: m5_launch<GGML_TYPE_Q4_K, M5_XDEF>(c.st, a, g);
+            }
+        } else if (g_tune[3] == 16) {   // A/B: the next chunks' loads interleaved with the MFMAs
+            m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 128>(c.st, a, g);
+        } else {
+            m5_launch<GGML_TYPE_Q4_K, M5_XDEF>(c.st, a, g);
+        }
+        MX_KLOG("mmq4 launch epi=1 ks=1 planes=0 tiles=%d gx=%d wide=1", R, T);
+        return;
+    }
     MX_ASSERT(m4_dispatch<1>(c, a, wg->type, wg->type, tiles, 1, tt));
 }
 

@@ -198,6 +198,37 @@ def test_mmq4_glu(pkg, backend, orc, tname, N):
     check(y.reshape(N, M), orc.swiglu(g, u), rows_out)
 
 
+@pytest.mark.parametrize("M,N", [(300, 300), (1024, 512), (2048, 700)])
+@pytest.mark.parametrize("outlier", [False, True])
+def test_mmq5_glu(pkg, backend, orc, M, N, outlier):
+    """gate/up/SwiGLU from 256 tokens on: k_mmq5 (256-token tiles, one wave per SIMD, the
+    row pair's weight scale fixed up front from a scan of its super-block headers); M = 300
+    ragged rows (linear tile order), 1024 / 2048 (row tiles a multiple of 8: the XCD-aware
+    order), N ragged"""
+    tid = NAMES["q4_K"]
+    rng = np.random.default_rng(3 * M + N + outlier)
+    K = 2048
+    wg, rb = rand_quant(tid, M, K, rng)
+    wu, _ = rand_quant(tid, M, K, rng)
+    rows_out = []
+    if outlier:
+        wg, rows_out = with_outliers(wg, tid, M, K, rng)
+        wu, _ = with_outliers(wu, tid, M, K, rng)
+    x = rng.standard_normal((N, K)).astype(np.float32)
+
+    def build(ctx):
+        tg = ctx.new_tensor(tid, K, M)
+        tu = ctx.new_tensor(tid, K, M)
+        tx = ctx.new_tensor("f32", K, N)
+        return [ctx.swiglu_split(ctx.mul_mat(tg, tx), ctx.mul_mat(tu, tx))], [(tg, wg), (tu, wu), (tx, x)]
+
+    (y,), log = run(pkg, backend, build)
+    assert klog_has(launch_lines(log), lambda l: "epi=1 " in l and "wide=1" in l), log
+    g = orc.mul_mat(tid, wg, rb, x, exact=True)
+    u = orc.mul_mat(tid, wu, rb, x, exact=True)
+    check(y.reshape(N, M), orc.swiglu(g, u), rows_out)
+
+
 @pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K"])
 def test_mmq4_moe(pkg, backend, orc, tname):
     """MUL_MAT_ID prefill: items sorted by expert on the device, ONE k_mmq4 launch of

@@ -72,14 +72,16 @@ def case_gemm(pkg, be, rng, tname, K, M, N=512):
     """prefill GEMM: M weight rows x N tokens over K."""
     tid = NAMES[tname]
     w, _ = rand_quant(tid, M, K, rng)
+    n = copies_for(len(w))
     ctx = pkg.Context()
     x = ctx.new_tensor("f32", K, N)
-    tw = ctx.new_tensor(tid, K, M)
-    g = ctx.build(ctx.mul_mat(tw, x))
+    tws = [ctx.new_tensor(tid, K, M) for _ in range(n)]
+    gs = [ctx.build(ctx.mul_mat(tw, x)) for tw in tws]
     ctx.alloc(be)
-    tw.set(w)
+    for tw in tws:
+        tw.set(w)
     x.set(rng.standard_normal((N, K)).astype(np.float32))
-    return ctx, [g]
+    return ctx, gs
 
 
 def case_gemm_qkv(pkg, be, rng, K=4096, Mq=4096, Mkv=1024, tv="q4_K", N=512):
@@ -88,29 +90,33 @@ def case_gemm_qkv(pkg, be, rng, K=4096, Mq=4096, Mkv=1024, tv="q4_K", N=512):
     wq, _ = rand_quant(tq, Mq, K, rng)
     wk, _ = rand_quant(tq, Mkv, K, rng)
     wv, _ = rand_quant(NAMES[tv], Mkv, K, rng)
+    n = copies_for(len(wq) + len(wk) + len(wv))
     ctx = pkg.Context()
     x = ctx.new_tensor("f32", K, N)
-    a, b, c = ctx.new_tensor(tq, K, Mq), ctx.new_tensor(tq, K, Mkv), ctx.new_tensor(NAMES[tv], K, Mkv)
-    g = ctx.build(ctx.mul_mat(a, x), ctx.mul_mat(b, x), ctx.mul_mat(c, x))
+    sets = [(ctx.new_tensor(tq, K, Mq), ctx.new_tensor(tq, K, Mkv), ctx.new_tensor(NAMES[tv], K, Mkv)) for _ in range(n)]
+    gs = [ctx.build(ctx.mul_mat(a, x), ctx.mul_mat(b, x), ctx.mul_mat(c, x)) for a, b, c in sets]
     ctx.alloc(be)
-    a.set(wq); b.set(wk); c.set(wv)
+    for a, b, c in sets:
+        a.set(wq); b.set(wk); c.set(wv)
     x.set(rng.standard_normal((N, K)).astype(np.float32))
-    return ctx, [g]
+    return ctx, gs
 
 
 def case_gemm_glu(pkg, be, rng, tname, K, M, N=512):
     """prefill gate/up/SwiGLU GEMM pair (fused): 2 x M weight rows x N tokens over K."""
     tid = NAMES[tname]
     wg, _ = rand_quant(tid, M, K, rng)
+    n = copies_for(2 * len(wg))
     ctx = pkg.Context()
     x = ctx.new_tensor("f32", K, N)
-    tg, tu = ctx.new_tensor(tid, K, M), ctx.new_tensor(tid, K, M)
-    g = ctx.build(ctx.swiglu_split(ctx.mul_mat(tg, x), ctx.mul_mat(tu, x)))
+    pairs = [(ctx.new_tensor(tid, K, M), ctx.new_tensor(tid, K, M)) for _ in range(n)]
+    gs = [ctx.build(ctx.swiglu_split(ctx.mul_mat(tg, x), ctx.mul_mat(tu, x))) for tg, tu in pairs]
     ctx.alloc(be)
-    tg.set(wg)
-    tu.set(wg)
+    for tg, tu in pairs:
+        tg.set(wg)
+        tu.set(wg)
     x.set(rng.standard_normal((N, K)).astype(np.float32))
-    return ctx, [g]
+    return ctx, gs
 
 
 def case_moe(pkg, be, rng, tname="q5_K", K=4096, M=14336, n_exp=8, used=2, T=512, skew=0.0):
