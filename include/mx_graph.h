@@ -68,6 +68,7 @@ void mxg_expand(mxg_context * ctx, struct ggml_cgraph * g, struct ggml_tensor * 
 
 /* allocate every tensor of ctx that has no data yet into one buffer of `buft` */
 int  mxg_alloc(mxg_context * ctx, ggml_backend_buffer_type_t buft);
+size_t mxg_alloc_bytes(const mxg_context * ctx);   /* device bytes of the buffers mxg_alloc created */
 void mxg_tensor_set(struct ggml_tensor * t, const void * data, size_t offset, size_t size);
 void mxg_tensor_get(const struct ggml_tensor * t, void * data, size_t offset, size_t size);
 size_t mxg_nbytes(const struct ggml_tensor * t);

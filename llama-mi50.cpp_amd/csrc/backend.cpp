@@ -549,9 +549,11 @@ Stream * mx_aux_stream(int logical) {
 // GGML_MI355X_SEGV_TRACE=<file>|1: on SIGSEGV/SIGBUS write the faulting PC and address, every
 // frame as module+offset (dladdr: stripped ROCm libraries still resolve to a module and an
 // offset that addr2line / llvm-symbolizer can turn into a symbol offline) and the
-// /proc/self/maps lines, then re-raise. Diagnostics only (the handler is not strictly
-// async-signal-safe); installed after a profiler's own handler, so it runs first.
+// /proc/self/maps lines, then hand the signal to the handler that was installed before
+// (a profiler's, say: restored and re-raised) or to the default action. Diagnostics only
+// (the handler is not strictly async-signal-safe).
 static int g_segv_fd = 2;
+static struct sigaction g_segv_prev[2];   // SIGSEGV, SIGBUS
 static void segv_write(const char * s) { if (write(g_segv_fd, s, strlen(s)) < 0) {} }
 static void segv_handler(int sig, siginfo_t * si, void * uc) {
     char line[512];
@@ -579,7 +581,9 @@ static void segv_handler(int sig, siginfo_t * si, void * uc) {
         while ((k = read(mf, buf, sizeof buf)) > 0) if (write(g_segv_fd, buf, (size_t) k) < 0) break;
         close(mf);
     }
-    signal(sig, SIG_DFL);
+    // chain: put back what was installed before this handler and re-raise (the fault
+    // re-triggers on return for a synchronous SIGSEGV; raise covers the rest)
+    sigaction(sig, &g_segv_prev[sig == SIGBUS], nullptr);
     raise(sig);
 }
 static void segv_trace_install() {
@@ -590,8 +594,8 @@ static void segv_trace_install() {
     sa.sa_sigaction = segv_handler;
     sa.sa_flags = SA_SIGINFO;
     sigemptyset(&sa.sa_mask);
-    sigaction(SIGSEGV, &sa, nullptr);
-    sigaction(SIGBUS, &sa, nullptr);
+    sigaction(SIGSEGV, &sa, &g_segv_prev[0]);
+    sigaction(SIGBUS, &sa, &g_segv_prev[1]);
 }
 
 void klog_env_init();

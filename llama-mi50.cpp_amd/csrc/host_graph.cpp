@@ -377,6 +377,12 @@ int mxg_alloc(mxg_context * ctx, ggml_backend_buffer_type_t buft) {
     return 0;
 }
 
+size_t mxg_alloc_bytes(const mxg_context * ctx) {
+    size_t n = 0;
+    for (auto b : ctx->buffers) n += b->size;
+    return n;
+}
+
 void mxg_tensor_set(ggml_tensor * t, const void * data, size_t offset, size_t size) {
     MX_ASSERT(t->buffer && t->data);
     t->buffer->iface.set_tensor(t->buffer, t, data, offset, size);

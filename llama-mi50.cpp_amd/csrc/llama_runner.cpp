@@ -603,19 +603,43 @@ static GraphInst * build_graph(mxr_context * c, int n_tokens, int n_kv, int n_ou
     return raw;
 }
 
+// Graph instances are cached by shape (n_tokens, n_kv, n_out); each holds its own
+// intermediates and inputs (no buffer sharing between instances: one graph per shape can be
+// replayed without re-planning). Bounded by count AND bytes: GGML_MI355X_RUNNER_GRAPHS (default
+// 6 — a pp2048 prompt alone has 4 shapes, n_kv 512 .. 2048) and GGML_MI355X_RUNNER_GRAPH_MB
+// (default 32768). Llama-3-8B pp512 ubatch ≈ 4.4 GB per instance, 70B ≈ 22 GB: at 70B the
+// byte bound keeps one or two.
+static size_t runner_env(const char * name, size_t dflt) {
+    const char * v = getenv(name);
+    return v && *v ? (size_t) strtoull(v, nullptr, 10) : dflt;
+}
+
 static GraphInst * get_graph(mxr_context * c, int n_tokens, int n_kv, int n_out) {
     for (auto & g : c->graphs)
         if (g->n_tokens == n_tokens && g->n_kv == n_kv && g->n_out == n_out) { g->last_use = ++c->tick; return g.get(); }
-    if (c->graphs.size() >= 6) {  // evict least recently used (a pp2048 prompt alone has 4 shapes: n_kv 512 .. 2048)
-        size_t victim = 0;
-        for (size_t i = 1; i < c->graphs.size(); ++i) if (c->graphs[i]->last_use < c->graphs[victim]->last_use) victim = i;
+    static const size_t max_n = std::max<size_t>(1, runner_env("GGML_MI355X_RUNNER_GRAPHS", 6));
+    static const size_t max_b = runner_env("GGML_MI355X_RUNNER_GRAPH_MB", 32768) << 20;
+    auto evict_lru = [&](const GraphInst * keep) {
+        size_t victim = SIZE_MAX;
+        for (size_t i = 0; i < c->graphs.size(); ++i)
+            if (c->graphs[i].get() != keep && (victim == SIZE_MAX || c->graphs[i]->last_use < c->graphs[victim]->last_use)) victim = i;
+        if (victim == SIZE_MAX) return false;
         mxg_synchronize(c->m->be);
         mxg_free(c->graphs[victim]->ctx);
         mxg_free(c->graphs[victim]->ictx);
         c->graphs.erase(c->graphs.begin() + victim);
-    }
+        return true;
+    };
+    while (c->graphs.size() >= max_n && evict_lru(nullptr)) {}
     GraphInst * g = build_graph(c, n_tokens, n_kv, n_out);
-    if (g) g->last_use = ++c->tick;
+    if (!g) return g;
+    g->last_use = ++c->tick;
+    auto bytes = [&] {
+        size_t b = 0;
+        for (auto & x : c->graphs) b += mxg_alloc_bytes(x->ctx) + mxg_alloc_bytes(x->ictx);
+        return b;
+    };
+    while (c->graphs.size() > 1 && bytes() > max_b && evict_lru(g)) {}
     return g;
 }
 

@@ -647,6 +647,8 @@ __global__ void k_mmq4_reduce(M4Args p) {
 #define M5_SCHED 1
 #endif
 constexpr int M5_WAVES = 4, M5_TT = M5TT_, M5_BT = 32 * M5_TT;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 constexpr int M5_TILE = M5_BT * 16;                  // uint4 per ring slot (64 KB)
 constexpr int M5_NDMA = M5_BT / 4 / M5_WAVES;        // 1-KB LDS-DMA pieces per wave per chunk
 constexpr int M5_LDS = 2 * M5_TILE * 16;
@@ -747,6 +749,11 @@ void k_mmq5_glu(M4Args p) {
         nu = __builtin_fmaxf(nu, __shfl_xor(nu, 32));
     }
     const float ws0 = m5_ws(ng), ws1 = m5_ws(nu);
+    // X bit 256 (diagnostic builds): cycle sums per wave of workgroup 0 — prologue, chunk-head
+    // wait + barrier, chunk compute, epilogue (s_memtime; opbench --trace)
+    unsigned long long t_k0 = 0, t_loop = 0, t_wait = 0, t_comp = 0, t_a = 0;
+    const bool trw = (X & 256) && p.trace && L == 0;
+    if constexpr (X & 256) t_k0 = __builtin_amdgcn_s_memtime();
     constexpr int NW = m4_loads<QT>();
     constexpr int NV = QT == GGML_TYPE_Q4_K ? 2 : 3;   // VALU per MFMA in the step schedule
     auto dma_part = [&](int i, int d0, int nd) {
@@ -806,9 +813,13 @@ void k_mmq5_glu(M4Args p) {
                 }
             }
 #pragma unroll
-            for (int t = 0; t < M5_TT; ++t) acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], bg[st & 1], acc[0][t], 0, 0, 0);
+            for (int t = 0; t < M5_TT; ++t)
+                acc[0][t] = (X & 512) ? __builtin_amdgcn_mfma_f32_32x32x16_f16(bg[st & 1], cur[t], acc[0][t], 0, 0, 0)
+                                      : __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], bg[st & 1], acc[0][t], 0, 0, 0);
 #pragma unroll
-            for (int t = 0; t < M5_TT; ++t) acc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], bu[st & 1], acc[1][t], 0, 0, 0);
+            for (int t = 0; t < M5_TT; ++t)
+                acc[1][t] = (X & 512) ? __builtin_amdgcn_mfma_f32_32x32x16_f16(bu[st & 1], cur[t], acc[1][t], 0, 0, 0)
+                                      : __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[t], bu[st & 1], acc[1][t], 0, 0, 0);
 #if M5_SCHED
 #pragma unroll
             for (int t = 0; t < M5_TT; ++t) {
@@ -833,6 +844,7 @@ void k_mmq5_glu(M4Args p) {
     // issued after DMA(i): the weights of chunk i + 1 (2 NW loads, at least); the wait also
     // retires the weights of chunk i (issued before DMA(i))
     auto iter = [&](int i, const M4W<QT> & cg, const M4W<QT> & cu, M4W<QT> & ng, M4W<QT> & nu) {
+        if constexpr (X & 256) { __builtin_amdgcn_sched_barrier(0); t_a = __builtin_amdgcn_s_memtime(); if (i == 0) t_loop = t_a; }
         if constexpr (!(X & 1)) {
             if (i + 1 < nc) m4_wait_vm<2 * NW>();
             else m4_wait_vm<0>();
@@ -848,7 +860,9 @@ void k_mmq5_glu(M4Args p) {
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (X & 256) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t = __builtin_amdgcn_s_memtime(); t_wait += t - t_a; t_a = t; }
         compute(i, cg, cu, ng, nu);
+        if constexpr (X & 256) { __builtin_amdgcn_sched_barrier(0); t_comp += __builtin_amdgcn_s_memtime() - t_a; }
     };
     for (int i = 0; i < nc; i += 3) {
         iter(i, ga, ua, gc, uc);
@@ -856,6 +870,51 @@ void k_mmq5_glu(M4Args p) {
         if (i + 2 < nc) iter(i + 2, gc, uc, gb, ub);
     }
     m4_wait_vm<0>();   // (the clamped loads past the end)
+    if constexpr (X & 512) {
+        // weights as the A operand (X bit 512): the accumulators are D[row][token] — lane
+        // (r, h) holds token 32t + r and rows 8g + 4h + 0..3 of the wave's 32 (g = e >> 2),
+        // i.e. four consecutive output floats: one 16-byte store (and one 8-byte f16 store)
+        // per four values instead of four 4-byte (and four 2-byte) ones. The rows' weight
+        // scales come from the lanes that scanned them.
+        float ig[4][4], iu[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                ig[g][c] = 1.0f / __shfl(ws0, 8 * g + 4 * h + c);
+                iu[g][c] = 1.0f / __shfl(ws1, 8 * g + 4 * h + c);
+            }
+        const int rbase = rt * 128 + wave * 32 + 4 * h;          // + 8 g
+        const bool rows_full = rt * 128 + 128 <= sg.M;
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(sg.dst, 0, (int) ((uint32_t) ntok * (uint32_t) sg.d_col * 4u), 0x00020000);
+        const uint32_t lo = ((uint32_t) (tok0 + r) * (uint32_t) sg.d_col + (uint32_t) rbase) * 4u;
+        const uint32_t lh = ((uint32_t) (tok0 + r) * (uint32_t) p.h_col + (uint32_t) rbase) * 2u;
+        auto store = [&](auto with_h) {
+            const __amdgpu_buffer_rsrc_t rh = with_h ? __builtin_amdgcn_make_buffer_rsrc(p.h, 0, (int) ((uint32_t) ntok * (uint32_t) p.h_col * 2u), 0x00020000) : rd;
+#pragma unroll
+            for (int t = 0; t < M5_TT; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    float v[4];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const float a = acc[0][t][4 * g + c] * ig[g][c], b = acc[1][t][4 * g + c] * iu[g][c];
+                        v[c] = a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-a * 1.4426950408889634f)) * b;
+                    }
+                    if (!rows_full && rbase + 8 * g >= sg.M) continue;   // (M % 4 == 0: whole groups)
+                    const uint32_t ot = 32u * t;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rd, (int) (lo + (ot * (uint32_t) sg.d_col + 8u * g) * 4u), 0, 0);
+                    if constexpr (decltype(with_h)::value) {
+                        const h2 p0 = {(_Float16) v[0], (_Float16) v[1]}, p1 = {(_Float16) v[2], (_Float16) v[3]};
+                        v2u hv = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+                        __builtin_amdgcn_raw_buffer_store_b64(hv, rh, (int) (lh + (ot * (uint32_t) p.h_col + 8u * g) * 2u), 0, 0);
+                    }
+                }
+        };
+        if (p.h) store(std::true_type{});
+        else store(std::false_type{});
+        return;
+    }
     const float inv0 = 1.0f / ws0, inv1 = 1.0f / ws1;
     if (row >= sg.M) return;
     // raw buffer stores: the lane's 32-bit byte offset (the host checks both outputs
@@ -883,6 +942,14 @@ void k_mmq5_glu(M4Args p) {
     };
     if (p.h) store(std::true_type{});
     else store(std::false_type{});
+    if constexpr (X & 256) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        if (trw && lane == 0) {
+            unsigned long long * tr = p.trace + wave * 8;
+            tr[0] = 1; tr[1] = 1 + t_loop - t_k0; tr[2] = 1 + t_wait; tr[3] = 1 + t_comp;
+            tr[4] = 1 + t_end - t_loop - t_wait - t_comp; tr[5] = 1 + nc;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1092,10 +1159,16 @@ void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const g
         const int R = (int) mx_ceil_div(wg->ne[1], 128), T = (int) mx_ceil_div(a.N, M5_BT);
         a.ksplit = 1;
         const dim3 g((unsigned) (R * T));
+        // 16-byte row-vector stores: rows in whole groups of four, 16- / 8-byte aligned
+        const bool vec_ok = wg->ne[1] % 4 == 0 && (a.seg[0].d_col % 4) == 0 && ((uintptr_t) glu->data % 16) == 0 &&
+                            (!h || (h_col % 4 == 0 && (uintptr_t) h % 8 == 0));
         if constexpr (MX_AB_VARIANTS) {
             // timing experiments (results wrong): g_tune[31] 1 no wait + barrier, 2 no
             // dequantisation; g_tune[19] 4 no activation DMA, 8 weights of chunk 0 only
             a.dbg = g_tune[19];
+            a.trace = mx_trace_slot(3);
+            if (a.trace && g_tune[3] == 32 && vec_ok) { m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 256 | 512>(c.st, a, g); goto m5_done; }
+            if (a.trace) { m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 256>(c.st, a, g); goto m5_done; }
             switch (g_tune[31]) {
                 case 1: m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 1>(c.st, a, g); break;
                 case 2: m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 2>(c.st, a, g); break;
@@ -1104,9 +1177,12 @@ void mmq4_glu(OpCtx & c, const ggml_tensor * wg, const ggml_tensor * wu, const g
             }
         } else if (g_tune[3] == 16) {   // A/B: the next chunks' loads interleaved with the MFMAs
             m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 128>(c.st, a, g);
+        } else if (g_tune[3] == 32 && vec_ok) {   // A/B: weights as the A operand, 16-byte stores
+            m5_launch<GGML_TYPE_Q4_K, M5_XDEF | 512>(c.st, a, g);
         } else {
             m5_launch<GGML_TYPE_Q4_K, M5_XDEF>(c.st, a, g);
         }
+    m5_done:
         MX_KLOG("mmq4 launch epi=1 ks=1 planes=0 tiles=%d gx=%d wide=1", R, T);
         return;
     }
