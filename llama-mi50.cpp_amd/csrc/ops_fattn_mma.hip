@@ -13,6 +13,7 @@
 // the same MFMA. Key tiles the mask removes entirely (the causal upper triangle) are
 // skipped.
 #include "backend.h"
+#include "gemv.h"
 
 namespace mx {
 
@@ -249,19 +250,27 @@ __device__ __forceinline__ int fm2_off(int row, int ch) {     // byte offset in 
 // one key chunk fall on 32 distinct bank pairs
 __device__ __forceinline__ int vt_off(int row, int q) { return 128 * row + 8 * (q ^ ((row >> 1) & 15)); }
 
-template <int HG, bool VT = false>
+// KS (key split, round 4): the four waves are 2 heads x 2 key halves of 32 queries — waves
+// 0-1 take the even 64-key tiles, 2-3 the odd ones (two tiles staged per iteration), and
+// the halves' (O, m, l) are merged through LDS at the end. At pp512 the HG = 4 grid was
+// n_q / 32 x Hkv = 128 workgroups of 4 waves = 512 waves for 1,024 SIMDs, and the causal
+// last query block walked all 8 tiles alone; split, 256 workgroups, 4 tiles at most per wave.
+template <int HG, bool VT = false, bool KS = false>
 __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
     constexpr int D = 128, NKS = D / 16, NDT = D / 32;
-    constexpr int QB = 32 * (4 / HG);                          // queries per workgroup
-    __shared__ __align__(16) char ks[FM_KT * 256];
-    __shared__ __align__(16) char vs[FM_KT * 256];
+    static_assert(!KS || HG == 2, "key split: 2 heads x 2 key halves");
+    constexpr int QB = KS ? 32 : 32 * (4 / HG);                // queries per workgroup
+    constexpr int NB = KS ? 2 : 1;                             // K/V tiles staged per iteration
+    __shared__ __align__(16) char ks[NB * FM_KT * 256];
+    __shared__ __align__(16) char vs[NB * FM_KT * 256];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l32 = lane & 31, hl = lane >> 5;
     const int Gt = p.H / p.Hkv, NGB = Gt / HG;
     const int hk = blockIdx.y / NGB;
     const int h = hk * Gt + (blockIdx.y % NGB) * HG + wave % HG;
-    const int qw = blockIdx.x * QB + 32 * (wave / HG);          // this wave's first query
+    const int khalf = KS ? wave >> 1 : 0;                       // KS: this wave's tile parity
+    const int qw = blockIdx.x * QB + (KS ? 0 : 32 * (wave / HG));   // this wave's first query
     const int qr = min(qw + l32, p.n_q - 1);                   // this lane's query (clamped)
     const char * kb = p.k + (size_t) hk * p.k2;
     const char * vb = p.v + (size_t) hk * p.v2;
@@ -318,8 +327,10 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
     // VT: V^T rows (one per dimension, 64 keys = 128 B, p.v1 = the dimension stride): thread
     // tid + 256 j loads keys 8 (u & 7) .. +7 of dimension u >> 3 (n_kv % 64 == 0: no clamp)
     uint4 kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3;
+    uint4 kq0, kq1, kq2, kq3, vq0, vq1, vq2, vq3;               // KS: the odd tile
 #define FM2_VT_SRC(KT, J) (vb + ((size_t) ((tid + 256 * (J)) >> 3) * p.v1 + (size_t) (2 * ((KT) * FM_KT + 8 * ((tid + 256 * (J)) & 7)))))
-#define FM2_LOAD_KV(KT, LIVE) do { \
+#define FM2_LOAD_KV(KT, LIVE) FM2_LOAD_KV_INTO(KT, LIVE, kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3)
+#define FM2_LOAD_KV_INTO(KT, LIVE, kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3) do { \
         const int kt_ = (KT); const bool lv_ = (LIVE); \
         const size_t r0_ = (size_t) min(kt_ * FM_KT + (tid >> 4), p.n_kv - 1), r1_ = (size_t) min(kt_ * FM_KT + 16 + (tid >> 4), p.n_kv - 1); \
         const size_t r2_ = (size_t) min(kt_ * FM_KT + 32 + (tid >> 4), p.n_kv - 1), r3_ = (size_t) min(kt_ * FM_KT + 48 + (tid >> 4), p.n_kv - 1); \
@@ -345,40 +356,58 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
     float m_run = -INFINITY, l_run = 0.f;                       // l_run: this half's keys only
 
     const int n_tiles = (p.n_kv + FM_KT - 1) / FM_KT;
+    const int n_it = KS ? (n_tiles + 1) / 2 : n_tiles;
     // software pipeline, one tile deep: tile kt+1's K/V rows and mask words are loaded
     // while tile kt computes. The load destinations are consumed (mask fixed into mA,
     // K/V stored to LDS) before they are reloaded, so no register copy waits on them.
+    // KS: iteration it stages tiles 2 it (buffer 0) and 2 it + 1 (buffer 1, clamped for the
+    // load; its mask index is not clamped, so a tile past the end is dead for waves 2-3)
     uint2 mreg[8], mA[8];
+    auto my_tile = [&](int it) { return KS ? 2 * it + khalf : it; };
     FM2_LOAD_KV(0, true);
-    load_mask(0, mreg);
-    for (int kt = 0; kt < n_tiles; ++kt) {
+    if constexpr (KS) FM2_LOAD_KV_INTO(min(1, n_tiles - 1), true, kq0, kq1, kq2, kq3, vq0, vq1, vq2, vq3);
+    load_mask(min(my_tile(0), n_tiles - 1), mreg);
+    auto store_kv = [&](char * kd, char * vd, const uint4 & k0, const uint4 & k1, const uint4 & k2, const uint4 & k3,
+                        const uint4 & v0, const uint4 & v1, const uint4 & v2, const uint4 & v3) {
+        const int row = tid >> 4, ch = tid & 15;
+        *(uint4 *) (kd + fm2_off(row, ch)) = k0;
+        *(uint4 *) (kd + fm2_off(row + 16, ch)) = k1;
+        *(uint4 *) (kd + fm2_off(row + 32, ch)) = k2;
+        *(uint4 *) (kd + fm2_off(row + 48, ch)) = k3;
+        if constexpr (VT) {
+            const uint4 vv[4] = {v0, v1, v2, v3};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int u = tid + 256 * j, d = u >> 3, c = u & 7;
+                *(uint2 *) (vd + vt_off(d, 2 * c)) = make_uint2(vv[j].x, vv[j].y);
+                *(uint2 *) (vd + vt_off(d, 2 * c + 1)) = make_uint2(vv[j].z, vv[j].w);
+            }
+        } else {
+            *(uint4 *) (vd + fm2_off(row, ch)) = v0;
+            *(uint4 *) (vd + fm2_off(row + 16, ch)) = v1;
+            *(uint4 *) (vd + fm2_off(row + 32, ch)) = v2;
+            *(uint4 *) (vd + fm2_off(row + 48, ch)) = v3;
+        }
+    };
+    const char * const ksw = ks + khalf * FM_KT * 256;          // this wave's tile buffer
+    const char * const vsw = vs + khalf * FM_KT * 256;
+    for (int it = 0; it < n_it; ++it) {
+        const int kt = my_tile(it);
 #pragma unroll
         for (int i = 0; i < 8; ++i) mA[i] = mreg[i];
         fix_mask(kt, mA);
-        {
-            const int row = tid >> 4, ch = tid & 15;
-            *(uint4 *) (ks + fm2_off(row, ch)) = kr0;
-            *(uint4 *) (ks + fm2_off(row + 16, ch)) = kr1;
-            *(uint4 *) (ks + fm2_off(row + 32, ch)) = kr2;
-            *(uint4 *) (ks + fm2_off(row + 48, ch)) = kr3;
-            if constexpr (VT) {
-                const uint4 vv[4] = {vr0, vr1, vr2, vr3};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int u = tid + 256 * j, d = u >> 3, c = u & 7;
-                    *(uint2 *) (vs + vt_off(d, 2 * c)) = make_uint2(vv[j].x, vv[j].y);
-                    *(uint2 *) (vs + vt_off(d, 2 * c + 1)) = make_uint2(vv[j].z, vv[j].w);
-                }
-            } else {
-                *(uint4 *) (vs + fm2_off(row, ch)) = vr0;
-                *(uint4 *) (vs + fm2_off(row + 16, ch)) = vr1;
-                *(uint4 *) (vs + fm2_off(row + 32, ch)) = vr2;
-                *(uint4 *) (vs + fm2_off(row + 48, ch)) = vr3;
-            }
+        store_kv(ks, vs, kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3);
+        if constexpr (KS) store_kv(ks + FM_KT * 256, vs + FM_KT * 256, kq0, kq1, kq2, kq3, vq0, vq1, vq2, vq3);
+        bool live_cur;
+        if constexpr (KS) { __syncthreads(); live_cur = __any(any_live(mA)); }   // per wave (its own tile)
+        else live_cur = __syncthreads_or(any_live(mA));          // + the tiles are visible
+        if constexpr (KS) {
+            FM2_LOAD_KV(min(2 * it + 2, n_tiles - 1), true);
+            FM2_LOAD_KV_INTO(min(2 * it + 3, n_tiles - 1), true, kq0, kq1, kq2, kq3, vq0, vq1, vq2, vq3);
+        } else {
+            FM2_LOAD_KV(min(kt + 1, n_tiles - 1), true);
         }
-        const bool live_cur = __syncthreads_or(any_live(mA));   // + the tiles are visible
-        FM2_LOAD_KV(min(kt + 1, n_tiles - 1), true);
-        load_mask(min(kt + 1, n_tiles - 1), mreg);
+        load_mask(min(my_tile(it + 1), n_tiles - 1), mreg);
         if (live_cur) {
             // ---- S^T = K Q^T: 64 keys (2 blocks of 32) x this wave's 32 queries
             ffloat16v acc_s[2];
@@ -390,7 +419,7 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
             for (int s = 0; s < NKS; ++s)
 #pragma unroll
                 for (int n = 0; n < 2; ++n) {
-                    const fhalf8 kf = *(const fhalf8 *) (ks + fm2_off(32 * n + l32, 2 * s + hl));
+                    const fhalf8 kf = *(const fhalf8 *) (ksw + fm2_off(32 * n + l32, 2 * s + hl));
                     acc_s[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qa[s], acc_s[n], 0, 0, 0);
                 }
             // ---- online softmax of this lane's query over its 32 keys + the partner half's,
@@ -445,12 +474,12 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
                     fhalf4 lo, hi;
                     if constexpr (VT) {   // A row = dimension 32 t + l32; its keys 4 hl + (0..3) and 8 + 4 hl + (0..3)
                         const int d = 32 * t + l32, q = 8 * (s >> 1) + 4 * (s & 1) + hl;
-                        lo = *(const fhalf4 *) (vs + vt_off(d, q));
-                        hi = *(const fhalf4 *) (vs + vt_off(d, q + 2));
+                        lo = *(const fhalf4 *) (vsw + vt_off(d, q));
+                        hi = *(const fhalf4 *) (vsw + vt_off(d, q + 2));
                     } else {
                         const int c0 = 4 * t + 2 * (g & 1) + (ip >> 1);
-                        lo = lds_tr16(vs + fm2_off(r0, c0) + 8 * (ip & 1));
-                        hi = lds_tr16(vs + fm2_off(r0 + 8, c0) + 8 * (ip & 1));
+                        lo = lds_tr16(vsw + fm2_off(r0, c0) + 8 * (ip & 1));
+                        hi = lds_tr16(vsw + fm2_off(r0 + 8, c0) + 8 * (ip & 1));
                     }
                     const fhalf8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                     acc_o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pb[s], acc_o[t], 0, 0, 0);
@@ -458,6 +487,32 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
             }
         }
         __syncthreads();                                        // K/V tiles are rewritten next
+    }
+    if constexpr (KS) {
+        // merge the odd-tile half into the even one: waves 2-3 leave (O, m, l) in LDS (the
+        // tile buffers are free after the loop's last barrier), waves 0-1 rescale both to
+        // the larger reference max and add
+        float * xo = (float *) ks;                              // [2 heads][NDT * 16][64 lanes]
+        float * xm = (float *) vs;                              // [2 heads][2][64 lanes]
+        if (khalf) {
+#pragma unroll
+            for (int t = 0; t < NDT; ++t)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) xo[((wave & 1) * NDT * 16 + t * 16 + e) * 64 + lane] = acc_o[t][e];
+            xm[((wave & 1) * 2 + 0) * 64 + lane] = m_run;
+            xm[((wave & 1) * 2 + 1) * 64 + lane] = l_run;
+        }
+        __syncthreads();
+        if (khalf) return;
+        const float m1 = xm[((wave & 1) * 2 + 0) * 64 + lane], l1 = xm[((wave & 1) * 2 + 1) * 64 + lane];
+        const float mm = fmaxf(m_run, m1);
+        const float a0 = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_run - mm);
+        const float a1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m1 - mm);
+        l_run = l_run * a0 + l1 * a1;
+#pragma unroll
+        for (int t = 0; t < NDT; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc_o[t][e] = acc_o[t][e] * a0 + xo[((wave & 1) * NDT * 16 + t * 16 + e) * 64 + lane] * a1;
     }
     // ---- normalise and store: lane = query l32, rows d = 32 t + 8 g + 4 hl + (0..3)
     const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -482,8 +537,12 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
         }
     }
 #undef FM2_LOAD_KV
+#undef FM2_LOAD_KV_INTO
 #undef FM2_VT_SRC
 }
+
+// the key-split form (KS above) for GQA groups of an even size; g_tune[0] = 1 keeps HG = 4
+static bool fa_key_split(int Gt) { return Gt % 2 == 0 && g_tune[0] != 1; }
 
 bool fa_mma_ok(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0];
@@ -535,6 +594,12 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
         // contiguous [D, H, n_q] output: the output projection reads it as [H*D, n_q] rows
         if (dst->nb[1] == 4 * (size_t) k->ne[0] && dst->nb[2] == (size_t) 4 * k->ne[0] * p.H && dst->ne[3] == 1)
             p.h = mmq_act_claim(c, dst->data, k->ne[0] * p.H, p.n_q, dst->nb[2]);
+        if (fa_key_split(Gt)) {   // 2 heads x 2 key halves per workgroup (g_tune[0] = 1: off)
+            const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32), (unsigned) (p.Hkv * (Gt / 2)));
+            MX_KLOG("fa_mma2 HG=2 ks=2 n_q=%d n_kv=%d H=%d Hkv=%d", p.n_q, p.n_kv, p.H, p.Hkv);
+            k_fa_mma2<2, false, true><<<g2, 256, 0, c.st>>>(p);
+            return;
+        }
         const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32 * (4 / HG)), (unsigned) (p.Hkv * (Gt / HG)));
         MX_KLOG("fa_mma2 HG=%d n_q=%d n_kv=%d H=%d Hkv=%d", HG, p.n_q, p.n_kv, p.H, p.Hkv);
         if (HG == 4) k_fa_mma2<4><<<g2, 256, 0, c.st>>>(p);
@@ -590,6 +655,12 @@ void fa_mma_nofa_launch(OpCtx & c, const ggml_tensor * q, const ggml_tensor * k,
     p.dst = (char *) out->data; p.d1 = (size_t) D * 4; p.d2 = (size_t) D * 4 * p.H;
     p.h = mmq_act_claim(c, out->data, (int64_t) D * p.H, p.n_q, p.d2);
     const int Gt = p.H / p.Hkv, HG = Gt % 4 == 0 ? 4 : (Gt % 2 == 0 ? 2 : 1);
+    if (fa_key_split(Gt)) {
+        const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32), (unsigned) (p.Hkv * (Gt / 2)));
+        MX_KLOG("attn_nofa_mma HG=2 ks=2 n_q=%d n_kv=%d H=%d Hkv=%d mask=%d", p.n_q, p.n_kv, p.H, p.Hkv, m ? (int) m->type : -1);
+        k_fa_mma2<2, true, true><<<g2, 256, 0, c.st>>>(p);
+        return;
+    }
     const dim3 g2((unsigned) mx_ceil_div(p.n_q, 32 * (4 / HG)), (unsigned) (p.Hkv * (Gt / HG)));
     MX_KLOG("attn_nofa_mma HG=%d n_q=%d n_kv=%d H=%d Hkv=%d mask=%d", HG, p.n_q, p.n_kv, p.H, p.Hkv, m ? (int) m->type : -1);
     if (HG == 4) k_fa_mma2<4, true><<<g2, 256, 0, c.st>>>(p);
