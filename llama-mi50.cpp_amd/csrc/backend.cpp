@@ -313,8 +313,10 @@ static void be_free(ggml_backend_t b) {
                 (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n : 0),
                 (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n_flush : 0));
     if (const char * kp = getenv("GGML_MI355X_KLOG")) klog_dump(kp);
-    if (s->gcache.exec) hipGraphExecDestroy(s->gcache.exec);
-    if (s->gcache.graph) hipGraphDestroy(s->gcache.graph);
+    for (GraphCache & gc : s->gslots) {
+        if (gc.exec) hipGraphExecDestroy(gc.exec);
+        if (gc.graph) hipGraphDestroy(gc.graph);
+    }
     if (s->scratch.base) hipFree(s->scratch.base);
     if (s->act.base) hipFree(s->act.base);
     if (s->f16.base) hipFree(s->f16.base);

@@ -81,7 +81,9 @@ struct GraphCache {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     int hits = 0;
+    uint64_t last_use = 0;        // LRU among the stream's slots
 };
+constexpr int kGraphSlots = 8;    // captured cgraphs kept per stream (a pp2048 prompt: 4 ubatch shapes)
 
 // RMS_NORM → MUL(w) whose only consumers are single-token GEMVs: not materialised,
 // the GEMV prologues recompute it from x (exec.cpp run_nodes)
@@ -112,7 +114,10 @@ struct Stream {
     int f16_last = 0;
     int act_next = 0;
     size_t act_slot = 0;               // bytes per ring slot
-    GraphCache gcache;
+    GraphCache gslots[kGraphSlots];
+    int gcur = 0;                      // slot of the last graph computed
+    uint64_t gtick = 0;
+    std::vector<uint64_t> gsig;        // signature of the last graph computed
     // RoPE cos/sin table of the current token (ops_qkv.hip): computed once per graph
     // pass by the first fused QKV block, read by all layers' (same position, same params)
     float * rope_tab = nullptr;        // device, float2 [MX_ROPE_TAB]
@@ -206,6 +211,7 @@ bool rms_norm_mul_q8(OpCtx & c, ggml_tensor * norm, const ggml_tensor * w, ggml_
 // activation-cache management (ops_mmvq.hip)
 size_t act_slot_bytes(const ggml_tensor * src1);
 void act_cache_reset(Stream * s);
+void graph_cache_forget(Stream * s);   // buffers moved: no captured graph may replay
 void act_cache_invalidate(Stream * s, const ggml_tensor * written);
 ActQ * act_cache_alloc(Stream * s, const ggml_tensor * t);   // reserve a slot for t (caller fills it)
 ActQ * act_cache_alloc_raw(Stream * s, const void * data, int64_t ne0, int64_t ncols, size_t bytes);

@@ -589,6 +589,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
 }
 
 // grow a stream's scratch arena, activation ring and f16 slots to the given sizes
+void graph_cache_forget(Stream * s) {
+    for (GraphCache & gc : s->gslots) gc.key.clear();
+}
+
 // (never inside a capture)
 static void stream_reserve(Stream * s, size_t need, size_t slot, size_t f16need) {
     if (slot > s->act_slot || f16need > s->f16.cap || need > s->scratch.cap) ++g_buf_gen;
@@ -598,7 +602,7 @@ static void stream_reserve(Stream * s, size_t need, size_t slot, size_t f16need)
         s->act_slot = (slot + 4095) & ~(size_t) 4095;
         HIP_CHECK(hipMalloc((void **) &s->act.base, 4 * s->act_slot));
         s->act.cap = 4 * s->act_slot;
-        s->gcache.key.clear();
+        graph_cache_forget(s);
     }
     if (f16need > s->f16.cap) {
         HIP_CHECK(hipStreamSynchronize(s->stream));
@@ -606,7 +610,7 @@ static void stream_reserve(Stream * s, size_t need, size_t slot, size_t f16need)
         HIP_CHECK(hipMalloc((void **) &s->f16.base, 2 * f16need));
         s->f16.cap = f16need;
         s->f16_src[0] = s->f16_src[1] = nullptr;
-        s->gcache.key.clear();
+        graph_cache_forget(s);
     }
     if (need > s->scratch.cap) {
         HIP_CHECK(hipStreamSynchronize(s->stream));
@@ -614,7 +618,7 @@ static void stream_reserve(Stream * s, size_t need, size_t slot, size_t f16need)
         size_t cap = std::max<size_t>(need + need / 4, 16u << 20);
         HIP_CHECK(hipMalloc((void **) &s->scratch.base, cap));
         s->scratch.cap = cap;
-        s->gcache.key.clear();  // captured kernels point at the old arena
+        graph_cache_forget(s);  // captured kernels point at the old arena
     }
 }
 
@@ -634,27 +638,60 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     // A graph identical to the last one (the decode steps of libllama and of our runner)
     // replays its capture before anything else: the per-node buffer sizing below cost
     // ~100 us of host time per token while the GPU waited (drop-in stats, round 2).
-    GraphCache & gc = s->gcache;
+    // Round 4: kGraphSlots captures per stream, found by signature (LRU), so graphs that
+    // alternate — a pp2048 prompt's four ubatches (n_kv 512 .. 2048), a prompt and its
+    // decode — replay too instead of each evicting the other's capture (the eager form of a
+    // prefill graph ran ~8 % behind its replay: the host's per-node work does not stay
+    // ahead of the GPU).
     const bool graphs = s->use_graphs && !g_sync_debug;
-    bool same = false;
+    static const int nslots = [] {   // GGML_MI355X_GRAPH_SLOTS=1: the round-3 single capture (A/B)
+        const char * v = getenv("GGML_MI355X_GRAPH_SLOTS");
+        return v && *v ? std::max(1, std::min(kGraphSlots, atoi(v))) : kGraphSlots;
+    }();
+    bool seen = false;   // this signature was computed before (second sighting or later)
     if (graphs) {
         const auto t0 = std::chrono::steady_clock::now();
-        same = graph_signature_same(g, gc.key);   // gc.key now holds g's signature
+        const bool same_prev = graph_signature_same(g, s->gsig);   // s->gsig now holds g's signature
+        int k = -1;
+        if (same_prev && s->gslots[s->gcur].key.size() == s->gsig.size() && !s->gsig.empty() &&
+            s->gslots[s->gcur].key.data() != nullptr && !s->gslots[s->gcur].key.empty())
+            k = s->gcur;                                            // (the slot holds gsig by construction)
+        for (int j = 0; j < nslots && k < 0; ++j) {
+            const std::vector<uint64_t> & kk = s->gslots[j].key;
+            if (kk.size() == s->gsig.size() && !kk.empty() && memcmp(kk.data(), s->gsig.data(), kk.size() * 8) == 0) k = j;
+        }
         const auto t1 = std::chrono::steady_clock::now();
         s->us_sig += std::chrono::duration<double, std::micro>(t1 - t0).count();
-        if (gc.exec && same && gc.buf_gen == g_buf_gen.load()) {
-            HIP_CHECK(hipGraphLaunch(gc.exec, s->stream));
-            s->us_launch += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
-            s->n_graph_replay++;
-            return;
-        }
-        if (!same || (gc.exec && gc.buf_gen != g_buf_gen.load())) {   // a different graph (or moved buffers): the capture is stale
-            same = false;
-            gc.hits = 0;
+        if (k >= 0) {
+            GraphCache & gc = s->gslots[k];
+            s->gcur = k;
+            gc.last_use = ++s->gtick;
+            if (gc.exec && gc.buf_gen == g_buf_gen.load()) {
+                HIP_CHECK(hipGraphLaunch(gc.exec, s->stream));
+                s->us_launch += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
+                s->n_graph_replay++;
+                return;
+            }
+            if (gc.exec) { HIP_CHECK(hipGraphExecDestroy(gc.exec)); gc.exec = nullptr; }   // moved buffers: stale
+            if (gc.graph) { HIP_CHECK(hipGraphDestroy(gc.graph)); gc.graph = nullptr; }
+            seen = true;
+        } else {
+            // first sighting: the least recently used slot (an empty one first) takes it
+            int v = 0;
+            for (int j = 1; j < nslots; ++j) {
+                const GraphCache & a = s->gslots[j], & b = s->gslots[v];
+                if ((a.key.empty() && !b.key.empty()) || (a.key.empty() == b.key.empty() && a.last_use < b.last_use)) v = j;
+            }
+            GraphCache & gc = s->gslots[v];
             if (gc.exec) { HIP_CHECK(hipGraphExecDestroy(gc.exec)); gc.exec = nullptr; }
             if (gc.graph) { HIP_CHECK(hipGraphDestroy(gc.graph)); gc.graph = nullptr; }
+            gc.key = s->gsig;
+            gc.hits = 0;
+            gc.last_use = ++s->gtick;
+            s->gcur = v;
         }
     }
+    GraphCache & gc = s->gslots[s->gcur];
 
     size_t need = 0, slot = 0, f16need = 0;
     for (int i = 0; i < g->n_nodes; ++i) {
@@ -666,7 +703,8 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         if (g->nodes[i]->op == GGML_OP_MUL_MAT_ID && g->nodes[i]->src[2]->ne[1] <= 8)
             slot = std::max({slot, act_slot_bytes(g->nodes[i]), act_slot_bytes(g->nodes[i]->src[1])});
     }
-    stream_reserve(s, need, slot, f16need);   // a reallocation clears gc.key: no capture of old buffers replays
+    stream_reserve(s, need, slot, f16need);   // a reallocation clears every key: no capture of old buffers replays
+    if (graphs && gc.key.empty()) { gc.key = s->gsig; seen = false; }   // (counts as a first sighting again)
 
     // row-split weights (split.cpp): every device works on the node, the slices fork off
     // onto the devices' own streams and join back by events; only the fusions without a
@@ -681,8 +719,22 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         s->split_graph = false;
         return;
     }
-    if (!graphs || !same || gc.key.empty()) { run_nodes(s, g); s->split_graph = false; return; }   // first sighting: eager
-    // second sighting of the same signature: capture and launch
+    if (!graphs || !seen || gc.key.empty()) { run_nodes(s, g); s->split_graph = false; return; }   // first sighting: eager
+    // second sighting of the same signature: capture and launch. (Recording it on a side
+    // stream behind an eager run instead measured no better for the prompt and slower for the
+    // first decode repetition: profiles/r04/graph_slots_ab.txt)
+    HIP_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+        run_nodes(s, g);
+        hipGraph_t graph = nullptr;
+        HIP_CHECK(hipStreamEndCapture(s->stream, &graph));
+        s->stream = main_stream;
+        g_klog = klog;
+        s->n_nodes_run = nr; s->n_fused = nf;
+        HIP_CHECK(hipGraphInstantiate(&gc.exec, graph, nullptr, nullptr, 0));
+        gc.graph = graph;
+        gc.buf_gen = g_buf_gen.load();
+        return;
+    }
     HIP_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
     run_nodes(s, g);
     s->split_graph = false;

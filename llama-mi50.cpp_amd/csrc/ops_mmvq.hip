@@ -427,7 +427,7 @@ double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * 
             if (s->scratch.base) HIP_CHECK(hipFree(s->scratch.base));
             HIP_CHECK(hipMalloc((void **) &s->scratch.base, need));
             s->scratch.cap = need;
-            s->gcache.key.clear();
+            graph_cache_forget(s);
         }
         s->scratch.reset();
         ActQ a = carve((char *) s->scratch.take(act_slot_bytes(x)), x);
