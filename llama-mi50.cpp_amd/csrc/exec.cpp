@@ -724,18 +724,6 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     // stream behind an eager run instead measured no better for the prompt and slower for the
     // first decode repetition: profiles/r04/graph_slots_ab.txt)
     HIP_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-        run_nodes(s, g);
-        hipGraph_t graph = nullptr;
-        HIP_CHECK(hipStreamEndCapture(s->stream, &graph));
-        s->stream = main_stream;
-        g_klog = klog;
-        s->n_nodes_run = nr; s->n_fused = nf;
-        HIP_CHECK(hipGraphInstantiate(&gc.exec, graph, nullptr, nullptr, 0));
-        gc.graph = graph;
-        gc.buf_gen = g_buf_gen.load();
-        return;
-    }
-    HIP_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
     run_nodes(s, g);
     s->split_graph = false;
     hipGraph_t graph = nullptr;
