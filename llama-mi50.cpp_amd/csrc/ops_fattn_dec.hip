@@ -631,17 +631,25 @@ struct NfArgs {
 constexpr int NF_NI = 8;                // key rows per lane in flight
 constexpr int NF_MAX_KV = 16384;        // scores in LDS: 64 KB dynamic + ~1 KB static (> the 64 KB default)
 
-template <int D>
-__global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
+// NI key rows per lane per pass, NT threads; VPRE > 0 (round 4, caches of one pass): the
+// lane's V row segment (VPRE x 16 B) and the mask values are loaded together with the K
+// rows, before any arithmetic — one memory round trip instead of K (two passes at NI 8 for
+// 256 keys), then the mask, then V after the softmax. At 256 keys, 1,024 threads (NI 4,
+// VPRE 4: 32 B of K and 64 B of V per lane): 10.1 -> 8.05 us per layer in the drop-in -fa 0
+// decode, tg128 557.6 -> 577.0 tok/s (256 threads, NI 16 / VPRE 16: 9.1 us, 568;
+// profiles/r04/nofa_decode_ab.txt; g_tune[2] = 10 / 9 select those)
+template <int D, int NI = NF_NI, int VPRE = 0, int NT = 256>
+__global__ __launch_bounds__(NT) void k_attn_nofa_dec(NfArgs p) {
+    constexpr int NW = NT / 64;
     extern __shared__ __align__(16) float sc[];   // [n_kv]: scores, then f16-rounded probabilities
-    __shared__ float red[4];
-    __shared__ float opart[256 / D][D];
+    __shared__ float red[NW];
+    __shared__ float opart[NT / D][D];
     typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-    constexpr int LPK = D / 8, KPI = 64 / LPK, PER = 4 * NF_NI * KPI;   // keys per workgroup pass
+    constexpr int LPK = D / 8, KPI = 64 / LPK, PER = NW * NI * KPI;   // keys per workgroup pass
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (blockIdx.y > 0) {                      // weight prefetch rows, as in k_fattn_dec2
         const unsigned L = blockIdx.x + gridDim.x * blockIdx.y, xcd = L & 7;
-        const unsigned T = (gridDim.x * (gridDim.y - 1) >> 3) * 256, t0 = ((L - gridDim.x) >> 3) * 256 + tid;
+        const unsigned T = (gridDim.x * (gridDim.y - 1) >> 3) * NT, t0 = ((L - gridDim.x) >> 3) * NT + tid;
         unsigned acc = 0;
         for (int r = 0; r < p.pf_n; ++r) {
             const unsigned * w = (const unsigned *) (p.pf[r] + (size_t) xcd * p.pf_eighth[r]);
@@ -661,16 +669,34 @@ __global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
         qh[2] = h2v{(_Float16) b.x, (_Float16) b.y}; qh[3] = h2v{(_Float16) b.z, (_Float16) b.w};
     }
     const char * kb = p.k + (size_t) hk * p.k2 + c * 16;
-    for (int base = 0; base < p.n_kv; base += PER) {
-        uint4 kr[NF_NI];
-        int key[NF_NI];
+    // P·V geometry (below): NT/D threads per dimension, each a contiguous key range
+    constexpr int SPLIT = NT / D;
+    const int d = tid % D, part = tid / D;
+    const int nk = p.n_kv / SPLIT;                           // host: n_kv % (8 SPLIT) == 0
+    const char * vr = p.v + (size_t) hk * p.v2 + (size_t) d * p.v1 + (size_t) part * nk * 2;
+    uint4 vpre[VPRE > 0 ? VPRE : 1];
+    if constexpr (VPRE > 0) {
 #pragma unroll
-        for (int t = 0; t < NF_NI; ++t) {
-            key[t] = base + (wave * NF_NI + t) * KPI + kq;
+        for (int j = 0; j < VPRE; ++j) vpre[j] = *(const uint4 *) (vr + 16 * min(j, nk / 8 - 1));
+    }
+    for (int base = 0; base < p.n_kv; base += PER) {
+        uint4 kr[NI];
+        int key[NI];
+        float mval[NI];
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+            key[t] = base + (wave * NI + t) * KPI + kq;
             kr[t] = *(const uint4 *) (kb + (size_t) min(key[t], p.n_kv - 1) * p.k1);
         }
+        if constexpr (VPRE > 0) {     // the mask values with the rows (unconditional, clamped)
 #pragma unroll
-        for (int t = 0; t < NF_NI; ++t) {
+            for (int t = 0; t < NI; ++t) {
+                const int kk = min(key[t], p.n_kv - 1);
+                mval[t] = !p.mask ? 0.f : p.mask_f16 ? h2f(((const uint16_t *) p.mask)[kk]) : ((const float *) p.mask)[kk];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
             float acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[0], 0.f, false);
             acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[1], acc, false);
             acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[2], acc, false);
@@ -678,7 +704,8 @@ __global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
             acc = dpp_sum_group<LPK>(acc);
             if (c == LPK - 1 && key[t] < p.n_kv) {
                 float m = 0.f;
-                if (p.mask) m = p.mask_f16 ? h2f(((const uint16_t *) p.mask)[key[t]]) : ((const float *) p.mask)[key[t]];
+                if constexpr (VPRE > 0) m = mval[t];
+                else if (p.mask) m = p.mask_f16 ? h2f(((const uint16_t *) p.mask)[key[t]]) : ((const float *) p.mask)[key[t]];
                 sc[key[t]] = acc * p.scale + m;
             }
         }
@@ -686,14 +713,15 @@ __global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
     __syncthreads();
     // softmax (ggml_vec_soft_max_f32: exp(x - max), Σ, times 1/Σ)
     float mx = -INFINITY;
-    for (int k = tid; k < p.n_kv; k += 256) mx = fmaxf(mx, sc[k]);
+    for (int k = tid; k < p.n_kv; k += NT) mx = fmaxf(mx, sc[k]);
     mx = wave_max(mx);
     if (lane == 0) red[wave] = mx;
     __syncthreads();
-    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mx = fmaxf(mx, red[w]);
     __syncthreads();
     float sum = 0.f;
-    for (int k = tid; k < p.n_kv; k += 256) {
+    for (int k = tid; k < p.n_kv; k += NT) {
         const float e = sc[k] == -INFINITY ? 0.f : expf(sc[k] - mx);
         sc[k] = e;
         sum += e;
@@ -701,17 +729,28 @@ __global__ __launch_bounds__(256) void k_attn_nofa_dec(NfArgs p) {
     sum = wave_sum(sum);
     if (lane == 0) red[wave] = sum;
     __syncthreads();
-    const float inv = 1.0f / ((red[0] + red[1]) + (red[2] + red[3]));
-    for (int k = tid; k < p.n_kv; k += 256) sc[k] = (float) (_Float16) (sc[k] * inv);
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tot += red[w];
+    const float inv = 1.0f / tot;
+    for (int k = tid; k < p.n_kv; k += NT) sc[k] = (float) (_Float16) (sc[k] * inv);
     __syncthreads();
-    // P·V over the transposed rows: 256/D threads per dimension, each a contiguous key range
-    constexpr int SPLIT = 256 / D;
-    const int d = tid % D, part = tid / D;
-    const int nk = p.n_kv / SPLIT;                           // host: n_kv % (8 SPLIT) == 0
-    const char * vr = p.v + (size_t) hk * p.v2 + (size_t) d * p.v1 + (size_t) part * nk * 2;
+    // P·V over the transposed rows
     const float * pp = sc + part * nk;
     float o = 0.f;
-    for (int k = 0; k < nk; k += 8) {
+    if constexpr (VPRE > 0) {
+#pragma unroll
+        for (int j = 0; j < VPRE; ++j) {
+            if (8 * j >= nk) break;
+            const uint32_t ww[4] = {vpre[j].x, vpre[j].y, vpre[j].z, vpre[j].w};
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2) {
+                o += pp[8 * j + 2 * i2] * h2f((uint16_t) (ww[i2] & 0xFFFF));
+                o += pp[8 * j + 2 * i2 + 1] * h2f((uint16_t) (ww[i2] >> 16));
+            }
+        }
+    }
+    for (int k = 8 * VPRE; k < nk; k += 8) {
         const uint4 w = *(const uint4 *) (vr + 2 * k);
         const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -836,10 +875,16 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
     static const bool attr = [] {
         HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<128>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
         HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<64>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
+        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<128, 16, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
+        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<128, 4, 4, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
         return true;
     }();
     (void) attr;
-    if (D == 128) k_attn_nofa_dec<128><<<grid, 256, lds, c.st>>>(a);
+    // one pass over a cache of <= 256 keys with V and the mask loaded up front (D 128);
+    // g_tune[2] = 10: the 256-thread one-pass form, 9: the round-3 two-pass form (A/B)
+    if (D == 128 && n_kv <= 256 && n_kv % 64 == 0 && g_tune[2] != 9 && g_tune[2] != 10) k_attn_nofa_dec<128, 4, 4, 1024><<<grid, 1024, lds, c.st>>>(a);
+    else if (D == 128 && n_kv <= 4 * 16 * 4 && g_tune[2] != 9) k_attn_nofa_dec<128, 16, 16><<<grid, 256, lds, c.st>>>(a);
+    else if (D == 128) k_attn_nofa_dec<128><<<grid, 256, lds, c.st>>>(a);
     else k_attn_nofa_dec<64><<<grid, 256, lds, c.st>>>(a);
     return last - i + 1;
 }
