@@ -61,19 +61,35 @@ static inline void sig_tensor(SigCursor & c, const ggml_tensor * t) {
 
 // returns true when g's signature equals the stored key (which is updated to g's)
 extern unsigned g_tune_gen;   // backend.cpp: bumped by every changed ggml_backend_mi355x_set_tune
+// Round 4: a node's sources enter by pointer, data pointer, row stride and the first two
+// extents (packed) — 4 words instead of 10 (a source that is itself a node of this graph
+// is signed in full as that node; a scheduler split's graph view has no leafs, so sources
+// from outside it are covered by these four), ~29 words per node instead of ~55 (the walk
+// was ~27 us of host time per drop-in token, with the GPU idle).
 static bool graph_signature_same(const ggml_cgraph * g, std::vector<uint64_t> & key) {
     SigCursor c{key};
     c.put((uint64_t) g->n_nodes | ((uint64_t) g_tune_gen << 32));
+    c.put((uint64_t) g->n_leafs);
     for (int i = 0; i < g->n_nodes; ++i) {
         const ggml_tensor * n = g->nodes[i];
         sig_tensor(c, n);
         const uint64_t * p = (const uint64_t *) n->op_params;
         for (int j = 0; j < GGML_MAX_OP_PARAMS / 8; ++j) c.put(p[j]);
+        uint64_t ns = 0;
         for (int j = 0; j < GGML_MAX_SRC; ++j) {
             const ggml_tensor * s = n->src[j];
-            if (!s) { c.put(0); continue; }
-            sig_tensor(c, s);
+            if (!s) continue;
+            c.put((uint64_t) (uintptr_t) s ^ ((uint64_t) j << 58));
+            c.put((uint64_t) (uintptr_t) s->data);
+            c.put((uint64_t) s->nb[1] ^ ((uint64_t) s->type << 56) ^ ((uint64_t) s->op << 48));
+            c.put((uint64_t) (uint32_t) s->ne[0] | ((uint64_t) (uint32_t) s->ne[1] << 32));
+            ++ns;
         }
+        c.put(ns | ((uint64_t) n->flags << 8));
+    }
+    for (int i = 0; i < g->n_leafs; ++i) {
+        sig_tensor(c, g->leafs[i]);
+        c.put((uint64_t) (uintptr_t) g->leafs[i]);
     }
     if (c.pos != key.size()) { key.resize(c.pos); c.same = false; }
     return c.same;
