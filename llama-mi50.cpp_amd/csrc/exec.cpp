@@ -556,6 +556,13 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             // row-split weights: the fusions that touch no MUL_MAT (split or not: a split
             // slice runs on its device's own stream, which no deferred norm reaches)
             if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
+            // decode MUL_MAT -> ADD over a row-split weight whose slices are on this GPU: the
+            // residual GEMV per slice (mmvq_fused_add), no separate ADD pass
+            static const bool no_split_fusion = getenv("GGML_MI355X_NO_SPLIT_FUSION") != nullptr;   // A/B
+            if (!no_split_fusion && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0]) && mmvq_small_batch_ok(n)) {
+                const int k = try_fuse_mm_add(c, g, i, uses);
+                if (k) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; continue; }
+            }
         } else if (s->use_fusion) {
             const int i0 = i;
             if (n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }

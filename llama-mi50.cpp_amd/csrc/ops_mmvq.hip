@@ -350,6 +350,29 @@ bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, 
     if (res->type != GGML_TYPE_F32 || add->type != GGML_TYPE_F32 || !mx_are_same_shape(res, mm) || !mx_are_same_shape(add, mm)) return false;
     if (res->nb[0] != 4 || add->nb[0] != 4 || w->ne[2] != 1 || w->ne[3] != 1) return false;
     XStage xs;
+    if (tensor_is_split(w)) {
+        // round 4, row-split weights whose slices all lie on this GPU (split.cpp): one residual
+        // GEMV per slice on this stream, each writing its rows of the sum — the unsplit
+        // decode's fused launch instead of per-slice GEMVs + an ADD pass
+        void * sd[MX_MAX_DEVICES];
+        int64_t lo[MX_MAX_DEVICES], hi[MX_MAX_DEVICES];
+        const int ns = split_local_slices(c.s, w, sd, lo, hi);
+        if (!ns || !g_gemv2 || !mx_is_contiguous(res) || !mx_is_contiguous(add)) return false;
+        ggml_tensor ws[MX_MAX_DEVICES], av[MX_MAX_DEVICES];
+        for (int k = 0; k < ns; ++k) {
+            const int64_t rows = hi[k] - lo[k];
+            ws[k] = *w; ws[k].ne[1] = rows; ws[k].nb[2] = ws[k].nb[3] = ws[k].nb[1] * rows; ws[k].data = sd[k];
+            ws[k].buffer = nullptr; ws[k].extra = nullptr; ws[k].view_src = nullptr;
+            av[k] = *add; av[k].ne[0] = rows; av[k].data = (char *) add->data + lo[k] * 4; av[k].buffer = nullptr; av[k].view_src = nullptr;
+            av[k].nb[1] = av[k].nb[2] = av[k].nb[3] = (size_t) rows * 4;
+            if (!gemv2_ok(&ws[k], x, &av[k])) return false;
+        }
+        if (!gemv2_stage(c, x, {add}, {res}, &xs)) return false;
+        MX_KLOG("mm_split_add M=%lld K=%lld slices=%d", (long long) w->ne[1], (long long) w->ne[0], ns);
+        for (int k = 0; k < ns; ++k)
+            gemv2_launch(c, &ws[k], nullptr, xs, (float *) add->data + lo[k], (const float *) res->data + lo[k]);
+        return true;
+    }
     if (g_gemv2 && gemv2_ok(w, x, add) && mx_is_contiguous(res)) {
         if (gemv2_stage(c, x, {add}, {res}, &xs)) {
             gemv2_launch(c, w, nullptr, xs, (float *) add->data, (const float *) res->data);

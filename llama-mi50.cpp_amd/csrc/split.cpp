@@ -223,6 +223,23 @@ bool mx_force_peer() {
     return f;
 }
 
+// the slices of a row-split weight when every non-empty one lies on the main stream's own
+// GPU (logical devices of one GPU, no forced peer path): their data and row ranges; 0 when
+// any slice needs another device's stream (the fused per-slice launches run on c.st only)
+int split_local_slices(const Stream * s, const ggml_tensor * w, void ** data, int64_t * lo, int64_t * hi) {
+    if (!tensor_is_split(w) || !w->extra || mx_force_peer()) return 0;
+    const SplitExtra * e = (const SplitExtra *) w->extra;
+    if (mx_dev_hip(split_main_device(w->buffer->buft)) != s->device) return 0;
+    int n = 0;
+    for (int d = 0; d < mx_dev_count(); ++d) {
+        if (e->hi[d] == e->lo[d]) continue;
+        if (mx_dev_hip(d) != s->device || !mx_peer_enabled(s->device, s->device)) return 0;
+        data[n] = e->data[d]; lo[n] = e->lo[d]; hi[n] = e->hi[d];
+        ++n;
+    }
+    return n;
+}
+
 void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) {
     const ggml_tensor * w = dst->src[0];
     const ggml_tensor * x = dst->src[1];
