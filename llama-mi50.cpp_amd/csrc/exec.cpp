@@ -360,7 +360,7 @@ static int try_fuse_mm_rows_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses
 
 // MUL_MAT(gate) , MUL_MAT(up) , GLU(gate, up) with one activation column:
 // one pass over the activation, two weight streams (ggml-cuda.cu:2145-2181).
-static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
+static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses, bool gemv_only = false) {
     if (i + 2 >= g->n_nodes) return false;
     ggml_tensor * a = g->nodes[i];
     ggml_tensor * b = g->nodes[i + 1];
@@ -375,7 +375,7 @@ static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     else return false;
     if (uses[a] != 1 || uses[b] != 1 || ((a->flags | b->flags) & GGML_TENSOR_FLAG_OUTPUT)) return false;
     act_cache_invalidate(c.s, glu);
-    return mmvq_fused_glu(c, gate, up, glu) || mmq_fused_glu(c, gate, up, glu);
+    return mmvq_fused_glu(c, gate, up, glu) || (!gemv_only && mmq_fused_glu(c, gate, up, glu));
 }
 
 // MUL_MAT_ID(gate), MUL_MAT_ID(up), GLU of a decode step (llama build_moe_ffn): one v2
@@ -556,10 +556,11 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             // row-split weights: the fusions that touch no MUL_MAT (split or not: a split
             // slice runs on its device's own stream, which no deferred norm reaches)
             if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
-            // decode MUL_MAT -> ADD over a row-split weight whose slices are on this GPU: the
-            // residual GEMV per slice (mmvq_fused_add), no separate ADD pass
+            // decode gate/up/SwiGLU and MUL_MAT -> ADD over row-split weights whose slices are
+            // on this GPU: the SwiGLU / residual GEMV per slice (mmvq_fused_glu / _add)
             static const bool no_split_fusion = getenv("GGML_MI355X_NO_SPLIT_FUSION") != nullptr;   // A/B
             if (!no_split_fusion && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0]) && mmvq_small_batch_ok(n)) {
+                if (try_fuse_glu(c, g, i, uses, true)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
                 const int k = try_fuse_mm_add(c, g, i, uses);
                 if (k) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; continue; }
             }

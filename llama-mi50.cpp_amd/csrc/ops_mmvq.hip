@@ -329,6 +329,38 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up,
     if (wg->ne[2] != 1 || wg->ne[3] != 1) return false;
     if (glu->type != GGML_TYPE_F32 || glu->nb[0] != 4 || !mx_are_same_shape(glu, gate)) return false;
     XStage xs;
+    if (tensor_is_split(wg) || tensor_is_split(wu)) {
+        // round 4, row-split gate and up whose slices (the same row ranges) all lie on this
+        // GPU: one SwiGLU GEMV per slice on this stream, each writing its rows of the GLU and
+        // of its q8 copy (the down projection's input) — as the unsplit decode does
+        void * dg[MX_MAX_DEVICES], * du[MX_MAX_DEVICES];
+        int64_t lg[MX_MAX_DEVICES], hg[MX_MAX_DEVICES], lu[MX_MAX_DEVICES], hu[MX_MAX_DEVICES];
+        const int ns = split_local_slices(c.s, wg, dg, lg, hg);
+        if (!ns || ns != split_local_slices(c.s, wu, du, lu, hu) || !g_gemv2 || !mx_is_contiguous(glu)) return false;
+        ggml_tensor ws[2][MX_MAX_DEVICES], gv[MX_MAX_DEVICES];
+        for (int k = 0; k < ns; ++k) {
+            if (lg[k] != lu[k] || hg[k] != hu[k] || lg[k] % 32) return false;
+            const int64_t rows = hg[k] - lg[k];
+            for (int t = 0; t < 2; ++t) {
+                ggml_tensor & w = ws[t][k];
+                w = t ? *wu : *wg; w.ne[1] = rows; w.nb[2] = w.nb[3] = w.nb[1] * rows; w.data = t ? du[k] : dg[k];
+                w.buffer = nullptr; w.extra = nullptr; w.view_src = nullptr;
+            }
+            gv[k] = *glu; gv[k].ne[0] = rows; gv[k].data = (char *) glu->data + lg[k] * 4; gv[k].buffer = nullptr; gv[k].view_src = nullptr;
+            gv[k].nb[1] = gv[k].nb[2] = gv[k].nb[3] = (size_t) rows * 4;
+            if (!gemv2_ok(&ws[0][k], x, &gv[k])) return false;
+        }
+        if (!gemv2_stage(c, x, {glu}, {}, &xs)) return false;
+        ActQ * q8 = wg->ne[1] % 32 == 0 ? act_cache_alloc(c.s, glu) : nullptr;
+        if (q8 && xs.q8 == q8->q) q8 = nullptr;
+        MX_KLOG("glu_split M=%lld K=%lld slices=%d q8o=%d", (long long) wg->ne[1], (long long) wg->ne[0], ns, q8 != nullptr);
+        for (int k = 0; k < ns; ++k) {
+            ActQ qs{};
+            if (q8) { qs = *q8; qs.q += lg[k]; qs.d += lg[k] / 32; qs.s += lg[k] / 32; }
+            gemv2_launch(c, &ws[0][k], &ws[1][k], xs, (float *) glu->data + lg[k], nullptr, q8 ? &qs : nullptr);
+        }
+        return true;
+    }
     if (g_gemv2 && gemv2_ok(wg, x, glu) && gemv2_stage(c, x, {glu}, {}, &xs)) {
         // the q8 form of the output feeds the down projection's prologue (act cache)
         ActQ * q8 = (wg->ne[1] % 32 == 0 && mx_is_contiguous(glu)) ? act_cache_alloc(c.s, glu) : nullptr;

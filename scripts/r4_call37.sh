@@ -1,5 +1,5 @@
 #!/bin/bash
-# per-slice fused residual GEMV for local row splits: split tests, then -sm row A/B (GGML_MI355X_NO_SPLIT_FUSION=1 = before)
+# per-slice fused SwiGLU + residual GEMVs for local row splits: split tests, then -sm row A/B (GGML_MI355X_NO_SPLIT_FUSION=1 = before)
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 timeout -k 10 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_dropin_gpu.py tests/test_dropin_shapes_gpu.py -k "split or row" > gpurun_out/r4_splitfuse_tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r4_splitfuse_tests.log
