@@ -140,27 +140,39 @@ def test_layer_split_handoff_cpy_tensor_async(tmp_path):
     assert '"mismatches": 0' in r.stdout and "MI355X" in r.stdout, r.stdout
 
 
-@pytest.mark.parametrize("incremental,no_peer", [(False, False), (True, False), (True, True)])
-def test_dropin_row_split(ggufs, tmp_path, incremental, no_peer):
+@pytest.mark.parametrize("incremental,no_peer,force_peer", [(False, False, True), (True, False, True), (True, True, True),
+                                                          (False, False, False), (True, False, False)])
+def test_dropin_row_split(ggufs, tmp_path, incremental, no_peer, force_peer):
     """llama -sm row -ts 1,1: libllama puts every matrix in the backend's split buffer type
     (proc ggml_backend_split_buffer_type), rows halved over two devices — here two logical
     devices of the one MI355X (GGML_MI355X_VIRTUAL_DEVICES=2) — and every MUL_MAT runs its
-    slices on both and gathers them (split.cpp). Logits against the reference CPU backend."""
+    slices on both and gathers them (split.cpp). Logits against the reference CPU backend.
+    force_peer False: the slices are local to the GPU, so decode's gate/up/SwiGLU and
+    MUL_MAT -> ADD run as per-slice fused GEMVs (klog glu_split / mm_split_add)."""
     _need_ref()
     toks = np.random.default_rng(10).integers(0, 1000, 24 if incremental else 40)
     g = ggufs[("small", "q4_k_m")]
     klog = tmp_path / "klog.txt"
     cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental)
+    env = {"GGML_MI355X_VIRTUAL_DEVICES": "2"}
+    if force_peer:
+        env["GGML_MI355X_FORCE_PEER"] = "1"
+    if no_peer:
+        env["GGML_MI355X_NO_PEER"] = "1"
     gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, klog=klog, extra=["-sm", "row", "-ts", "1,1"],
-                       env_extra={"GGML_MI355X_VIRTUAL_DEVICES": "2", "GGML_MI355X_FORCE_PEER": "1",
-                                  **({"GGML_MI355X_NO_PEER": "1"} if no_peer else {})})
+                       env_extra=env)
     assert "MI355X" in log
     assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
     kl = klog.read_text()
     assert "mm_split" in kl and "devices=2" in kl, kl[-2000:]
-    # GGML_MI355X_FORCE_PEER: the cross-device broadcast / gather branches of split.cpp ran
-    # (no_peer: the slices come back by one contiguous peer copy and a 2D copy on main)
-    assert all("peer=1" in ln and f"direct={int(not no_peer)}" in ln for ln in kl.splitlines() if ln.startswith("mm_split")), kl[-2000:]
+    if force_peer:
+        # GGML_MI355X_FORCE_PEER: the cross-device broadcast / gather branches of split.cpp ran
+        # (no_peer: the slices come back by one contiguous peer copy and a 2D copy on main)
+        assert all("peer=1" in ln and f"direct={int(not no_peer)}" in ln for ln in kl.splitlines() if ln.startswith("mm_split ")), kl[-2000:]
+        assert "glu_split" not in kl and "mm_split_add" not in kl, kl[-2000:]
+    elif incremental:
+        # one-token steps: the per-slice fused SwiGLU and residual GEMVs
+        assert "glu_split" in kl and "mm_split_add" in kl, kl[-2000:]
 
 
 @pytest.mark.parametrize("ts", ["1,1", "1,1,1,1"])
