@@ -85,6 +85,7 @@ struct Staging {
     uint64_t n_flush = 0;          // flush launches
 };
 static Staging g_stage[MX_MAX_DEVICES];
+static bool env_flag(const char * name) { const char * v = getenv(name); return v && *v && strcmp(v, "0") != 0; }
 static constexpr size_t kStageMax = 4 << 20, kStageRing = 32 << 20;
 
 static void stage_flush_locked(Staging & st) {
@@ -147,6 +148,14 @@ void staged_writes_wait(int dev, hipStream_t stream) {
     Staging & st = g_stage[dev];
     std::lock_guard<std::mutex> lk(st.mu);
     if (st.s) stage_flush_locked(st);
+    if (!st.pending || (st.s && st.s->stream == stream)) return;
+    HIP_CHECK(hipStreamWaitEvent(stream, st.ev, 0));
+}
+// the same without flushing the queue: only writes already sent are ordered before `stream`
+static void staged_writes_pending_wait(int dev, hipStream_t stream) {
+    if (dev < 0 || dev >= MX_MAX_DEVICES) return;
+    Staging & st = g_stage[dev];
+    std::lock_guard<std::mutex> lk(st.mu);
     if (!st.pending || (st.s && st.s->stream == stream)) return;
     HIP_CHECK(hipStreamWaitEvent(stream, st.ev, 0));
 }
@@ -313,6 +322,8 @@ static void be_free(ggml_backend_t b) {
                 (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n : 0),
                 (unsigned long long) (s->device >= 0 && s->device < MX_MAX_DEVICES ? g_stage[s->device].n_flush : 0));
     if (const char * kp = getenv("GGML_MI355X_KLOG")) klog_dump(kp);
+    split_stream_free(s);
+    hipSetDevice(s->device);
     for (GraphCache & gc : s->gslots) {
         if (gc.exec) hipGraphExecDestroy(gc.exec);
         if (gc.graph) hipGraphDestroy(gc.graph);
@@ -370,11 +381,20 @@ static bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const ggml_te
     }
     return true;
 }
+// Round 5: synchronize leaves queued staged writes queued. The scheduler synchronizes the
+// backend before EVERY graph input it copies (ggml-backend.cpp:1464-1471, no events with
+// one GPU), so flushing here made each of the ~6 inputs of a decoded token its own flush
+// launch plus a host wait for it (BENCH_r04: n_stage_flush == n_staged). A queued write
+// already holds its bytes in the pinned ring (the caller's buffer is free to reuse), and
+// every path that reads or orders device memory flushes first (staged_writes_wait), so
+// the token's inputs now go out in the one flush graph_compute issues.
 static void be_sync(ggml_backend_t b) {
     Stream * s = stream_of(b);
     const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));
-    staged_writes_wait(s->device, s->stream);   // queued input writes are part of "done"
+    static const bool flush_on_sync = env_flag("GGML_MI355X_SYNC_FLUSH");   // A/B: the round-4 behaviour
+    if (flush_on_sync) staged_writes_wait(s->device, s->stream);
+    else staged_writes_pending_wait(s->device, s->stream);   // flushed writes on another stream: ordered
     HIP_CHECK(hipStreamSynchronize(s->stream));
     s->us_sync += now_us() - t0;
 }
@@ -404,7 +424,6 @@ static const ggml_backend_i kBackendIface = {
 };
 static bool is_our_backend(ggml_backend_t b) { return b && b->iface.graph_compute == be_graph_compute; }
 
-static bool env_flag(const char * name) { const char * v = getenv(name); return v && *v && strcmp(v, "0") != 0; }
 
 static ggml_backend_t make_backend(Device * d) {
     HIP_CHECK(hipSetDevice(d->id));

@@ -185,6 +185,7 @@ void op_argsort(OpCtx & c, ggml_tensor * dst);
 void op_mul_mat(OpCtx & c, ggml_tensor * dst);
 void op_mul_mat_split(OpCtx & c, ggml_tensor * dst);
 int split_local_slices(const Stream * s, const ggml_tensor * w, void ** data, int64_t * lo, int64_t * hi);
+void split_stream_free(const Stream * main);   // be_free: drop the freed stream's row-split staging
 void op_mul_mat_id(OpCtx & c, ggml_tensor * dst);
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst);
 

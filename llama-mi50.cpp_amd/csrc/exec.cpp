@@ -83,6 +83,10 @@ static bool graph_signature_same(const ggml_cgraph * g, std::vector<uint64_t> & 
             c.put((uint64_t) (uintptr_t) s->data);
             c.put((uint64_t) s->nb[1] ^ ((uint64_t) s->type << 56) ^ ((uint64_t) s->op << 48));
             c.put((uint64_t) (uint32_t) s->ne[0] | ((uint64_t) (uint32_t) s->ne[1] << 32));
+            // round 5: the outer extents and strides as one mixed word, so a
+            // source from outside a split's view that changes only there re-captures
+            c.put(((uint64_t) s->ne[2] * 0x9E3779B97F4A7C15ull) ^ ((uint64_t) s->ne[3] * 0xC2B2AE3D27D4EB4Full) ^
+                  ((uint64_t) s->nb[2] * 0x165667B19E3779F9ull) ^ ((uint64_t) s->nb[3] * 0xD6E8FEB86659FD93ull));
             ++ns;
         }
         c.put(ns | ((uint64_t) n->flags << 8));

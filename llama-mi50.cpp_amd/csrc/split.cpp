@@ -190,6 +190,25 @@ static void * grow(void *& p, size_t & cap, int hip, size_t bytes) {
     return p;
 }
 
+// a freed backend's staging state goes with it (a later Stream allocated at the
+// same address found the old one's events and gather buffer, possibly on another GPU)
+void split_stream_free(const Stream * main) {
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    for (auto it = g_slices.begin(); it != g_slices.end();) {
+        if (it->first.first != main) { ++it; continue; }
+        SliceState & st = it->second;
+        const int d = it->first.second;
+        HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
+        if (st.ev_done) { HIP_CHECK(hipEventSynchronize(st.ev_done)); HIP_CHECK(hipEventDestroy(st.ev_done)); }
+        if (st.x) HIP_CHECK(hipFree(st.x));
+        if (st.y) HIP_CHECK(hipFree(st.y));
+        HIP_CHECK(hipSetDevice(main->device));
+        if (st.ev_main) { HIP_CHECK(hipEventSynchronize(st.ev_main)); HIP_CHECK(hipEventDestroy(st.ev_main)); }
+        if (st.g) HIP_CHECK(hipFree(st.g));
+        it = g_slices.erase(it);
+    }
+}
+
 static SliceState & slice_state(const Stream * main, int main_l, int d) {
     SliceState & st = g_slices[{main, d}];
     if (!st.ev_main) {
