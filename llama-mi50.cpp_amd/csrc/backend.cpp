@@ -54,7 +54,10 @@ static Device * dev_ctx(ggml_backend_dev_t d) { return (Device *) d->context; }
 // the GPU (drop-in profile, profiles/r04/), became one launch.
 struct StageEntry { const char * src; char * dst; uint32_t n, chunk0; };
 constexpr int kFlushMax = 16;                  // ranges per flush launch
-constexpr uint32_t kFlushChunk = 16384;        // bytes per workgroup
+// bytes per workgroup: one 16-B load per thread, i.e. ONE round trip over PCIe per workgroup
+// (16 KB per workgroup took four: the decoded token's 16 KB embedding row made the flush
+// 10.4 us, profiles/r05/)
+constexpr uint32_t kFlushChunk = 4096;
 struct StageFlushArgs { StageEntry e[kFlushMax]; int n; };
 
 __global__ __launch_bounds__(256) void k_stage_flush(StageFlushArgs a) {
@@ -726,7 +729,7 @@ void ggml_backend_mi355x_stats(ggml_backend_t b, uint64_t out[4]) {
 namespace mx {
 double time_mmvq(Stream * s, const ggml_tensor * const * w, const ggml_tensor * const * w2, int nw,
                  const ggml_tensor * x, ggml_tensor * dst, int iters);
-extern int g_tune[32];
+extern int g_tune[48];
 }
 
 extern "C" double ggml_backend_mi355x_time_mmvq(ggml_backend_t b, const ggml_tensor * const * w, const ggml_tensor * const * w2,
@@ -819,7 +822,7 @@ extern "C" size_t ggml_backend_mi355x_klog_read(char * out, size_t n) {
 namespace mx { unsigned g_tune_gen = 0; }   // part of every cgraph signature (exec.cpp)
 // a changed knob changes the launches a graph makes: captured graphs must not replay
 extern "C" void ggml_backend_mi355x_set_tune(int idx, int value) {
-    if (idx >= 0 && idx < 32 && mx::g_tune[idx] != value) { mx::g_tune[idx] = value; ++mx::g_tune_gen; }
+    if (idx >= 0 && idx < 48 && mx::g_tune[idx] != value) { mx::g_tune[idx] = value; ++mx::g_tune_gen; }
 }
 
 extern "C" int ggml_backend_mi355x_ab_variants(void) { return MX_AB_VARIANTS; }

@@ -362,6 +362,87 @@ static int try_fuse_mm_rows_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses
     return last - i + 1;
 }
 
+// Round 5: FLASH_ATTN_EXT of one decode token -> RESHAPE -> MUL_MAT(wo) -> ADD(residual)
+// (build_attn + the residual, src/models/llama.cpp; or the last layer's MUL_MAT ->
+// GET_ROWS x2 -> ADD chain above). The attention runs as split partials into scratch
+// (fa_dec2_partials: 4 x more workgroups, a quarter of the K/V each) and the residual GEMV
+// merges them in its prologue (XStage::fap) instead of a combine launch: the attention's
+// output tensor is never written. Returns the nodes consumed (0: no match).
+int fa_dec2_partials_nsplit(const ggml_tensor * fa);           // ops_fattn_dec.hip
+void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit);
+static const bool g_no_fa_split_o = getenv("GGML_MI355X_NO_FA_SPLIT_O") != nullptr;   // A/B
+static const bool g_fa_dec1_env = getenv("GGML_MI355X_FA_DEC1") != nullptr;
+static int fuse_attn_split_o(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
+    // g_tune[32] = 1 (or GGML_MI355X_NO_FA_SPLIT_O): the round-4 path (one-split attention, O from x)
+    if (g_no_fa_split_o || g_tune[32] == 1 || g_fa_dec1_env || g_tune[10] == 1 || !g_gemv2) return 0;
+    ggml_tensor * fa = g->nodes[i];
+    const int ns = fa_dec2_partials_nsplit(fa);
+    if (!ns) return 0;
+    const ggml_tensor * q = fa->src[0];
+    const int64_t D = fa->src[1]->ne[0], H = q->ne[2];
+    if (fa->type != GGML_TYPE_F32 || !mx_is_contiguous(fa) || mx_nelements(fa) != D * H) return 0;
+    if (uses[fa] != 1 || (fa->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    ggml_tensor * rs = nullptr, * mm = nullptr;
+    int jm = -1;
+    for (int j = i + 1; j < g->n_nodes && j < i + 8; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (is_view_op(n->op)) {
+            if (!rs && n->src[0] == fa) rs = n;
+            continue;
+        }
+        if (n->op == GGML_OP_MUL_MAT && rs && n->src[1] == rs) { mm = n; jm = j; }
+        break;
+    }
+    if (!mm || rs->op != GGML_OP_RESHAPE || rs->ne[0] != D * H || mx_nrows(rs) != 1 || uses[rs] != 1 || (rs->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    const ggml_tensor * wo = mm->src[0];
+    if (tensor_is_split(wo) || !gemv2_ok(wo, rs, mm) || !gemv2_fap_ok(wo->type, wo->ne[0], wo->ne[1])) return 0;
+    if (uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    // the tail: ADD(mm, res) right after, or GET_ROWS(mm) , GET_ROWS(res) -> ADD
+    const ggml_tensor * res = nullptr;
+    ggml_tensor * add = nullptr, * g1 = nullptr, * g2 = nullptr;
+    int last = -1;
+    if (jm + 1 < g->n_nodes && g->nodes[jm + 1]->op == GGML_OP_ADD) {
+        add = g->nodes[jm + 1];
+        res = add->src[0] == mm ? add->src[1] : (add->src[1] == mm ? add->src[0] : nullptr);
+        last = jm + 1;
+    } else {
+        for (int j = jm + 1; j < g->n_nodes && j <= jm + 4; ++j) {
+            ggml_tensor * n = g->nodes[j];
+            if (is_view_op(n->op)) continue;
+            if (n->op == GGML_OP_GET_ROWS && !g1 && n->src[0] == mm) { g1 = n; continue; }
+            if (n->op == GGML_OP_GET_ROWS && !g2 && n->src[0] != mm) { g2 = n; continue; }
+            if (n->op == GGML_OP_ADD && g1 && g2 && ((n->src[0] == g1 && n->src[1] == g2) || (n->src[0] == g2 && n->src[1] == g1))) {
+                add = n; last = j;
+            }
+            break;
+        }
+        if (!add) return 0;
+        for (const ggml_tensor * gr : {g1, g2}) {   // one token: both GET_ROWS are the identity
+            if (gr->type != GGML_TYPE_F32 || gr->src[0]->type != GGML_TYPE_F32 || mx_nrows(gr->src[0]) != 1 || mx_nrows(gr) != 1 ||
+                mx_nelements(gr->src[1]) != 1 || uses[gr] != 1 || (gr->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+        }
+        res = g2->src[0];
+    }
+    if (!res || res == mm || add->type != GGML_TYPE_F32 || res->type != GGML_TYPE_F32) return 0;
+    if (!mx_are_same_shape(res, mm) || !mx_are_same_shape(add, mm) || !mx_is_contiguous(res) || !mx_is_contiguous(add)) return 0;
+    // the epilogue reads each residual element and writes the sum from the same thread
+    const bool same = res->nb[1] == add->nb[1];
+    if (!fused_io_ok({add}, {res}, {{add, same ? res : nullptr}})) return 0;
+    const size_t part_bytes = (size_t) H * ns * (D + 2) * sizeof(float) + 256;
+    if (c.scratch->avail() < part_bytes) return 0;
+    for (int j = i; j <= last; ++j) {
+        deferred_guard_node(c, g->nodes[j]);
+        act_cache_invalidate(c.s, g->nodes[j]);
+    }
+    float * part = (float *) c.scratch->take(part_bytes);
+    fa_dec2_partials(c, fa, part, ns);
+    XStage xs{nullptr, nullptr, 0.0f, 0};
+    xs.xcd = g_tune[15] != 1;
+    xs.fap = part; xs.fap_ns = ns; xs.fap_d = (int) D;
+    gemv2_launch(c, wo, nullptr, xs, (float *) add->data, (const float *) res->data);
+    return last - i + 1;
+}
+
 // MUL_MAT(gate) , MUL_MAT(up) , GLU(gate, up) with one activation column:
 // one pass over the activation, two weight streams (ggml-cuda.cu:2145-2181).
 static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses, bool gemv_only = false) {
@@ -487,7 +568,7 @@ static bool try_group_mm(OpCtx & c, ggml_cgraph * g, int i, std::unordered_map<c
 // (latency-bound at ~2 TB/s) gained nothing, and budgets past ~24 MB outlast the
 // attention itself. Budget: g_tune[23] MB (> 0), else GGML_MI355X_FA_PREFETCH_MB
 // (default 16; 0 = off); minimum matrix size g_tune[24] KB (-1 = none).
-extern int g_tune[32];
+extern int g_tune[48];
 static int g_pf_mb_env = getenv("GGML_MI355X_FA_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_FA_PREFETCH_MB")) : 16;
 static int g_gpf_mb_env = getenv("GGML_MI355X_GEMV_PREFETCH_MB") ? atoi(getenv("GGML_MI355X_GEMV_PREFETCH_MB")) : 0;
 static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q, bool nofa) {
@@ -579,6 +660,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             if (n->op == GGML_OP_MUL_MAT && !g_no_attn_nofa) {
                 const int k = fuse_attn_nofa(c, g, i, uses);
                 if (k > 0) { i += k - 1; s->n_fused += 3; s->n_nodes_run += 4; deferred_retire(s, g, i0, i); continue; }
+            }
+            if (n->op == GGML_OP_FLASH_ATTN_EXT) {
+                const int k = fuse_attn_split_o(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             }
             if (n->op == GGML_OP_FLASH_ATTN_EXT) {
                 const int k = fuse_attn_oproj(c, g, i, uses);

@@ -39,9 +39,12 @@ struct LdsAct {
 // *_H2 modes hold two 16-value halves per thread (K up to 32 * threads); the plain modes
 // one (K <= 16 * threads, e.g. n_embd 4096 on 256 threads) and so half the registers,
 // which is occupancy on the large grids.
-enum { XS_F32 = 0, XS_NORM = 1, XS_Q8 = 2, XS_F32_LDS = 3, XS_NORM_LDS = 4, XS_F32_H2 = 5, XS_NORM_H2 = 6 };
+// XS_FAP2/4/8 (round 5): the attention's split partials (up to 2/4/8 splits) merged into x
+enum { XS_F32 = 0, XS_NORM = 1, XS_Q8 = 2, XS_F32_LDS = 3, XS_NORM_LDS = 4, XS_F32_H2 = 5, XS_NORM_H2 = 6,
+       XS_FAP2 = 7, XS_FAP4 = 8, XS_FAP8 = 9 };
 __host__ __device__ constexpr bool xs_norm(int m) { return m == XS_NORM || m == XS_NORM_H2; }
 __host__ __device__ constexpr bool xs_f32reg(int m) { return m == XS_F32 || m == XS_F32_H2; }
+__host__ __device__ constexpr int xs_fap(int m) { return m == XS_FAP2 ? 2 : m == XS_FAP4 ? 4 : m == XS_FAP8 ? 8 : 0; }
 
 __host__ __device__ inline size_t gemv_lds_base(int64_t K) { return ((size_t) K + (size_t) (K / 32) * 8 + 64 + 15) & ~(size_t) 15; }
 __host__ __device__ inline size_t gemv_lds_bytes(int64_t K, int mode = XS_Q8) {
@@ -53,8 +56,9 @@ __host__ __device__ inline float * gemv_lds_red(char * smem, int64_t K) { return
 // MI355X (tools/opbench.py ffn_block / q_q4k, profiles/r01): grids of one block per CU
 // (the 4096-row projections) are latency-bound and win with registers; grids of several
 // waves' worth per SIMD (SwiGLU, lm_head) win with the occupancy LDS staging buys.
-extern int g_tune[32];
+extern int g_tune[48];
 inline int gemv_mode(const XStage & xs, int64_t K, int64_t n_waves = 0, int nt = 256) {
+    if (xs.fap) return xs.fap_ns <= 4 ? XS_FAP4 : XS_FAP8;   // (XS_FAP2 not instantiated)
     if (xs.q8) return XS_Q8;
     bool lds = n_waves >= 2048;
     if (g_tune[9] == 1) lds = true;    // sweeps
@@ -230,8 +234,10 @@ __device__ __forceinline__ void q8_half(const float (&v)[16], int hg, LdsAct a) 
 template <int NT, int MODE>
 struct StageRegs {
     static constexpr int HPT = (MODE == XS_F32_H2 || MODE == XS_NORM_H2) ? 2 : 1;   // f32 halves per thread
-    float v[HPT][16];
+    static constexpr int NSP = xs_fap(MODE) ? xs_fap(MODE) : 1;                      // attention splits
+    float v[xs_fap(MODE) ? NSP : HPT][16];       // XS_FAP*: split s's O of the thread's half
     float w[xs_norm(MODE) ? HPT : 1][16];
+    float ml[NSP][2];                            // XS_FAP*: split s's (max, sum) of the half's head
 };
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
@@ -272,6 +278,24 @@ __device__ __forceinline__ void stage_issue(const XStage & xs, int K, const LdsA
         char * stg = (char *) a.q + gemv_lds_base(K);
         dma_to_lds<NT, 16>(xs.x, stg, 4 * K);
         if constexpr (MODE == XS_NORM_LDS) dma_to_lds<NT, 16>(xs.nw, stg + 4 * K, 4 * K);
+    } else if constexpr (xs_fap(MODE)) {
+        // the thread's 16 values lie in one head (fap_d % 16 == 0): its O run and the
+        // (max, sum) pair of every split, all loads in flight together (K <= 16 NT)
+        const int t = threadIdx.x, hg = min(t, K / 16 - 1);
+        const int hh = (16 * hg) / xs.fap_d, d0 = 16 * hg - hh * xs.fap_d;
+#pragma unroll
+        for (int s = 0; s < xs_fap(MODE); ++s) {
+            const float * b = xs.fap + ((size_t) hh * xs.fap_ns + min(s, xs.fap_ns - 1)) * (xs.fap_d + 2);
+            // rows of fap_d + 2 floats: 8-byte aligned only
+#pragma unroll
+            for (int j = 0; j < 16; j += 4) {
+                float4 f;
+                __builtin_memcpy(&f, __builtin_assume_aligned(b + d0 + j, 8), 16);
+                r.v[s][j] = f.x; r.v[s][j + 1] = f.y; r.v[s][j + 2] = f.z; r.v[s][j + 3] = f.w;
+            }
+            const float2 m = *(const float2 *) (b + xs.fap_d);
+            r.ml[s][0] = m.x; r.ml[s][1] = m.y;
+        }
     } else {
         const int t = threadIdx.x, nhg = K / 16;
 #pragma unroll
@@ -359,6 +383,30 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
                 for (int j = 0; j < 16; ++j) v2[j] = (v2[j] * scale) * w2[j];
             }
             q8_half<true>(v2, hg, a);
+        }
+    } else if constexpr (xs_fap(MODE)) {
+        // merge of the splits (k_fattn_dec2_combine's arithmetic): weights 2^(m_s - max),
+        // x = sum_s w_s O_s / sum_s w_s l_s
+        constexpr int NS = xs_fap(MODE);
+        if (t < nhg) {                               // nhg is even: partner lanes stay paired
+            float mx = -INFINITY;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) if (s < xs.fap_ns) mx = fmaxf(mx, r.ml[s][0]);
+            float wt[NS], l = 0.f;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                wt[s] = s < xs.fap_ns && r.ml[s][0] != -INFINITY ? __builtin_amdgcn_exp2f(r.ml[s][0] - mx) : 0.f;
+                l += wt[s] * r.ml[s][1];
+            }
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                float o = 0.f;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) o += wt[s] * r.v[s][j];
+                v[j] = l == 0.f ? 0.f : o / l;
+            }
+            q8_half(v, t, a);
         }
     } else if constexpr (xs_norm(MODE)) {
         // K <= 16 * HPT * NT (GEMV2_MAX_NORM_K checks it for the 256-thread kernels)
@@ -655,6 +703,14 @@ __device__ __forceinline__ void gemv_rows_staged(const char * const (&rows)[NM],
                 asm volatile("" : "+v"(sr.v[h][j]));
                 if constexpr (xs_norm(MODE)) asm volatile("" : "+v"(sr.w[h][j]));
             }
+    }
+    if constexpr (xs_fap(MODE) != 0) {
+#pragma unroll
+        for (int s = 0; s < StageRegs<NT, MODE>::NSP; ++s) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(sr.v[s][j]));
+            asm volatile("" : "+v"(sr.ml[s][0]), "+v"(sr.ml[s][1]));
+        }
     }
     if (!MX_DBG(xs.dbg & 1)) stage_finish<NT, MODE, UPL * NM * w2_loads<QT>()>(xs, K, a, red, sr);
     fence();                                  // older than the staged x: already landed

@@ -24,12 +24,19 @@ struct XStage {
     int xcd = 1;                    // XCD-contiguous block order (g_tune[15] = 1 turns it off)
     int drain = 0;                  // f32 LDS-staged sources: wait for every weight load
                                     // before the prologue (g_tune[14] = 1; A/B)
+    // round 5: x = the decode attention's split partials merged in the prologue (the output
+    // projection after fa_dec2_partials): per query head hh and split s, fap + (hh * fap_ns +
+    // s) * (fap_d + 2) floats hold the unnormalised O (fap_d values), the max (log2 domain)
+    // and the sum
+    const float * fap = nullptr;
+    int fap_ns = 0, fap_d = 0;
 };
 
-extern int g_tune[32];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)
+extern int g_tune[48];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)
 extern bool g_gemv2;        // v2 GEMV enabled (GGML_MI355X_GEMV_V1 turns it off)
 
 bool gemv2_type_ok(int t);
+bool gemv2_fap_ok(int type, int64_t K, int64_t M);   // XStage::fap source instantiated for this GEMV
 bool gemv2_ok(const ggml_tensor * w, const ggml_tensor * x, const ggml_tensor * dst);
 // dst[r] = epi(W[r]·x): w2 != null → silu(W·x)*(W2·x); res != null → + res[r].
 // q8out (SwiGLU only, rows % 32 == 0): also write the q8 form of dst there.

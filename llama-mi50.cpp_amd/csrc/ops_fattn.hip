@@ -22,7 +22,7 @@ namespace mx {
 // critical path (decode FA v2: 6.95 -> 5.56 us at 256 keys with the same change)
 __device__ __forceinline__ float fa_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
-extern int g_tune[32];
+extern int g_tune[48];
 
 constexpr int FA_TILE = 256;
 constexpr int FA_MAXG = 8;

@@ -22,7 +22,7 @@
 #include "backend.h"
 #include "quants.cuh"
 
-namespace mx { extern int g_tune[32]; }
+namespace mx { extern int g_tune[48]; }
 
 namespace mx {
 
@@ -33,6 +33,7 @@ struct FaDecArgs {
     const char * mask; size_t m1, m3; int mne3;
     char * dst; size_t d1, d2, d3;
     float * part;                  // [rows][nsplit][G*(D+2)] partials (scratch)
+    int to_part;                   // LONG: partials even for one split (fa_dec2_partials)
     unsigned int * cnt;            // per (q row, seq, KV head) arrival counters, zero between launches
     int n_q, n_kv, H, Hkv, ns_kv, nsplit;
     float scale;
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             Lw += wl[w][h] * f;
             O += wo[w][h][d] * f;
         }
-        if (p.nsplit == 1) {
+        if (p.nsplit == 1 && !(LONG && p.to_part)) {
             float * out = (float *) (p.dst + (size_t) (hb + h) * p.d1 + (size_t) iq1 * p.d2 + (size_t) iq3 * p.d3);
             out[d] = Lw == 0.f ? 0.f : O / Lw;
         } else if constexpr (LONG) {      // plain stores: the combine is a later launch
@@ -605,6 +606,71 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     FD(128, 4, 4) FD(128, 1, 4) FD(128, 2, 4) FD(128, 8, 4) FD(64, 1, 4) FD(64, 2, 4) FD(64, 4, 4) FD(64, 8, 4)
 #undef FD
     MX_ABORT("fattn dec2 D=%d G=%d NW=%d", D, f.G, f.NW);
+}
+
+// Round 5: decode attention whose split partials the output projection merges in its
+// prologue (exec.cpp fuse_attn_split_o, XStage::fap). At llama-bench tg128 (256 keys) the
+// one-split form ran 32 workgroups of 16 waves, each pulling 128 KB of K/V through one
+// CU (~6.5 us per layer, 82 % of wave time parked on waits); the LONG geometry with 64-key
+// chunks runs Hkv x Gt x 4 four-wave workgroups with 32 KB each, and its (O, max, sum)
+// partials need no combine launch (~4 us, profiles/r04/fa256_split_ab.txt) because the
+// output projection's 256 workgroups merge them while their weight loads are in flight.
+// Partial layout (G = 1): head hh, split s at part + (hh * nsplit + s) * (D + 2).
+static int fa_split_ni() {   // key rows per lane per chunk: 4 (64-key chunks), 2 (32) or 8 (128); g_tune[33]
+    static const int ni = [] { const char * v = getenv("GGML_MI355X_FA_SPLIT_NI"); const int n = v ? atoi(v) : 4; return n == 2 || n == 8 ? n : 4; }();
+    return g_tune[33] == 2 || g_tune[33] == 4 || g_tune[33] == 8 ? g_tune[33] : ni;
+}
+int fa_dec2_partials_nsplit(const ggml_tensor * fa) {
+    const ggml_tensor * q = fa->src[0], * k = fa->src[1];
+    if (!fa_dec2_ok(fa) || k->ne[0] != 128 || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1) return 0;
+    if (fa->src[3] && fa->src[3]->ne[3] != 1) return 0;
+    const int64_t cs = 4 * fa_split_ni() * 4;                   // 4 waves x NI rows x 4 keys per instruction
+    const int64_t ns = mx_ceil_div(k->ne[1], cs);
+    return ns >= 1 && ns <= 8 ? (int) ns : 0;
+}
+void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit) {
+    const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
+    FaDecArgs a{};
+    a.q = (const char *) q->data; a.q1 = q->nb[1]; a.q2 = q->nb[2]; a.q3 = q->nb[3];
+    a.k = (const char *) k->data; a.k1 = k->nb[1]; a.k2 = k->nb[2]; a.k3 = k->nb[3];
+    a.v = (const char *) v->data; a.v1 = v->nb[1]; a.v2 = v->nb[2]; a.v3 = v->nb[3];
+    if (m) { a.mask = (const char *) m->data; a.m1 = m->nb[1]; a.m3 = m->nb[3]; a.mne3 = (int) m->ne[3]; }
+    else a.mne3 = 1;
+    a.dst = (char *) dst->data; a.d1 = dst->nb[1]; a.d2 = dst->nb[2]; a.d3 = dst->nb[3];
+    a.n_q = 1; a.n_kv = (int) k->ne[1]; a.H = (int) q->ne[2]; a.Hkv = (int) k->ne[2];
+    a.ns_kv = 1;
+    a.scale = mx_op_param<float>(dst, 0);
+    a.nsplit = nsplit;
+    a.part = part;
+    a.to_part = 1;
+    a.cnt = c.s->fa_cnt;
+    a.trace = mx_trace_slot(0);
+    a.trace_blk = mx_trace_blocks();
+    const unsigned gx = (unsigned) a.H;                          // G = 1: one query head per workgroup
+    unsigned pf_rows = 0;
+    a.pf_n = c.s->pf_n;
+    for (int r = 0; r < a.pf_n; ++r) {
+        a.pf[r] = c.s->pf_ptr[r]; a.pf_eighth[r] = c.s->pf_len[r] / 8; a.pf_lines[r] = (unsigned) (c.s->pf_take[r] / 128);
+    }
+    if (a.pf_n && (gx * a.nsplit) % 8 == 0) {   // ~160 prefetch workgroups (see fa_dec2_run)
+        pf_rows = (unsigned) mx_ceil_div(160, gx);
+        while ((gx * pf_rows) % 8) ++pf_rows;
+    } else a.pf_n = 0;
+    const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
+    const bool kq = k->type == GGML_TYPE_Q8_0;
+    const int ni = fa_split_ni();
+    MX_KLOG("fattn_dec2_part D=128 G=1 NI=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u", ni, nsplit, a.n_kv, a.H, a.Hkv,
+            (int) kq, pf_rows);
+    if (ni == 2) {
+        if (kq) k_fattn_dec2<128, 1, 4, true, 2, true><<<grid, 256, 0, c.st>>>(a);
+        else k_fattn_dec2<128, 1, 4, false, 2, true><<<grid, 256, 0, c.st>>>(a);
+    } else if (ni == 8) {
+        if (kq) k_fattn_dec2<128, 1, 4, true, 8, true><<<grid, 256, 0, c.st>>>(a);
+        else k_fattn_dec2<128, 1, 4, false, 8, true><<<grid, 256, 0, c.st>>>(a);
+    } else {
+        if (kq) k_fattn_dec2<128, 1, 4, true, 4, true><<<grid, 256, 0, c.st>>>(a);
+        else k_fattn_dec2<128, 1, 4, false, 4, true><<<grid, 256, 0, c.st>>>(a);
+    }
 }
 
 // ---------------------------------------------------------------------------

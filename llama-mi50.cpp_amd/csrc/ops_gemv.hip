@@ -7,7 +7,7 @@
 
 namespace mx {
 
-int g_tune[32] = {0};
+int g_tune[48] = {0};
 // GGML_MI355X_TUNE="i=v,i=v": the same knobs for processes that load the backend without
 // calling ggml_backend_mi355x_set_tune (the reference libllama in drop-in A/B runs)
 static const bool g_tune_env = [] {
@@ -15,7 +15,7 @@ static const bool g_tune_env = [] {
         for (const char * p = e; *p;) {
             int i = 0, v = 0, n = 0;
             if (sscanf(p, "%d=%d%n", &i, &v, &n) != 2) break;
-            if (i >= 0 && i < 32) g_tune[i] = v;
+            if (i >= 0 && i < 48) g_tune[i] = v;
             p += n;
             while (*p == ',' || *p == ' ') ++p;
         }
@@ -142,6 +142,15 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
 
 template <int QT, int LPR, int UPL, int EPI, int W, bool EXT>
 static void launch_mode(hipStream_t st, const G2Args & p, int mode, dim3 grid, size_t lds) {
+    if (xs_fap(mode)) {   // the output projection after fa_dec2_partials: residual epilogue only
+        // (instantiated for the decode output projection's geometries only: gemv2_fap_ok)
+        if constexpr (EPI == 2 && !EXT && W == 4 && (UPL == 4 || (LPR == 64 && UPL == 2))) {
+            if (mode == XS_FAP8) k_gemv2<QT, LPR, UPL, EPI, W, XS_FAP8, EXT><<<grid, 64 * W, lds, st>>>(p);
+            else k_gemv2<QT, LPR, UPL, EPI, W, XS_FAP4, EXT><<<grid, 64 * W, lds, st>>>(p);
+            return;
+        }
+        MX_ABORT("gemv2: attention-partials source needs the residual epilogue, 4 waves");
+    }
     switch (mode) {
         case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8, EXT><<<grid, 64 * W, lds, st>>>(p); break;
         case XS_NORM_LDS: k_gemv2<QT, LPR, UPL, EPI, W, XS_NORM_LDS, EXT><<<grid, 64 * W, lds, st>>>(p); break;
@@ -218,6 +227,16 @@ static void pick_cfg(int type, int units, int nrows, bool glu, int & lpr, int & 
     const int base = glu ? 2 : 0;
     if (g_tune[base]) lpr = g_tune[base];
     if (g_tune[base + 1]) upl = g_tune[base + 1];
+}
+
+// the residual GEMV can take its x as attention split partials (XS_FAP*: fa_dec2_partials):
+// a geometry instantiated for it (launch_mode), one 16-value half per thread
+bool gemv2_fap_ok(int type, int64_t K, int64_t M) {
+    if (!gemv2_type_ok(type) || K > 16 * 256 || K % 32) return false;
+    int lpr, upl;
+    pick_cfg(type, units_of(type, K), (int) M, false, lpr, upl);
+    if (type != GGML_TYPE_Q4_K && type != GGML_TYPE_Q6_K) upl = 4;   // launch_type: the reduced tuning grid
+    return upl == 4 || (lpr == 64 && upl == 2);
 }
 
 bool gemv2_type_ok(int t) {

@@ -141,11 +141,18 @@ def test_llama3_8b_width_decode(l8b, tmp_path, fa):
     # libllama's one-row inp_out_ids GET_ROWS pair (exec.cpp try_fuse_mm_rows_add), whose
     # ADD the allocator puts over the dead attention output: that GEMV streams from a q8
     # copy of x (mode 2, like the down projections), the others read x itself (mode 0)
-    assert k["gemv2 epi=2 mode=0 M=4096 q8o=0"] + k["gemv2 epi=2 mode=2 M=4096 q8o=0"] == 2 * n * L, k
-    assert k["gemv2 epi=2 mode=0 M=4096 q8o=0"] >= n * (L - 1), k
     assert k["gemv2 epi=0 mode=0 M=4096 q8o=0"] == 0, k
     if fa:
-        assert k["fattn_dec2"] + k["fattn_dec"] == n * L, k
+        # round 5 (exec.cpp fuse_attn_split_o): the attention writes split partials and the
+        # O projection merges them in its prologue (mode 8 = XS_FAP4) in every layer, the
+        # last one's GET_ROWS chain included; the down projections stream the q8 copy (mode 2)
+        assert k["fattn_dec2_part"] == n * L, k
+        assert k["gemv2 epi=2 mode=8 M=4096 q8o=0"] == n * L, k
+        assert k["gemv2 epi=2 mode=2 M=4096 q8o=0"] == n * L, k
+        assert k["gemv2 epi=2 mode=0 M=4096 q8o=0"] == 0, k
+    else:
+        assert k["gemv2 epi=2 mode=0 M=4096 q8o=0"] + k["gemv2 epi=2 mode=2 M=4096 q8o=0"] == 2 * n * L, k
+        assert k["gemv2 epi=2 mode=0 M=4096 q8o=0"] >= n * (L - 1), k
     assert k["mmvq1"] == 0, k                                  # no first-generation fallback GEMV
 
 

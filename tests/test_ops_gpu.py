@@ -676,3 +676,78 @@ def test_attn_oproj_decode_chain(pkg, backend, orc, n_kv, H, Hkv, M, mask_tail, 
     assert not any(l.startswith("attn_o ") for l in backend.klog_read())
     backend.klog(False)
     assert nmse(y, y3) < 1e-5
+
+
+@pytest.mark.parametrize("kind", ["f16", "q8_0"])
+@pytest.mark.parametrize("n_kv,H,Hkv,M,wt,mask_tail,ni", [
+    (256, 32, 8, 4096, "q4_K", 0, 4),      # llama-bench tg128: 4 splits of 64 keys
+    (256, 32, 8, 4096, "q4_K", 200, 4),    # mostly masked: splits 1-3 fully masked (max -inf)
+    (256, 32, 8, 4096, "q4_K", 0, 2),      # 8 splits of 32 keys (XS_FAP8)
+    (37, 32, 8, 4096, "q5_K", 5, 4),       # one ragged split
+    (130, 32, 4, 1000, "q6_K", 0, 4),      # 3 splits, ragged rows (M % 16 != 0), GQA 8
+    (1, 8, 2, 512, "q4_0", 0, 4),          # one key, small model (lpr 64 geometry)
+    (200, 16, 16, 2048, "q8_0", 17, 2),    # no GQA, 7 splits
+])
+def test_attn_split_oproj_decode(pkg, backend, orc, kind, n_kv, H, Hkv, M, wt, mask_tail, ni):
+    """Round 5: FLASH_ATTN_EXT -> RESHAPE -> MUL_MAT(wo) -> ADD(residual) of one decode token
+    as the attention's split partials (fa_dec2_partials, 64- or 32-key chunks) merged in the
+    residual GEMV's prologue (XStage::fap, modes 8 / 9) — the default decode path (exec.cpp
+    fuse_attn_split_o) — against the node-by-node oracle, and against the round-4 path
+    (g_tune[32] = 1: one-split attention, O projection from x)"""
+    from qgen import KV_TYPES, kv_rows
+    D = 128
+    rng = np.random.default_rng(n_kv * 7 + H + M)
+    q = rng.standard_normal((H, 1, D)).astype(np.float32)
+    k = kv_rows(kind, Hkv, n_kv, D, rng, orc)
+    v = kv_rows(kind, Hkv, n_kv, D, rng, orc)
+    mask = np.zeros((1, n_kv), np.float32)
+    if mask_tail:
+        mask[0, n_kv - mask_tail:] = -np.inf
+    m16 = mask.astype(np.float16).view(np.uint16)
+    scale = 1.0 / np.sqrt(D)
+    K = D * H
+    tw_t = NAMES[wt]
+    w, rb = rand_quant(tw_t, M, K, rng)
+    r = rng.standard_normal((1, M)).astype(np.float32)
+    tid = KV_TYPES[kind]
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, 1, H)
+        tk = ctx.new_tensor(tid, D, n_kv, Hkv)
+        tv = ctx.new_tensor(tid, D, n_kv, Hkv)
+        tm = ctx.new_tensor("f16", n_kv, 1)
+        tw = ctx.new_tensor(tw_t, K, M)
+        tr = ctx.new_tensor("f32", M, 1)
+        fa = ctx.flash_attn_ext(tq, tk, tv, tm, scale)
+        y = ctx.add(ctx.mul_mat(tw, ctx.reshape(fa, K, 1)), tr)
+        return [y], [(tq, q), (tk, k), (tv, v), (tm, m16), (tw, w), (tr, r)]
+
+    lib = pkg._lib.load()
+    lib.ggml_backend_mi355x_set_tune(33, ni)
+    try:
+        backend.klog(True)
+        y = run(pkg, backend, build)[0].reshape(M)
+        log = backend.klog_read()
+        backend.klog(False)
+        ns = -(-n_kv // (16 * ni))
+        assert any(l.startswith("fattn_dec2_part ") and f"NI={ni} nsplit={ns} " in l for l in log), log
+        mode = 8 if ns <= 4 else 9
+        assert any(l.startswith("gemv2 ") and "epi=2" in l and f"mode={mode} " in l for l in log), log
+        y2 = run(pkg, backend, build)[0].reshape(M)
+        lib.ggml_backend_mi355x_set_tune(32, 1)
+        backend.klog(True)
+        y3 = run(pkg, backend, build)[0].reshape(M)
+        log3 = backend.klog_read()
+        backend.klog(False)
+        assert not any(l.startswith("fattn_dec2_part ") for l in log3), log3
+    finally:
+        lib.ggml_backend_mi355x_set_tune(32, 0)
+        lib.ggml_backend_mi355x_set_tune(33, 0)
+    att = orc.flash_attn_t(q, k, v, m16, scale, tid, 0.0, 0.0).reshape(1, K)
+    ref = orc.mul_mat(tw_t, w, rb, att)[0] + r[0]
+    ref_exact = orc.mul_mat(tw_t, w, rb, att, exact=True)[0] + r[0]
+    assert np.all(np.isfinite(y))
+    assert nmse(y, ref) < 5e-4, nmse(y, ref)
+    assert nmse(y, ref_exact) < 5e-4, nmse(y, ref_exact)
+    assert np.array_equal(y, y2)                  # deterministic (no atomics in either launch)
+    assert nmse(y, y3) < 1e-5, nmse(y, y3)
