@@ -6,9 +6,10 @@ heads, n_ff 14336, vocab 128256) with Q4_K_M weights (Q4_K + Q6_K attn_v/ffn_dow
 the 16 use_more_bits layers + Q6_K output), synthetic random weights (no checkpoints
 offline).
 
-Headline (`value`, round 4): the drop-in path the north star names — the reference's own
-libllama (oracle/_ref/ref-llama-bench: llama-bench's test_gen loop, tools/llama-bench/
-llama-bench.cpp:1991-2010) loading libggml-mi355x.so through GGML_BACKEND_PATH, -ngl 99,
+Headline (`value`, round 4; round 5: measured by the reference's own llama-bench, built
+unmodified from tools/llama-bench/llama-bench.cpp + common/ into oracle/_ref/llama-bench) —
+the drop-in path the north star names: the reference's libllama loading
+libggml-mi355x.so through GGML_BACKEND_PATH, -ngl 99,
 -fa 1, on a synthetic GGUF of that shape (tools/gguf_synth.py). A *step* is one tg128
 repetition (llama-bench -r K after its own untimed warmup run: W - 1 further untimed
 repetitions run first); value = K * 128 tokens / the sum of the K repetitions' times as
@@ -192,16 +193,16 @@ def cpu_baseline(args):
     """Reference CPU backend (oracle/_ref, built from /root/reference sources) on the same
     GGUF, bounded sample, every CPU thread this process is granted (-t nproc).
     Returns None when the reference build is absent."""
-    if not os.path.exists(REF_BENCH) or args.no_cpu_baseline:
+    if not (os.path.exists(REF_BENCH) or os.path.exists(LLAMA_BENCH)) or args.no_cpu_baseline:
         return None
     threads = host_threads()
     try:
         gguf = bench_gguf()
-        r = subprocess.run([REF_BENCH, "-m", gguf, "-t", str(threads), "-ngl", "0", "-fa", "1", "-p", str(args.cpu_pp),
-                            "-n", str(args.cpu_tg), "-r", str(args.cpu_reps)], capture_output=True, text=True, timeout=900)
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
-        res = json.loads(line)
-        return {"value": res["tg_tok_s"], "unit": "tok/s", "cores": threads, "kind": "reference",
+        res, err = ref_bench(gguf, dict(os.environ), ["-t", threads, "-ngl", 0, "-fa", 1, "-p", args.cpu_pp,
+                                                      "-n", args.cpu_tg, "-r", args.cpu_reps])
+        if isinstance(res, str):
+            raise RuntimeError(res)
+        return {"value": res["tg_tok_s"], "unit": "tok/s", "cores": threads, "kind": "reference", "tool": bench_tool(),
                 "pp_tok_s": res.get("pp_tok_s"), "tg_samples": res.get("tg_samples"), "pp_samples": res.get("pp_samples"),
                 "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
                 "sample": f"reference CPU backend (libllama+ggml-cpu from /root/reference), same GGUF, the bench's own "
@@ -213,9 +214,45 @@ def cpu_baseline(args):
         return {"value": None, "unit": "tok/s", "cores": threads, "kind": "reference", "sample": f"failed: {e}"}
 
 
+# Round 5: the reference's own llama-bench, unmodified (oracle/Makefile builds
+# tools/llama-bench/llama-bench.cpp with the common/ sources it links from /root/reference);
+# ref-llama-bench (the round-4 restatement of its loop) stays as the fallback when absent.
+LLAMA_BENCH = os.path.join(ROOT, "oracle", "_ref", "llama-bench")
+
+
+def bench_tool():
+    return "llama-bench" if os.path.exists(LLAMA_BENCH) else "ref-llama-bench"
+
+
 def ref_bench(gguf, env, flags, timeout=900):
-    """one ref-llama-bench run -> its JSON line (or an error string)"""
-    r = subprocess.run([REF_BENCH, "-m", gguf] + [str(f) for f in flags], capture_output=True, text=True,
+    """one llama-bench run -> {tg_tok_s, tg_samples, pp_tok_s, pp_samples} (or an error
+    string). With the real tool: `-o jsonl`, one line per test; its own defaults for
+    everything not passed (-b 2048 -ub 512, its warmup run); -c is the restatement's flag
+    only (llama-bench sizes the context from -p + -n + -d itself)."""
+    flags = [str(f) for f in flags]
+    if bench_tool() == "llama-bench":
+        fl = []
+        i = 0
+        while i < len(flags):
+            if flags[i] == "-c":
+                i += 2
+                continue
+            fl.append(flags[i])
+            i += 1
+        r = subprocess.run([LLAMA_BENCH, "-m", gguf, "-o", "jsonl"] + fl, capture_output=True, text=True,
+                           timeout=timeout, env=env)
+        lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return f"failed rc={r.returncode}: {r.stderr[-300:]}", r.stderr
+        res = {"tool": "llama-bench", "pp_tok_s": 0.0, "tg_tok_s": 0.0, "pp_samples": [], "tg_samples": []}
+        for t in lines:
+            kind = "tg" if t["n_gen"] > 0 and t["n_prompt"] == 0 else "pp"
+            res[f"{kind}_tok_s"] = t["avg_ts"]
+            res[f"{kind}_samples"] = t["samples_ts"]
+            res[f"{kind}_test"] = {k: t[k] for k in ("n_prompt", "n_gen", "n_depth", "n_batch", "n_ubatch", "n_threads",
+                                                     "flash_attn", "type_k", "type_v", "split_mode", "avg_ts", "stddev_ts")}
+        return res, r.stderr
+    r = subprocess.run([REF_BENCH, "-m", gguf] + flags, capture_output=True, text=True,
                        timeout=timeout, env=env)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not line:
@@ -245,7 +282,7 @@ def dropin_tg(args, env, flags, key):
     value, ms = tg_from_samples(res["tg_samples"], args.tg)
     st = [json.loads(x.split("stats ", 1)[1]) for x in err.splitlines() if "[mi355x] stats" in x]
     return {"key": key, "tok_s": value, "ms_per_step": ms, "samples": res["tg_samples"], "avg_ts": res["tg_tok_s"],
-            "wall_s_incl_load": round(wall, 2), "executor": st[0] if st else None}
+            "tool": bench_tool(), "test": res.get("tg_test"), "wall_s_incl_load": round(wall, 2), "executor": st[0] if st else None}
 
 
 def dropin_bench(args, skip=()):
@@ -257,9 +294,9 @@ def dropin_bench(args, skip=()):
     and with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv), pp512 at each, pp2048
     (-b 2048 -ub 512, BASELINE configs[2]), tg128 at depth (-d: llama-bench.cpp:2191-2226,
     the KV cache filled with D tokens first)."""
-    if not os.path.exists(REF_BENCH) or args.no_dropin:
+    if not (os.path.exists(REF_BENCH) or os.path.exists(LLAMA_BENCH)) or args.no_dropin:
         return None
-    out = {"how": "reference libllama (oracle/_ref/ref-llama-bench) + GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, "
+    out = {"how": f"the reference's {bench_tool()} (oracle/_ref) + GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, "
                   f"-r {args.dropin_reps}, llama-bench warmup"}
     try:
         gguf = bench_gguf()
@@ -298,7 +335,7 @@ def dropin_layer_split(args, world, tg_leg=True):
     per device, boundary activations by cpy_tensor_async (hipMemcpyPeerAsync over xGMI),
     pipeline parallelism on (src/llama-context.cpp:307-334). The timed tg128 (-r K after
     W untimed repetitions) is the N > 1 headline; pp512 at -fa 1 beside it."""
-    if not os.path.exists(REF_BENCH) or args.no_dropin:
+    if not (os.path.exists(REF_BENCH) or os.path.exists(LLAMA_BENCH)) or args.no_dropin:
         return None
     vis = os.environ.get("HIP_VISIBLE_DEVICES")
     devs = vis.split(",")[:world] if vis else [str(i) for i in range(world)]
@@ -308,10 +345,13 @@ def dropin_layer_split(args, world, tg_leg=True):
         # every layer boundary on the peer-copy branch — the control flow of the real N-GPU run
         devs = [devs[0]]
         env.update(HIP_VISIBLE_DEVICES=devs[0], GGML_MI355X_VIRTUAL_DEVICES=str(world), GGML_MI355X_FORCE_PEER="1")
+    virtual = os.environ.get("MX_BENCH_VIRTUAL") == "1"
     ts = ",".join(["1"] * world)
     split = ["-fa", "1", "-sm", "layer", "-ts", ts]
     out = {"how": f"reference libllama -sm layer -ts {ts} over HIP devices {','.join(devs)}, -ngl 99, -fa 1",
            "devices": devs}
+    if virtual:   # a rehearsal must not pass for a multi-GPU number
+        out["virtual_devices"] = True
     try:
         if tg_leg:
             out["tg"] = dropin_tg(args, env, split + ["-c", 256], "tg128_split")
@@ -458,10 +498,14 @@ def split_headline(args, world, rank, local, dist, run_split=None):
     tg = (split or {}).get("tg")
     ok = isinstance(tg, dict)
     line = base_line(args, world, tg["tok_s"] if ok else None, tg["ms_per_step"] if ok else None, "strong",
-                     f"Llama-3-8B Q4_K_M tg{args.tg} decode (llama-bench test_gen) through the reference libllama, "
+                     f"Llama-3-8B Q4_K_M tg{args.tg} decode: the reference's {bench_tool()} on the reference libllama, "
                      f"layer split over {world} GPUs", f"libllama -sm layer -ts {','.join(['1'] * world)} "
                      "(cpy_tensor_async peer hand-off over xGMI), one sequence", "q4_k_m", "Llama-3-8B")
     line["dropin_layer_split"] = split
+    if os.environ.get("MX_BENCH_VIRTUAL") == "1":
+        line["virtual_devices"] = True
+        line["scaling_note"] = (f"rehearsal: {world} logical devices of ONE GPU (GGML_MI355X_VIRTUAL_DEVICES), "
+                                "not a multi-GPU measurement; keep out of any scaling curve")
     line["wall_s_all_legs"] = round(wall, 2)
     line["roofline"] = None
     line["cpu_baseline"] = None
@@ -513,7 +557,7 @@ def main():
         return
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    dropin_ok = os.path.exists(REF_BENCH) and not args.no_dropin and args.model == "llama3_8b" and not args.no_fa
+    dropin_ok = (os.path.exists(REF_BENCH) or os.path.exists(LLAMA_BENCH)) and not args.no_dropin and args.model == "llama3_8b" and not args.no_fa
     mode = args.mode
     if mode == "auto":
         mode = "dropin" if dropin_ok else ("pipeline" if world_env > 1 else "single")
@@ -643,8 +687,9 @@ def main():
                   "executor": stats, "pipelined": pipelined}
         if isinstance(head_dropin, dict):
             out = base_line(args, world, head_dropin["tok_s"], head_dropin["ms_per_step"], "weak",
-                            f"{label} {recipe.upper()} tg{args.tg} decode (llama-bench test_gen) through the reference "
-                            "libllama (GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, -fa 1)", "single", recipe, label)
+                            f"{label} {recipe.upper()} tg{args.tg} decode: the reference's {bench_tool()} (-o jsonl, its own "
+                            "defaults otherwise) on the reference libllama (GGML_BACKEND_PATH=libggml-mi355x.so, -ngl 99, -fa 1)",
+                            "single", recipe, label)
             out["headline"] = head_dropin
             hv = head_dropin["tok_s"]
         else:

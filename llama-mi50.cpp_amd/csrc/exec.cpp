@@ -439,6 +439,7 @@ static int fuse_attn_split_o(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     XStage xs{nullptr, nullptr, 0.0f, 0};
     xs.xcd = g_tune[15] != 1;
     xs.fap = part; xs.fap_ns = ns; xs.fap_d = (int) D;
+    c.s->gpf_armed = c.s->gpf_node && c.s->gpf_node == mm;   // the second prefetch stage rides on this GEMV
     gemv2_launch(c, wo, nullptr, xs, (float *) add->data, (const float *) res->data);
     return last - i + 1;
 }

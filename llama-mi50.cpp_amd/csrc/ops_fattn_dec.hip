@@ -648,7 +648,12 @@ void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit) {
     a.trace_blk = mx_trace_blocks();
     const unsigned gx = (unsigned) a.H;                          // G = 1: one query head per workgroup
     unsigned pf_rows = 0;
-    a.pf_n = c.s->pf_n;
+    // the gate/up weight prefetch rows (exec.cpp fa_prefetch_plan) only on request
+    // (GGML_MI355X_FA_PREFETCH_MB or g_tune[23] > 0): this launch is short enough that the
+    // default 16 MB outlasts it — same box, drop-in tg128 630 (16 MB) / 640 (8) / 644 tok/s
+    // without (profiles/r05/fa_split_prefetch_ab.txt)
+    static const bool pf_env = getenv("GGML_MI355X_FA_PREFETCH_MB") != nullptr;
+    a.pf_n = pf_env || g_tune[23] > 0 ? c.s->pf_n : 0;
     for (int r = 0; r < a.pf_n; ++r) {
         a.pf[r] = c.s->pf_ptr[r]; a.pf_eighth[r] = c.s->pf_len[r] / 8; a.pf_lines[r] = (unsigned) (c.s->pf_take[r] / 128);
     }
