@@ -237,6 +237,11 @@ def ref_bench(gguf, env, flags, timeout=900):
             if flags[i] == "-c":
                 i += 2
                 continue
+            if flags[i] == "-ctk":   # the restatement takes a ggml_type id, llama-bench a name for K and V
+                name = {"8": "q8_0", "2": "q4_0", "1": "f16", "30": "bf16"}.get(flags[i + 1], flags[i + 1])
+                fl += ["-ctk", name, "-ctv", name]
+                i += 2
+                continue
             fl.append(flags[i])
             i += 1
         r = subprocess.run([LLAMA_BENCH, "-m", gguf, "-o", "jsonl"] + fl, capture_output=True, text=True,
@@ -281,6 +286,7 @@ def dropin_tg(args, env, flags, key):
         return res
     value, ms = tg_from_samples(res["tg_samples"], args.tg)
     st = [json.loads(x.split("stats ", 1)[1]) for x in err.splitlines() if "[mi355x] stats" in x]
+    st.sort(key=lambda e: -e.get("graph_compute", 0))   # the decode context's backend (llama-bench frees several)
     return {"key": key, "tok_s": value, "ms_per_step": ms, "samples": res["tg_samples"], "avg_ts": res["tg_tok_s"],
             "tool": bench_tool(), "test": res.get("tg_test"), "wall_s_incl_load": round(wall, 2), "executor": st[0] if st else None}
 
@@ -362,6 +368,51 @@ def dropin_layer_split(args, world, tg_leg=True):
             out["pp512"] = res
         else:
             out["pp512_tok_s"], out["pp512_samples"] = res["pp_tok_s"], res["pp_samples"]
+    except Exception as e:  # noqa: BLE001
+        out["error"] = str(e)
+    return out
+
+
+def plan_decode_bytes(shape, recipe):
+    """HBM bytes one decoded token streams for a synthetic GGUF (tools/gguf_synth.py's own
+    tensor plan): every weight once, the experts' tensors (*_exps) by n_expert_used /
+    n_expert, token_embd one row (a GET_ROWS)"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gguf_synth as gs
+    s = gs.SHAPES[shape]
+    used = s.get("n_expert_used", 1) / s.get("n_expert", 1) if s.get("n_expert") else 1.0
+    tot = 0
+    for name, tname, ne in gs.tensor_plan(s, recipe):
+        b = gs.nbytes(tname, ne)
+        if name.startswith("token_embd"):
+            b = gs.nbytes(tname, [ne[0], 1])
+        elif "_exps" in name:
+            b = b * used
+        tot += b
+    return int(tot)
+
+
+def moe_leg(args):
+    """BASELINE configs[4]: Mixtral-8x7B Q5_K_M (MUL_MAT_ID, 8-expert recipe: k/v Q8_0) + flash
+    attention, through the reference's llama-bench like the headline: tg128 and pp512 at -fa 1,
+    with its own decode roofline (the experts streamed by 2 of 8)"""
+    if not (os.path.exists(REF_BENCH) or os.path.exists(LLAMA_BENCH)):
+        return None
+    out = {"how": f"the reference's {bench_tool()} + GGML_BACKEND_PATH=libggml-mi355x.so, Mixtral-8x7B Q5_K_M synthetic GGUF, "
+                  f"-ngl 99 -fa 1 -r {args.dropin_reps}"}
+    try:
+        gguf = bench_gguf("mixtral_8x7b", "q5_k_m")
+        env = dict(os.environ, GGML_BACKEND_PATH=LIB, GGML_MI355X_STATS="1")
+        res, _ = ref_bench(gguf, env, ["-t", "8", "-ngl", "99", "-fa", "1", "-p", args.pp, "-n", args.tg,
+                                       "-r", args.dropin_reps], timeout=1500)
+        if isinstance(res, str):
+            out["error"] = res
+            return out
+        bpt = plan_decode_bytes("mixtral_8x7b", "q5_k_m")
+        out.update({"tg128_tok_s": res["tg_tok_s"], "tg128_samples": res["tg_samples"], "pp512_tok_s": res["pp_tok_s"],
+                    "pp512_samples": res["pp_samples"], "decode_bytes_per_token": bpt,
+                    "decode_roofline": {"achieved_GBs": round(bpt * res["tg_tok_s"] / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
+                                        "frac": round(bpt * res["tg_tok_s"] / 1e9 / HBM_PEAK_GBS, 4)}})
     except Exception as e:  # noqa: BLE001
         out["error"] = str(e)
     return out
@@ -537,6 +588,9 @@ def main():
     ap.add_argument("--cpu-tg", type=int, default=128)
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--skip-roofline", action="store_true")
+    ap.add_argument("--moe-leg", action="store_true", help="add the Mixtral-8x7B Q5_K_M drop-in leg (BASELINE configs[4]; "
+                    "writes a 32 GB GGUF)")
+    ap.add_argument("--moe-only", action="store_true", help="run only the Mixtral drop-in leg and print it")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing (for scripts/pmc_roofline.sh's rocprofv3 --pmc passes)")
     ap.add_argument("--tune", nargs="*", default=[], help="backend tuning knobs IDX=VAL (A/B experiments)")
@@ -547,6 +601,9 @@ def main():
         for t in args.tune:
             k, v = (int(x) for x in t.split("="))
             lib.ggml_backend_mi355x_set_tune(k, v)
+    if args.moe_only:
+        print(json.dumps({"moe": moe_leg(args)}), flush=True)
+        return
     if args.roofline_only:
         from mi355x_pkg import load_package
         pkg = load_package()
@@ -674,6 +731,7 @@ def main():
         head_dropin = dropin_tg(args, env, ["-fa", 1, "-c", 256], "tg128_fa1")
     dropin = dropin_bench(args, skip=("tg128_fa1",) if mode == "dropin" else ()) \
         if (rank == 0 and world == 1 and args.model == "llama3_8b") else None
+    moe = moe_leg(args) if (rank == 0 and world == 1 and args.moe_leg) else None
     barrier(dist, local)
 
     if rank == 0:
@@ -700,6 +758,8 @@ def main():
             if head_dropin is not None:
                 out["headline_dropin_error"] = head_dropin
             hv = tg_value
+        if moe is not None:
+            out["moe"] = moe
         pp_ref = (dropin or {}).get("pp512_fa1_tok_s") if isinstance(head_dropin, dict) else pp_tok_s
         out.update({
             "pp512_tok_s": round(pp_ref, 1) if pp_ref else None,

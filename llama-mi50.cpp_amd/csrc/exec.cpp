@@ -833,7 +833,28 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         s->split_graph = false;
         return;
     }
-    if (!graphs || !seen || gc.key.empty()) { run_nodes(s, g); s->split_graph = false; return; }   // first sighting: eager
+    if (!graphs || gc.key.empty()) { run_nodes(s, g); s->split_graph = false; return; }
+    if (!seen) {
+        // first sighting: eager. Round 5: the capture is recorded and instantiated right
+        // behind the eager launches (the GPU is still executing them, so the host's capture
+        // time is mostly hidden), and the SECOND sighting already replays. Capturing only at
+        // the second sighting made it pay capture + instantiate with the GPU idle: llama-bench's
+        // first timed pp512 repetition ran 33.0k against 35.3-35.8k tok/s for the later ones
+        // (its warmup run is the first sighting; profiles/r05/trace_pp512_gaps.txt).
+        // GGML_MI355X_CAPTURE_SECOND=1 restores the round-4 order (A/B).
+        static const bool second = getenv("GGML_MI355X_CAPTURE_SECOND") != nullptr;
+        run_nodes(s, g);
+        if (second) { s->split_graph = false; return; }
+        HIP_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+        run_nodes(s, g);
+        s->split_graph = false;
+        hipGraph_t graph = nullptr;
+        HIP_CHECK(hipStreamEndCapture(s->stream, &graph));
+        HIP_CHECK(hipGraphInstantiate(&gc.exec, graph, nullptr, nullptr, 0));
+        gc.graph = graph;
+        gc.buf_gen = g_buf_gen.load();
+        return;
+    }
     // second sighting of the same signature: capture and launch. (Recording it on a side
     // stream behind an eager run instead measured no better for the prompt and slower for the
     // first decode repetition: profiles/r04/graph_slots_ab.txt)

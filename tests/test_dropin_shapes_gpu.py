@@ -298,15 +298,53 @@ def test_llama3_8b_width_pp2048(l8b, tmp_path):
         [ln for ln in klog if ln.startswith("fa_mma2")]
 
 
-def dump_run(tmp_path, gguf, toks, ngl, tag, incremental=False):
+def dump_run(tmp_path, gguf, toks, ngl, tag, incremental=False, last=8, with_logits=False):
     d = tmp_path / f"dump_{ngl}{tag}"
     d.mkdir()
-    run_ref(tmp_path, gguf, toks, ngl, 1, incremental=incremental, last=8,
-            extra=["--dump", str(d / "nodes.txt"), "--dump-dir", str(d)], tag=f"d{ngl}{tag}")
+    logits, _, _ = run_ref(tmp_path, gguf, toks, ngl, 1, incremental=incremental, last=last,
+                           extra=["--dump", str(d / "nodes.txt"), "--dump-dir", str(d)], tag=f"d{ngl}{tag}")
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import dump_compare
-    return [(n, op, ne, np.fromfile(d / f"{i:03d}.f32", np.float32))
-            for i, (n, op, ne) in enumerate(dump_compare.names(str(d / "nodes.txt")))]
+    nodes = [(n, op, ne, np.fromfile(d / f"{i:03d}.f32", np.float32))
+             for i, (n, op, ne) in enumerate(dump_compare.names(str(d / "nodes.txt")))]
+    return (nodes, logits) if with_logits else nodes
+
+
+def moe_flip_tokens(cpu, gpu, n_used=2):
+    """{layer: tokens} whose MUL_MAT_ID rows ran a different expert on the two backends
+    (row NMSE >= 0.5: an unrelated expert's output; rows between 1e-2 and 0.5 are a bug, not
+    a flip). A decode dump holds one token per node (the token index is then the dump's)."""
+    flips = {}
+    for (n, op, ne, a), (n2, _, _, b) in zip(cpu, gpu):
+        assert n == n2
+        if op != "MUL_MAT_ID":
+            continue
+        try:
+            layer = int(n.rsplit("-", 1)[1])
+        except (IndexError, ValueError):
+            continue
+        A = a.astype(np.float64).reshape(-1, ne[0]); B = b.astype(np.float64).reshape(-1, ne[0])
+        r = np.sum((A - B) ** 2, 1) / np.maximum(np.sum(A ** 2, 1), 1e-30)
+        assert not ((r > 1e-2) & (r < 0.5)).any(), (n, np.sort(r)[-10:])
+        flips.setdefault(layer, set()).update(int(i) // n_used for i in np.nonzero(r >= 0.5)[0])
+    return flips
+
+
+def per_position_moe(cpu_logits, gpu_logits, flips, positions):
+    """Round 5: every logits position that no routing flip can reach must be
+    within MOE_TOL — a layer-0 flip at token t reaches every position >= t (layer 1's causal
+    attention reads token t), a layer-1 flip only its own position. Returns (clean, reached)
+    NMSE lists; the reached positions are bounded loosely (a different expert somewhere
+    upstream, not garbage)."""
+    t0 = min(flips.get(0, set()) | {10 ** 9})
+    clean, reached = [], []
+    for i, p in enumerate(positions):
+        e = nmse(gpu_logits[i], cpu_logits[i])
+        (reached if p >= t0 or p in flips.get(1, set()) else clean).append(e)
+    assert clean, (flips, positions)
+    assert max(clean) < MOE_TOL, (clean, flips)
+    assert not reached or max(reached) < 0.1, (reached, flips)
+    return clean, reached
 
 
 def check_moe_layer0(cpu, gpu):
@@ -336,25 +374,45 @@ def test_mixtral_width_moe(mixtral, tmp_path):
     quantisation noise of the q8/f16 GEMMs (NMSE ~1e-4 against the CPU's q8_K arithmetic),
     so top-2 selection flips wherever two experts' probabilities nearly tie; those tokens
     then legitimately run different experts, and a flipped token in layer 0 perturbs every
-    later token through layer 1's attention. Checked: layer-0 expert rows match per
-    (token, slot) unless a flip happened, flips are rare (~5 % of rows measured), and the
-    median position's logits are within MOE_TOL (the dense 8B graph holds TOL)."""
+    later token through layer 1's attention. Checked: expert rows match per (token, slot) in
+    every layer unless a flip happened, layer-0 flips are rare (~5 % of rows measured), and
+    (round 5) EVERY logits position no flip can reach is within MOE_TOL, the reached ones
+    within 0.1 — prefill (all 64 positions) and incremental decode (12 steps)."""
     toks = np.random.default_rng(25).integers(0, 32000, 64)
-    f, r = check_moe_layer0(dump_run(tmp_path, mixtral, toks, 0, "p"), dump_run(tmp_path, mixtral, toks, 99, "p"))
+    n = len(toks)
+    dc, lc = dump_run(tmp_path, mixtral, toks, 0, "p", last=n, with_logits=True)
+    dg, lg = dump_run(tmp_path, mixtral, toks, 99, "p", last=n, with_logits=True)
+    f, r = check_moe_layer0(dc, dg)
     print(f"prefill: {f} of {r} layer-0 expert rows flipped")
+    flips = moe_flip_tokens(dc, dg)
+    clean, reached = per_position_moe(lc, lg, flips, list(range(n)))
+    print(f"prefill: {len(clean)} positions no flip reaches (max NMSE {max(clean):.2e}), {len(reached)} reached "
+          f"(max {max(reached or [0]):.2e}); flips {flips}")
+    # the ordinary (fused, non-callback) run: the kernels the dumps' node-by-node run cannot fuse
     cpu, _, _ = run_ref(tmp_path, mixtral, toks, 0, 1, last=8)
     gpu, log, klog = run_ref(tmp_path, mixtral, toks, 99, 1, last=8)
-    per = [nmse(g, c) for g, c in zip(gpu, cpu)]
-    assert np.median(per) < MOE_TOL, per
+    assert max(nmse(g, c) for g, c in zip(gpu, cpu)) < 0.1
     assert any(ln.startswith(("moe_", "mmid", "mmq4 moe", "gemv2 moe")) for ln in klog), klog[:40]
     t2 = toks[:12]
-    f, r = check_moe_layer0(dump_run(tmp_path, mixtral, t2, 0, "i", True), dump_run(tmp_path, mixtral, t2, 99, "i", True))
+    dci, lci = dump_run(tmp_path, mixtral, t2, 0, "i", True, last=len(t2), with_logits=True)
+    dgi, lgi = dump_run(tmp_path, mixtral, t2, 99, "i", True, last=len(t2), with_logits=True)
+    assert len(lci) == len(t2) and len(dci) % len(t2) == 0 and len(dci) == len(dgi), (len(lci), len(dci), len(dgi))
+    f, r = check_moe_layer0(dci, dgi)
     print(f"decode: {f} of {r} layer-0 expert rows flipped")
+    # incremental: one dump per decoded token, in order — node k of token t is dump entry t * per + k
+    per = len(dci) // len(t2)
+    fl = {}
+    for t in range(len(t2)):
+        ft = moe_flip_tokens(dci[t * per:(t + 1) * per], dgi[t * per:(t + 1) * per])
+        for layer, s_ in ft.items():
+            if s_:
+                fl.setdefault(layer, set()).add(t)
+    clean, reached = per_position_moe(lci, lgi, fl, list(range(len(t2))))
+    print(f"decode: {len(clean)} clean positions (max NMSE {max(clean):.2e}), {len(reached)} reached; flips {fl}")
     cpu_i, _, _ = run_ref(tmp_path, mixtral, t2, 0, 1, incremental=True, tag="i")
     gpu_i, _, klog_i = run_ref(tmp_path, mixtral, t2, 99, 1, incremental=True, tag="i",
                                env_extra={"GGML_MI355X_DISABLE_GRAPHS": "1"})
-    per = [nmse(g, c) for g, c in zip(gpu_i, cpu_i)]
-    assert np.median(per) < MOE_TOL, per
+    assert max(nmse(g, c) for g, c in zip(gpu_i, cpu_i)) < 0.1
     qkv = [ln for ln in klog_i if ln.startswith("qkv ")]
     assert len(qkv) == 2 * len(t2) and all("qta=13 qtk=8 qtv=8" in ln for ln in qkv), (qkv[:4], klog_i[:20])
 
