@@ -371,6 +371,7 @@ static int try_fuse_mm_rows_add(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses
 int fa_dec2_partials_nsplit(const ggml_tensor * fa);           // ops_fattn_dec.hip
 void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit);
 static const bool g_no_fa_split_o = getenv("GGML_MI355X_NO_FA_SPLIT_O") != nullptr;   // A/B
+int fuse_moe_router(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);   // ops_moe.hip
 static const bool g_fa_dec1_env = getenv("GGML_MI355X_FA_DEC1") != nullptr;
 static int fuse_attn_split_o(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     // g_tune[32] = 1 (or GGML_MI355X_NO_FA_SPLIT_O): the round-4 path (one-split attention, O from x)
@@ -652,6 +653,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
             }
         } else if (s->use_fusion) {
             const int i0 = i;
+            if (n->op == GGML_OP_RMS_NORM && !g_no_moe_fusion) {   // the MoE block's norm + router + top-k (ops_moe.hip)
+                const int k = fuse_moe_router(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; deferred_retire(s, g, i0, i); continue; }
+            }
             if (n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }
             if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
             if (n->op == GGML_OP_MUL_MAT && !g_no_qkv) {

@@ -140,6 +140,8 @@ void op_mul_mat_id(OpCtx & c, ggml_tensor * dst) {
 
 namespace mx {
 
+extern int g_tune[48];
+
 // ---------------------------------------------------------------------------
 // MoE router in one launch (reference fusion: ggml-cuda/topk-moe.cu): the node chain
 // SOFT_MAX(logits) -> ARGSORT(desc) [-> top-k view] -> GET_ROWS(probs, top-k)
@@ -158,10 +160,10 @@ struct TopkArgs {
     int n_exp, k;
 };
 
-__global__ __launch_bounds__(64) void k_topk_moe(TopkArgs a) {
-    const int lane = threadIdx.x, t = blockIdx.x;
+// one wave; lane e holds expert e's logit (before the soft_max scale) in `lg`
+__device__ __forceinline__ void topk_chain(const TopkArgs & a, int t, int lane, float lg) {
     const bool on = lane < a.n_exp;
-    const float x = on ? a.logits[(size_t) t * a.l1 + lane] * a.scale : -INFINITY;
+    const float x = on ? lg * a.scale : -INFINITY;
     const float m = wave_max(x);
     const float e = on ? expf(x - m) : 0.0f;
     const float s = wave_sum(e);
@@ -194,6 +196,11 @@ __global__ __launch_bounds__(64) void k_topk_moe(TopkArgs a) {
     }
 }
 
+__global__ __launch_bounds__(64) void k_topk_moe(TopkArgs a) {
+    const int lane = threadIdx.x, t = blockIdx.x;
+    topk_chain(a, t, lane, lane < a.n_exp ? a.logits[(size_t) t * a.l1 + lane] : 0.f);
+}
+
 // A fused chain runs its nodes at once, one workgroup per token (per row tile): a thread's
 // outputs must not land on data another thread still reads or writes. ggml-alloc gives
 // dead tensors' memory to later nodes and runs SOFT_MAX / DIV / CLAMP / ADD / MUL in
@@ -224,8 +231,9 @@ static const ggml_tensor * view_base(const ggml_tensor * t) {
     return t;
 }
 
-// returns the number of graph nodes consumed from i (0: no match)
-int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i) {
+// The SOFT_MAX -> ARGSORT -> GET_ROWS [-> SUM_ROWS -> CLAMP -> DIV] chain starting at node i:
+// its arguments in *out and the index of its last node (0: no match)
+static int match_topk_moe(ggml_cgraph * g, int i, TopkArgs * out) {
     ggml_tensor * sm = g->nodes[i];
     if (sm->op != GGML_OP_SOFT_MAX || sm->src[1] || sm->type != GGML_TYPE_F32 || sm->src[0]->type != GGML_TYPE_F32) return 0;
     if (mx_op_param<float>(sm, 1) != 0.0f || sm->ne[0] > 64 || sm->ne[2] != 1 || sm->ne[3] != 1) return 0;
@@ -266,7 +274,8 @@ int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i) {
     const ChainReg regs[] = {chain_reg(sm->src[0], 1), chain_reg(sm, 1), chain_reg(as, 1), chain_reg(gr, 2),
                              chain_reg(sr, 1), chain_reg(cl, 1), chain_reg(dv, 1)};
     if (n_tok > 1 && !chain_alias_ok(regs, 7, false)) return 0;
-    TopkArgs a{};
+    TopkArgs & a = *out;
+    a = TopkArgs{};
     a.logits = (const float *) sm->src[0]->data; a.l1 = sm->src[0]->nb[1] / 4;
     a.probs = (float *) sm->data; a.p1 = sm->nb[1] / 4;
     a.order = (int32_t *) as->data; a.o1 = as->nb[1] / 4;
@@ -278,12 +287,183 @@ int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i) {
         a.cmin = mx_op_param<float>(cl, 0); a.cmax = mx_op_param<float>(cl, 1);
         a.wn = (float *) dv->data; a.wn1 = (size_t) k;
     }
+    return last;
+}
+
+// returns the number of graph nodes consumed from i (0: no match)
+int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i) {
+    TopkArgs a;
+    const int last = match_topk_moe(g, i, &a);
+    if (!last) return 0;
+    const int n_tok = (int) g->nodes[i]->ne[1];
     for (int j = i; j <= last; ++j) {
         deferred_guard_node_ext(c, g->nodes[j]);
         act_cache_invalidate(c.s, g->nodes[j]);
     }
-    MX_KLOG("topk_moe n_exp=%d k=%d n_tok=%d norm=%d", n_exp, k, n_tok, dv != nullptr);
+    MX_KLOG("topk_moe n_exp=%d k=%d n_tok=%d norm=%d", a.n_exp, a.k, n_tok, a.wn != nullptr);
     k_topk_moe<<<(unsigned) n_tok, 64, 0, c.st>>>(a);
+    return last - i + 1;
+}
+
+// ---------------------------------------------------------------------------
+// Round 5: the MoE block's head in ONE launch for a decoded token — ffn_norm (RMS_NORM ->
+// MUL(w), the f32 output and its q8 copy for the expert GEMVs, k_rms_norm_q8's
+// arithmetic), the router MUL_MAT(gate_inp [K, n_exp] f32/f16, cur) and the top-k chain
+// above (build_moe_ffn, src/llama-graph.cpp:1183-1296). The Mixtral decode profile
+// (profiles/r05/) ran them as three ~5 us launches per layer (rms_norm_q8 4.8-5.1,
+// mmv_dense 4.8, topk_moe 4.6: 470 us of a 3,078 us token). One 512-thread workgroup:
+// the router rows are loaded first (wave e % 8 takes expert e, K/64 floats per lane) and
+// stay in flight while the norm runs; cur goes through LDS to the router dots.
+// ---------------------------------------------------------------------------
+struct RouterArgs {
+    const float * x; const float * nw; float eps; int K;
+    float * cur; int8_t * q; float * qd; float * qs;          // MUL output, its q8 copy (act cache)
+    const char * wr; size_t wr1; int wf16;                       // router weights, row (expert) stride in bytes
+    float * logits;                                               // MUL_MAT output [n_exp]
+    TopkArgs tk;
+};
+
+template <int KMAX>
+__global__ __launch_bounds__(512) void k_moe_router(RouterArgs p) {
+    __shared__ float xs[KMAX];
+    __shared__ float red[16];
+    __shared__ float lg[64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = p.K, nch = K / 32;
+    // 1) the norm: thread b owns 32-chunk b (K <= 32 x 512)
+    float xr[32], wr_[32];
+    float ss = 0.f;
+    if (tid < nch) {
+#pragma unroll
+        for (int j = 0; j < 32; j += 4) {
+            const float4 a = *(const float4 *) (p.x + 32 * tid + j), b = *(const float4 *) (p.nw + 32 * tid + j);
+            xr[j] = a.x; xr[j + 1] = a.y; xr[j + 2] = a.z; xr[j + 3] = a.w;
+            wr_[j] = b.x; wr_[j + 1] = b.y; wr_[j + 2] = b.z; wr_[j + 3] = b.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) ss += xr[j] * xr[j];
+    }
+    ss = block_sum(ss, red);
+    const float scale = 1.0f / sqrtf(ss / (float) K + p.eps);
+    if (tid < nch) {
+        float v[32];
+#pragma unroll
+        for (int j = 0; j < 32; j += 4) {
+            v[j] = (xr[j] * scale) * wr_[j]; v[j + 1] = (xr[j + 1] * scale) * wr_[j + 1];
+            v[j + 2] = (xr[j + 2] * scale) * wr_[j + 2]; v[j + 3] = (xr[j + 3] * scale) * wr_[j + 3];
+            *(float4 *) (p.cur + 32 * tid + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+            *(float4 *) (xs + 32 * tid + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+        const Q8Scale qsc = q8_scale(amax);
+        int sum = 0, packed[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            int wq = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int qi = q8_round(v[4 * j + k], qsc.id);
+                sum += qi;
+                wq |= (qi & 0xFF) << (8 * k);
+            }
+            packed[j] = wq;
+        }
+        int4 * o = (int4 *) (p.q + 32 * tid);
+        o[0] = make_int4(packed[0], packed[1], packed[2], packed[3]);
+        o[1] = make_int4(packed[4], packed[5], packed[6], packed[7]);
+        p.qd[tid] = qsc.d;
+        p.qs[tid] = qsc.d * (float) sum;
+    }
+    __syncthreads();
+    // 2) router dots: wave w takes experts w, w + 8, ...; f32 accumulation in K order per lane
+    for (int e = wave; e < p.tk.n_exp; e += 8) {
+        const char * row = p.wr + (size_t) e * p.wr1;
+        float acc = 0.f;
+        for (int k = 4 * lane; k < K; k += 256) {
+            float4 w4;
+            if (p.wf16) {
+                const uint2 h = *(const uint2 *) (row + 2 * (size_t) k);
+                w4 = make_float4(h2f((uint16_t) (h.x & 0xFFFF)), h2f((uint16_t) (h.x >> 16)), h2f((uint16_t) (h.y & 0xFFFF)),
+                                 h2f((uint16_t) (h.y >> 16)));
+            } else {
+                w4 = *(const float4 *) (row + 4 * (size_t) k);
+            }
+            const float4 c4 = *(const float4 *) (xs + k);
+            acc += w4.x * c4.x + w4.y * c4.y + w4.z * c4.z + w4.w * c4.w;
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) { lg[e] = acc; p.logits[e] = acc; }
+    }
+    __syncthreads();
+    // 3) soft_max -> top-k -> weights (k_topk_moe's arithmetic), one wave
+    if (wave == 0) topk_chain(p.tk, 0, lane, lane < p.tk.n_exp ? lg[lane] : 0.f);
+}
+
+// RMS_NORM at node i -> MUL(w) -> MUL_MAT(gate_inp, cur) -> the top-k chain, one token.
+// Returns the nodes consumed (0: no match).
+int fuse_moe_router(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map) {
+    static const bool off = getenv("GGML_MI355X_NO_MOE_ROUTER_FUSION") != nullptr;   // A/B
+    if (off || g_tune[34] == 1 || i + 3 >= g->n_nodes) return 0;
+    ggml_tensor * norm = g->nodes[i], * mul = g->nodes[i + 1];
+    if (norm->op != GGML_OP_RMS_NORM || mul->op != GGML_OP_MUL || norm->type != GGML_TYPE_F32 || mul->type != GGML_TYPE_F32) return 0;
+    const ggml_tensor * x = norm->src[0];
+    const ggml_tensor * w = mul->src[0] == norm ? mul->src[1] : (mul->src[1] == norm ? mul->src[0] : nullptr);
+    const int64_t K = x->ne[0];
+    if (!w || mx_nrows(x) != 1 || K % 32 || K > 8192 || !mx_is_contiguous(x) || !mx_are_same_shape(mul, norm)) return 0;
+    if (w->type != GGML_TYPE_F32 || mx_nelements(w) != K || !mx_is_contiguous(w) || !mx_is_contiguous(mul)) return 0;
+    if (((uintptr_t) x->data | (uintptr_t) w->data | (uintptr_t) mul->data) & 15) return 0;
+    auto uses = [&](const ggml_tensor * t) { auto it = use_map.find(t); return it == use_map.end() ? 0 : it->second; };
+    if (uses(norm) != 1 || (norm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    // the router MUL_MAT, then the soft_max chain right after it
+    int jm = i + 2;
+    while (jm < g->n_nodes && (g->nodes[jm]->op == GGML_OP_RESHAPE || g->nodes[jm]->op == GGML_OP_VIEW)) ++jm;
+    if (jm + 1 >= g->n_nodes) return 0;
+    ggml_tensor * mm = g->nodes[jm];
+    if (mm->op != GGML_OP_MUL_MAT || mm->src[1] != mul || mm->type != GGML_TYPE_F32 || !mx_is_contiguous(mm)) return 0;
+    const ggml_tensor * gi = mm->src[0];
+    const int n_exp = (int) gi->ne[1];
+    if ((gi->type != GGML_TYPE_F32 && gi->type != GGML_TYPE_F16) || gi->ne[0] != K || gi->ne[2] != 1 || gi->ne[3] != 1 ||
+        gi->nb[0] != (size_t) mx_type(gi->type).size || gi->nb[1] % 16 || (uintptr_t) gi->data % 16 || n_exp > 64) return 0;
+    if (mm->ne[0] != n_exp || mm->ne[1] != 1) return 0;
+    int js = jm + 1;
+    while (js < g->n_nodes && (g->nodes[js]->op == GGML_OP_RESHAPE || g->nodes[js]->op == GGML_OP_VIEW)) ++js;
+    if (js >= g->n_nodes || g->nodes[js]->op != GGML_OP_SOFT_MAX || g->nodes[js]->src[0] != mm) return 0;
+    TopkArgs tk;
+    const int last = match_topk_moe(g, js, &tk);
+    if (!last || tk.n_exp != n_exp) return 0;
+    for (int j = i + 2; j < js; ++j) if (g->nodes[j] != mm && g->nodes[j]->op != GGML_OP_RESHAPE && g->nodes[j]->op != GGML_OP_VIEW) return 0;
+    // written before the top-k chain reads anything: cur and logits must not overlap what
+    // the launch reads (x, w, the router rows) or each other; the chain's own outputs are
+    // one wave's, written after every read (fuse_topk_moe)
+    for (const ggml_tensor * o : {(const ggml_tensor *) mul, (const ggml_tensor *) mm})
+        for (const ggml_tensor * in : {x, w, gi})
+            if (t_overlaps_ext(o, in)) return 0;
+    if (t_overlaps_ext(mul, mm)) return 0;
+    for (const void * tkout : {(const void *) tk.probs, (const void *) tk.order, (const void *) tk.w, (const void *) tk.sum,
+                               (const void *) tk.clamped, (const void *) tk.wn}) {
+        // the chain's outputs may lie over the logits (in place) but not over cur or the inputs
+        if (!tkout) continue;
+        const char * p0 = (const char *) tkout;
+        for (const ggml_tensor * t : {(const ggml_tensor *) mul, x, w, gi})
+            if (p0 >= (const char *) t->data && p0 < (const char *) t->data + mx_nbytes(t)) return 0;
+    }
+    for (int j = i; j <= last; ++j) {
+        deferred_guard_node_ext(c, g->nodes[j]);
+        act_cache_invalidate(c.s, g->nodes[j]);
+    }
+    ActQ * a = act_cache_alloc(c.s, mul);
+    if (!a) return 0;
+    RouterArgs r{};
+    r.x = (const float *) x->data; r.nw = (const float *) w->data; r.eps = mx_op_param<float>(norm, 0); r.K = (int) K;
+    r.cur = (float *) mul->data; r.q = (int8_t *) a->q; r.qd = (float *) a->d; r.qs = (float *) a->s;
+    r.wr = (const char *) gi->data; r.wr1 = gi->nb[1]; r.wf16 = gi->type == GGML_TYPE_F16;
+    r.logits = (float *) mm->data;
+    r.tk = tk;
+    MX_KLOG("moe_router K=%d n_exp=%d k=%d norm=%d wf16=%d", (int) K, n_exp, tk.k, tk.wn != nullptr, r.wf16);
+    if (K <= 4096) k_moe_router<4096><<<1, 512, 0, c.st>>>(r);
+    else k_moe_router<8192><<<1, 512, 0, c.st>>>(r);
     return last - i + 1;
 }
 

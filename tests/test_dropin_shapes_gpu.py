@@ -312,9 +312,10 @@ def dump_run(tmp_path, gguf, toks, ngl, tag, incremental=False, last=8, with_log
 
 def moe_flip_tokens(cpu, gpu, n_used=2):
     """{layer: tokens} whose MUL_MAT_ID rows ran a different expert on the two backends
-    (row NMSE >= 0.5: an unrelated expert's output; rows between 1e-2 and 0.5 are a bug, not
-    a flip). A decode dump holds one token per node (the token index is then the dump's)."""
-    flips = {}
+    (row NMSE >= 0.5: an unrelated expert's output). Rows between 1e-2 and 0.5 are a bug, not
+    a flip — except for tokens an earlier layer's flip already reached (at and after its
+    first flipped token: their inputs differ). A decode dump holds one token per node."""
+    rows = {}
     for (n, op, ne, a), (n2, _, _, b) in zip(cpu, gpu):
         assert n == n2
         if op != "MUL_MAT_ID":
@@ -324,9 +325,15 @@ def moe_flip_tokens(cpu, gpu, n_used=2):
         except (IndexError, ValueError):
             continue
         A = a.astype(np.float64).reshape(-1, ne[0]); B = b.astype(np.float64).reshape(-1, ne[0])
-        r = np.sum((A - B) ** 2, 1) / np.maximum(np.sum(A ** 2, 1), 1e-30)
-        assert not ((r > 1e-2) & (r < 0.5)).any(), (n, np.sort(r)[-10:])
-        flips.setdefault(layer, set()).update(int(i) // n_used for i in np.nonzero(r >= 0.5)[0])
+        rows.setdefault(layer, []).append((n, np.sum((A - B) ** 2, 1) / np.maximum(np.sum(A ** 2, 1), 1e-30)))
+    flips, t0 = {}, 10 ** 9
+    for layer in sorted(rows):
+        for n, r in rows[layer]:
+            tok = np.arange(len(r)) // n_used
+            live = tok < t0
+            assert not ((r > 1e-2) & (r < 0.5) & live).any(), (n, t0, np.sort(r[live])[-10:])
+            flips.setdefault(layer, set()).update(int(t) for t in tok[(r >= 0.5) & live])
+        t0 = min(flips.get(layer, set()) | {t0})
     return flips
 
 

@@ -751,3 +751,67 @@ def test_attn_split_oproj_decode(pkg, backend, orc, kind, n_kv, H, Hkv, M, wt, m
     assert nmse(y, ref_exact) < 5e-4, nmse(y, ref_exact)
     assert np.array_equal(y, y2)                  # deterministic (no atomics in either launch)
     assert nmse(y, y3) < 1e-5, nmse(y, y3)
+
+
+@pytest.mark.parametrize("n_exp,E,wtype,knorm", [(8, 4096, "f32", True), (8, 4096, "f16", True), (4, 256, "f32", False),
+                                                 (16, 1024, "f32", True), (8, 6144, "f32", True)])
+def test_moe_router_head_fusion(pkg, backend, orc, n_exp, E, wtype, knorm):
+    """Round 5: the MoE block's head of one decoded token — RMS_NORM -> MUL(ffn_norm) ->
+    MUL_MAT(router) -> SOFT_MAX -> ARGSORT -> top-k GET_ROWS [-> SUM_ROWS -> CLAMP -> DIV] —
+    as ONE k_moe_router launch (ops_moe.hip fuse_moe_router), every node's output checked
+    against numpy, and against the node-by-node launches (g_tune[34] = 1)"""
+    rng = np.random.default_rng(7 + n_exp + E)
+    k = 2
+    x = rng.standard_normal((1, E)).astype(np.float32)
+    nw = (1 + 0.1 * rng.standard_normal(E)).astype(np.float32)
+    wr = (rng.standard_normal((n_exp, E)) * 0.05).astype(np.float32)
+    wr_feed = wr.astype(np.float16).view(np.uint16) if wtype == "f16" else wr
+    wr_ref = wr.astype(np.float16).astype(np.float32) if wtype == "f16" else wr
+
+    def build(ctx):
+        tx = ctx.new_tensor("f32", E, 1)
+        tn = ctx.new_tensor("f32", E)
+        tw = ctx.new_tensor(wtype, E, n_exp)
+        cur = ctx.mul(ctx.rms_norm(tx, 1e-5), tn)
+        tl = ctx.mul_mat(tw, cur)
+        probs = ctx.soft_max_ext(tl, None, 1.0)
+        order = ctx.argsort(probs, desc=True)
+        nb1 = order.nb[1]
+        topk = ctx.view_4d(order, k, 1, 1, 1, nb1, nb1, nb1, 0)
+        w = ctx.get_rows(ctx.reshape(probs, 1, n_exp, 1), topk)
+        outs = [cur, tl, probs, order, w]
+        if knorm:
+            w2 = ctx.reshape(w, k, 1)
+            cl = ctx.clamp(ctx.sum_rows(w2), 6.103515625e-5, float("inf"))
+            outs.append(ctx.div(w2, cl))
+        return outs, [(tx, x), (tn, nw), (tw, wr_feed)]
+
+    lib = pkg._lib.load()
+    backend.klog(True)
+    res = run(pkg, backend, build)
+    log = backend.klog_read()
+    backend.klog(False)
+    lib.ggml_backend_mi355x_set_tune(34, 1)
+    try:
+        res_u = run(pkg, backend, build)
+    finally:
+        lib.ggml_backend_mi355x_set_tune(34, 0)
+    assert any(ln.startswith("moe_router ") for ln in log), log
+    cur_ref = orc.rms_norm(x, 1e-5) * nw
+    assert nmse(res[0].reshape(1, E), cur_ref) < 1e-7
+    lg_ref = (cur_ref.astype(np.float64) @ wr_ref.T.astype(np.float64))[0]
+    assert nmse(res[1].reshape(n_exp), lg_ref) < 1e-6
+    e = np.exp(lg_ref - lg_ref.max())
+    p_ref = e / e.sum()
+    assert nmse(res[2].reshape(n_exp), p_ref) < 1e-5
+    o_ref = np.argsort(-p_ref, kind="stable")
+    assert np.array_equal(res[3].reshape(n_exp)[:k], o_ref[:k])
+    w_ref = p_ref[o_ref[:k]]
+    assert nmse(res[4].reshape(k), w_ref) < 1e-6
+    if knorm:
+        assert nmse(res[5].reshape(k), w_ref / w_ref.sum()) < 1e-6
+    for a, b in zip(res, res_u):   # fused == node by node (ordering / selection identical)
+        if a.dtype == np.int32:
+            assert np.array_equal(a.reshape(-1)[:k], b.reshape(-1)[:k])
+        else:
+            assert nmse(a.reshape(-1), b.reshape(-1)) < 1e-9
