@@ -902,7 +902,8 @@ static void mmq_run_ex(OpCtx & c, ggml_tensor * dst, ggml_tensor * out, const gg
     p.r2 = x->ne[2] / w->ne[2]; p.r3 = x->ne[3] / w->ne[3];
     p.dbg = MX_AB_VARIANTS ? g_tune[13] : 0;
     const bool kq = w->type == GGML_TYPE_Q4_K || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
-    if (kq && !g_mmq_v1 && p.K % 256 == 0 && mmq4_mul_mat(c, w, x, xa, kp, out, res)) return;
+    // (round 5: Q8_0 too — k_mmq4's Q8_0 B operand; the k_mmq2/3 paths below are K-quant only)
+    if ((kq || w->type == GGML_TYPE_Q8_0) && !g_mmq_v1 && p.K % 256 == 0 && mmq4_mul_mat(c, w, x, xa, kp, out, res)) return;
     if (kq && !g_mmq_v1 && p.K % 256 == 0) {
         const int64_t tiles128 = mx_ceil_div(p.N, MM_BT) * mx_ceil_div(p.M, 128) * (x->ne[2] * x->ne[3]);
         int bm = tiles128 < 512 ? 64 : 128;
@@ -1078,7 +1079,8 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, 
     const ggml_tensor * wg = gate->src[0], * wu = up->src[0];
     const ggml_tensor * x = gate->src[1];
     if (g_mmq_glu_off || g_mmq_v1 || up->src[1] != x || wg->type != wu->type) return false;
-    if (wg->type != GGML_TYPE_Q4_K && wg->type != GGML_TYPE_Q5_K && wg->type != GGML_TYPE_Q6_K) return false;
+    if (wg->type != GGML_TYPE_Q4_K && wg->type != GGML_TYPE_Q5_K && wg->type != GGML_TYPE_Q6_K && wg->type != GGML_TYPE_Q8_0) return false;
+    if (wg->type == GGML_TYPE_Q8_0 && !mmq4_glu_ok(wg, wu, x, glu)) return false;   // k_mmq4 only (round 5)
     if (mx_op_param<int32_t>(glu, 0) != GGML_GLU_OP_SWIGLU || mx_op_param<int32_t>(glu, 1) != 0) return false;
     if (x->type != GGML_TYPE_F32 || x->ne[1] <= 8 || x->ne[2] != 1 || x->ne[3] != 1) return false;
     for (int i = 0; i < 4; ++i) if (wg->ne[i] != wu->ne[i] || wg->nb[i] != wu->nb[i]) return false;
@@ -1123,12 +1125,16 @@ bool mmq_group_run(OpCtx & c, ggml_tensor * const * mms, int n) {
     int tb = ta;
     for (int k = 0; k < n; ++k) {
         const ggml_tensor * m = mms[k], * w = m->src[0];
-        if (m->src[1] != x || !kq_type(w->type) || !mmq_ok(m)) return false;
+        if (m->src[1] != x || !(kq_type(w->type) || w->type == GGML_TYPE_Q8_0) || !mmq_ok(m)) return false;
         if (w->ne[0] != x->ne[0] || w->ne[0] % 256 || w->ne[2] != 1 || w->ne[3] != 1) return false;
         if (m->type != GGML_TYPE_F32 || m->nb[0] != 4 || m->ne[2] != 1 || m->ne[3] != 1) return false;
         if (w->type != ta) { if (tb != ta && tb != w->type) return false; tb = w->type; }
     }
     if (x->type != GGML_TYPE_F32 || x->ne[1] <= 8 || x->ne[2] != 1 || x->ne[3] != 1) return false;
+    if (ta == GGML_TYPE_Q8_0 || tb == GGML_TYPE_Q8_0) {   // round 5: k_mmq4 only (the 8-expert recipe's q8_0 k / v)
+        const int64_t kp8 = mmq_kp(mms[0]);
+        return mmq4_group(c, mms, n, mmq_act(c, x, kp8), kp8);
+    }
     const bool combo = (ta == GGML_TYPE_Q6_K || tb == GGML_TYPE_Q6_K || ta == tb) && !(ta == GGML_TYPE_Q5_K && tb == GGML_TYPE_Q4_K) &&
                        !(ta == GGML_TYPE_Q4_K && tb == GGML_TYPE_Q5_K);
     if (!combo || (ta == GGML_TYPE_Q6_K && tb == GGML_TYPE_Q5_K)) return false;
@@ -1198,6 +1204,8 @@ bool mul_mat_supported(const ggml_tensor * dst) {
     return true;
 }
 
+bool mm_skinny_run(OpCtx & c, ggml_tensor * dst);   // ops_mmvq.hip
+
 size_t mmq_act_bytes(const ggml_tensor * dst) {
     const ggml_tensor * x = dst->src[1];
     if (dst->op != GGML_OP_MUL_MAT || x->ne[1] <= 8 || !mmq_ok(dst)) return 0;
@@ -1219,6 +1227,7 @@ void op_mul_mat(OpCtx & c, ggml_tensor * dst) {
         return;
     }
     if (x->ne[1] <= 8 && quant_fast_path_ok(dst)) { mmvq_run(c, dst); return; }
+    if (x->ne[1] > 8 && mm_skinny_run(c, dst)) return;   // few f32/f16 rows (the MoE router in prefill)
     if (x->ne[1] > 8 && mmq_ok(dst)) { mmq_run(c, dst); return; }
     mmv_generic_run(c, dst);
 }

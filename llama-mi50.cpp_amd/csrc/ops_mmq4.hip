@@ -105,9 +105,13 @@ template <int QT> struct M4W;
 template <> struct M4W<GGML_TYPE_Q4_K> { int4 hd, q0, q1; };
 template <> struct M4W<GGML_TYPE_Q5_K> { int4 hd, q0, q1, h0, h1; };
 template <> struct M4W<GGML_TYPE_Q6_K> { int4 l0, l1, h0, h1, sc; uint32_t d; };
+// round 5: Q8_0 (the 8-expert recipe's attn_k / attn_v, llama-quant.cpp:311-321; q8_0
+// models): the lane's two 32-weight blocks of the chunk (k 64h .. 64h + 63), each 34 B =
+// f16 d + 32 int8; unit j = block 2h + j
+template <> struct M4W<GGML_TYPE_Q8_0> { int4 a0, a1, b0, b1; uint32_t d; };
 
 template <int QT> __host__ __device__ constexpr int m4_loads() {   // vector loads per chunk (lower bound)
-    return QT == GGML_TYPE_Q4_K ? 3 : 5;
+    return QT == GGML_TYPE_Q4_K ? 3 : QT == GGML_TYPE_Q8_0 ? 6 : 5;
 }
 
 __device__ __forceinline__ int4 ldu16(const char * p) {   // 16 bytes at any 2-byte alignment
@@ -131,6 +135,13 @@ __device__ __forceinline__ void m4_load(const char * row, int kc, int h, M4W<QT>
         r.h1 = *(const int4 *) (b + 32);
         r.q0 = *(const int4 *) (b + 48 + 16 * (4 * hf + 2 * h));
         r.q1 = *(const int4 *) (b + 64 + 16 * (4 * hf + 2 * h));
+    } else if constexpr (QT == GGML_TYPE_Q8_0) {
+        const char * b = row + (size_t) (4 * kc + 2 * h) * 34;       // blocks 4kc + 2h, + 1
+        r.a0 = ldu16(b + 2);
+        r.a1 = ldu16(b + 18);
+        r.b0 = ldu16(b + 36);
+        r.b1 = ldu16(b + 52);
+        r.d = (uint32_t) *(const uint16_t *) b | ((uint32_t) *(const uint16_t *) (b + 34) << 16);
     } else {
         const char * b = row + (size_t) sb * 210;
         r.l0 = ldu16(b + 64 * hf + 32 * h);
@@ -189,6 +200,11 @@ __device__ __forceinline__ M4Scale m4_scales(const M4W<QT> & r, int kc, int h, i
         const _Float16 c = (_Float16) (-dm * (float) (mnp & 0xFF)), e = (_Float16) (-dm * (float) ((mnp >> 8) & 0xFF));
         s.slo = h2{a, a}; s.shi = h2{b, b}; s.mlo = h2{c, c}; s.mhi = h2{e, e};
         s.gb = 2 * g;
+    } else if constexpr (QT == GGML_TYPE_Q8_0) {
+        const _Float16 a = (_Float16) (h2f((uint16_t) (j ? r.d >> 16 : r.d & 0xFFFF)) * ws);
+        s.slo = h2{a, a}; s.shi = s.slo;
+        s.mlo = h2{0, 0}; s.mhi = h2{0, 0};
+        s.gb = 0;
     } else {
         // 16-wide groups: lo k = 128hf + 16U + i -> scale 8hf + U, hi (+64) -> 8hf + 4 + U
         const int slo = 8 * hf + U, shi = slo + 4;
@@ -214,6 +230,12 @@ __device__ __forceinline__ void m4_range(const M4W<QT> & r, float & ws, f16v (&a
     float need;
     if constexpr (QT == GGML_TYPE_Q6_K) {
         need = __builtin_fabsf(h2f((uint16_t) r.d)) * 4096.0f;
+    } else if constexpr (QT == GGML_TYPE_Q8_0) {
+        // the row's two lanes (h = 0, 1) hold different blocks (K-quant lanes share the
+        // super-block header): the largest of all four, so both pick the same scale — the
+        // MFMA sums both halves' B values into one output
+        need = __builtin_fmaxf(__builtin_fabsf(h2f((uint16_t) (r.d & 0xFFFF))), __builtin_fabsf(h2f((uint16_t) (r.d >> 16)))) * 128.0f;
+        need = __builtin_fmaxf(need, __shfl_xor(need, 32, 64));
     } else {
         const float d = __builtin_fabsf(h2f((uint16_t) (dw(r.hd, 0) & 0xFFFF)));
         const float dm = __builtin_fabsf(h2f((uint16_t) (dw(r.hd, 0) >> 16)));
@@ -262,6 +284,22 @@ __device__ __forceinline__ h8 m4_deq(const M4W<QT> & r, const M4Scale & s, int h
                 out[4 * dd + 2 * pp + 1] = f[1];
             }
         }
+    } else if constexpr (QT == GGML_TYPE_Q8_0) {
+        // bytes 8q .. 8q + 7 of block j: int8 -> f16 by the exponent trick, (q + 128) | 0x6400
+        // = 1024 + 128 + q as one v_xor (the pair's high bytes are zero), minus 1152 exactly,
+        // times d ws
+        const int4 & qs = (q < 2) ? (j ? r.b0 : r.a0) : (j ? r.b1 : r.a1);
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd) {
+            const uint32_t w = dw(qs, pd + dd);
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const uint32_t v = pair_bytes(w, pp) ^ 0x64806480u;
+                const h2 f = (as_h2(v) - h2{1152, 1152}) * s.slo;
+                out[4 * dd + 2 * pp] = f[0];
+                out[4 * dd + 2 * pp + 1] = f[1];
+            }
+        }
     } else {
         const int4 & ql = j ? r.l1 : r.l0;
         const int4 & qhv = j ? r.h1 : r.h0;
@@ -305,6 +343,7 @@ __device__ __forceinline__ h8 m4_deq(const M4W<QT> & r, const M4Scale & s, int h
 template <int QT>
 __device__ __forceinline__ int m4_ci(int h, int j, int q) {
     if constexpr (QT == GGML_TYPE_Q6_K) return 4 * h + 2 * j + (q < 2 ? q : 6 + q);   // lo 16U, hi 64 + 16U
+    else if constexpr (QT == GGML_TYPE_Q8_0) return 8 * h + 4 * j + q;               // k 64h + 32j + 8q
     else return 8 * h + 2 * j + (q < 2 ? q : 2 + q);                                 // lo 64h + 16j, hi + 32
 }
 
@@ -955,7 +994,7 @@ void k_mmq5_glu(M4Args p) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-static bool m4_kq(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
+static bool m4_kq(int t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K || t == GGML_TYPE_Q8_0; }
 
 // g_tune[17]: 0 = v4 for every K-quant prefill GEMM it takes (round 3: with the pipelined
 // loop and the cost-model split, also the q/k/v group and the K = 4096 projections),
@@ -1002,11 +1041,12 @@ static void m4_kernel(hipStream_t st, const M4Args & a, dim3 g) {
 template <int EPI, int TT>
 static bool m4_go(hipStream_t st, const M4Args & a, int ta, int tb, dim3 g) {
 #define M4K(A, B) if (ta == A && tb == B) { m4_kernel<A, B, TT, EPI>(st, a, g); return true; }
-    constexpr int Q4 = GGML_TYPE_Q4_K, Q5 = GGML_TYPE_Q5_K, Q6 = GGML_TYPE_Q6_K;
+    constexpr int Q4 = GGML_TYPE_Q4_K, Q5 = GGML_TYPE_Q5_K, Q6 = GGML_TYPE_Q6_K, Q8 = GGML_TYPE_Q8_0;
     if constexpr (EPI == 0) {
         M4K(Q4, Q4) M4K(Q4, Q6) M4K(Q6, Q4) M4K(Q5, Q5) M4K(Q5, Q6) M4K(Q6, Q5) M4K(Q6, Q6)
+        M4K(Q4, Q8) M4K(Q5, Q8) M4K(Q6, Q8) M4K(Q8, Q8)    // round 5: Q8_0 (8-expert k/v, q8_0 models)
     } else {
-        M4K(Q4, Q4) M4K(Q5, Q5) M4K(Q6, Q6)
+        M4K(Q4, Q4) M4K(Q5, Q5) M4K(Q6, Q6) M4K(Q8, Q8)
     }
 #undef M4K
     return false;

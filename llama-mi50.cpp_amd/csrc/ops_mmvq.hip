@@ -570,6 +570,64 @@ __global__ __launch_bounds__(256) void k_mmv_dense(MmvGen p) {
     if (threadIdx.x == 0) *(float *) (p.dst + row * p.d_row + col * p.d_col + i12 * p.d_c2 + i13 * p.d_c3) = acc;
 }
 
+// Round 5: few f32 / f16 weight rows (M <= 64: the MoE router [n_embd, n_expert]) against
+// many columns (a prefill ubatch): one wave per column holding all (up to 16 per pass)
+// row sums, 16-byte loads, the weight rows re-read from L2 by every wave. The generic
+// prefill GEMM took 184 us for Mixtral's 8 x 4096 router at 512 tokens (profiles/r05/).
+template <typename TW>
+__global__ __launch_bounds__(256) void k_mm_skinny(MmvGen p) {
+    const int lane = threadIdx.x & 63;
+    const int64_t col = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (col >= p.N) return;                                 // wave-uniform, no barrier below
+    const int64_t m0 = (int64_t) blockIdx.y * 16;
+    const float * xr = (const float *) (p.x + col * p.x_col);
+    float acc[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int64_t k = 4 * lane; k < p.K; k += 256) {
+        const float4 xv = *(const float4 *) (xr + k);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (m0 + r >= p.M) break;
+            const char * wr = p.w + (m0 + r) * p.w_row + k * sizeof(TW);
+            float4 w4;
+            if constexpr (sizeof(TW) == 4) w4 = *(const float4 *) wr;
+            else {
+                const uint2 h = *(const uint2 *) wr;
+                w4 = make_float4(h2f((uint16_t) (h.x & 0xFFFF)), h2f((uint16_t) (h.x >> 16)), h2f((uint16_t) (h.y & 0xFFFF)),
+                                 h2f((uint16_t) (h.y >> 16)));
+            }
+            acc[r] += w4.x * xv.x + w4.y * xv.y + w4.z * xv.z + w4.w * xv.w;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if (m0 + r >= p.M) break;
+        const float v = wave_sum(acc[r]);
+        if (lane == 0) *(float *) (p.dst + (m0 + r) * p.d_row + col * p.d_col) = v;
+    }
+}
+
+bool mm_skinny_run(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    if ((w->type != GGML_TYPE_F32 && w->type != GGML_TYPE_F16) || w->ne[1] > 64 || x->ne[1] <= 8) return false;
+    if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1 || x->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
+    const size_t ws = w->type == GGML_TYPE_F32 ? 4 : 2;
+    if (w->nb[0] != ws || x->nb[0] != 4 || dst->nb[0] != 4 || w->ne[0] % 4 || ((uintptr_t) w->data | w->nb[1]) % (4 * ws) ||
+        ((uintptr_t) x->data | x->nb[1]) % 16) return false;
+    MmvGen p{};
+    p.w = (const char *) w->data; p.w_row = w->nb[1];
+    p.x = (const char *) x->data; p.x_col = x->nb[1];
+    p.dst = (char *) dst->data; p.d_row = dst->nb[0]; p.d_col = dst->nb[1];
+    p.K = w->ne[0]; p.M = w->ne[1]; p.N = x->ne[1];
+    const dim3 gd((unsigned) mx_ceil_div(p.N, 4), (unsigned) mx_ceil_div(p.M, 16));
+    MX_KLOG("mm_skinny type=%d K=%lld M=%lld N=%lld", (int) w->type, (long long) p.K, (long long) p.M, (long long) p.N);
+    if (w->type == GGML_TYPE_F32) k_mm_skinny<float><<<gd, 256, 0, c.st>>>(p);
+    else k_mm_skinny<uint16_t><<<gd, 256, 0, c.st>>>(p);
+    return true;
+}
+
 void mmv_generic_run(OpCtx & c, ggml_tensor * dst) {
     const ggml_tensor * w = dst->src[0];
     const ggml_tensor * x = dst->src[1];

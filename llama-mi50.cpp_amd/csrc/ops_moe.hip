@@ -311,49 +311,71 @@ int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i) {
 // arithmetic), the router MUL_MAT(gate_inp [K, n_exp] f32/f16, cur) and the top-k chain
 // above (build_moe_ffn, src/llama-graph.cpp:1183-1296). The Mixtral decode profile
 // (profiles/r05/) ran them as three ~5 us launches per layer (rms_norm_q8 4.8-5.1,
-// mmv_dense 4.8, topk_moe 4.6: 470 us of a 3,078 us token). One 512-thread workgroup:
-// the router rows are loaded first (wave e % 8 takes expert e, K/64 floats per lane) and
-// stay in flight while the norm runs; cur goes through LDS to the router dots.
+// mmv_dense 4.8, topk_moe 4.6: 470 us of a 3,078 us token); one workgroup doing all of it
+// took 13.1 us (160 KB through one CU). Now one workgroup per expert: each normalises the
+// whole row (thread t holds 32-chunk t of x, the norm weight and of its expert's router row,
+// all loads issued together), writes its 1/n_exp share of cur and the q8 copy, and its
+// logit; the last workgroup to arrive (agent-scope write-through logit stores + one
+// device-scope counter, reset by it for the next launch / graph replay: the protocol of
+// k_fattn_dec2's in-launch split merge) runs the top-k chain.
 // ---------------------------------------------------------------------------
 struct RouterArgs {
     const float * x; const float * nw; float eps; int K;
     float * cur; int8_t * q; float * qd; float * qs;          // MUL output, its q8 copy (act cache)
     const char * wr; size_t wr1; int wf16;                       // router weights, row (expert) stride in bytes
     float * logits;                                               // MUL_MAT output [n_exp]
+    unsigned int * cnt;                                           // arrival counter, zero between launches
     TopkArgs tk;
 };
 
-template <int KMAX>
-__global__ __launch_bounds__(512) void k_moe_router(RouterArgs p) {
-    __shared__ float xs[KMAX];
+__global__ __launch_bounds__(256) void k_moe_router(RouterArgs p) {
     __shared__ float red[16];
-    __shared__ float lg[64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63, e = blockIdx.x;
     const int K = p.K, nch = K / 32;
-    // 1) the norm: thread b owns 32-chunk b (K <= 32 x 512)
-    float xr[32], wr_[32];
-    float ss = 0.f;
-    if (tid < nch) {
+    const bool on = tid < nch;                                    // K <= 32 x 256
+    const int ch = on ? tid : 0;
+    float xr[32], wn[32], wv[32];
+#pragma unroll
+    for (int j = 0; j < 32; j += 4) {
+        const float4 a = *(const float4 *) (p.x + 32 * ch + j), b = *(const float4 *) (p.nw + 32 * ch + j);
+        xr[j] = a.x; xr[j + 1] = a.y; xr[j + 2] = a.z; xr[j + 3] = a.w;
+        wn[j] = b.x; wn[j + 1] = b.y; wn[j + 2] = b.z; wn[j + 3] = b.w;
+    }
+    const char * row = p.wr + (size_t) e * p.wr1;
+    if (p.wf16) {
+#pragma unroll
+        for (int j = 0; j < 32; j += 8) {
+            const uint4 h = *(const uint4 *) (row + 2 * (size_t) (32 * ch + j));
+            const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { wv[j + 2 * k] = h2f((uint16_t) (hw[k] & 0xFFFF)); wv[j + 2 * k + 1] = h2f((uint16_t) (hw[k] >> 16)); }
+        }
+    } else {
 #pragma unroll
         for (int j = 0; j < 32; j += 4) {
-            const float4 a = *(const float4 *) (p.x + 32 * tid + j), b = *(const float4 *) (p.nw + 32 * tid + j);
-            xr[j] = a.x; xr[j + 1] = a.y; xr[j + 2] = a.z; xr[j + 3] = a.w;
-            wr_[j] = b.x; wr_[j + 1] = b.y; wr_[j + 2] = b.z; wr_[j + 3] = b.w;
+            const float4 c = *(const float4 *) (row + 4 * (size_t) (32 * ch + j));
+            wv[j] = c.x; wv[j + 1] = c.y; wv[j + 2] = c.z; wv[j + 3] = c.w;
         }
+    }
+    float ss = 0.f;
+    if (on) {
 #pragma unroll
         for (int j = 0; j < 32; ++j) ss += xr[j] * xr[j];
     }
     ss = block_sum(ss, red);
     const float scale = 1.0f / sqrtf(ss / (float) K + p.eps);
-    if (tid < nch) {
-        float v[32];
+    float v[32], acc = 0.f;
 #pragma unroll
-        for (int j = 0; j < 32; j += 4) {
-            v[j] = (xr[j] * scale) * wr_[j]; v[j + 1] = (xr[j + 1] * scale) * wr_[j + 1];
-            v[j + 2] = (xr[j + 2] * scale) * wr_[j + 2]; v[j + 3] = (xr[j + 3] * scale) * wr_[j + 3];
-            *(float4 *) (p.cur + 32 * tid + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
-            *(float4 *) (xs + 32 * tid + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
-        }
+    for (int j = 0; j < 32; ++j) {
+        v[j] = (xr[j] * scale) * wn[j];
+        acc += wv[j] * v[j];
+    }
+    // this workgroup's share of cur and of its q8 copy: chunks [e * per, (e + 1) * per)
+    const int per = (nch + gridDim.x - 1) / gridDim.x;
+    if (on && tid >= e * per && tid < (e + 1) * per) {
+#pragma unroll
+        for (int j = 0; j < 32; j += 4) *(float4 *) (p.cur + 32 * tid + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
         float amax = 0.f;
 #pragma unroll
         for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
@@ -376,29 +398,20 @@ __global__ __launch_bounds__(512) void k_moe_router(RouterArgs p) {
         p.qd[tid] = qsc.d;
         p.qs[tid] = qsc.d * (float) sum;
     }
+    acc = block_sum(on ? acc : 0.f, red);
+    if (tid == 0) __hip_atomic_store(&p.logits[e], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through
+    // ---- the last workgroup to arrive runs the top-k chain
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    // 2) router dots: wave w takes experts w, w + 8, ...; f32 accumulation in K order per lane
-    for (int e = wave; e < p.tk.n_exp; e += 8) {
-        const char * row = p.wr + (size_t) e * p.wr1;
-        float acc = 0.f;
-        for (int k = 4 * lane; k < K; k += 256) {
-            float4 w4;
-            if (p.wf16) {
-                const uint2 h = *(const uint2 *) (row + 2 * (size_t) k);
-                w4 = make_float4(h2f((uint16_t) (h.x & 0xFFFF)), h2f((uint16_t) (h.x >> 16)), h2f((uint16_t) (h.y & 0xFFFF)),
-                                 h2f((uint16_t) (h.y >> 16)));
-            } else {
-                w4 = *(const float4 *) (row + 4 * (size_t) k);
-            }
-            const float4 c4 = *(const float4 *) (xs + k);
-            acc += w4.x * c4.x + w4.y * c4.y + w4.z * c4.z + w4.w * c4.w;
-        }
-        acc = wave_sum(acc);
-        if (lane == 0) { lg[e] = acc; p.logits[e] = acc; }
+    if (tid == 0) s_last = __hip_atomic_fetch_add(p.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (tid < 64) {
+        const float lg = lane < p.tk.n_exp ? __hip_atomic_load(&p.logits[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        topk_chain(p.tk, 0, lane, lg);
     }
-    __syncthreads();
-    // 3) soft_max -> top-k -> weights (k_topk_moe's arithmetic), one wave
-    if (wave == 0) topk_chain(p.tk, 0, lane, lane < p.tk.n_exp ? lg[lane] : 0.f);
+    if (tid == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // RMS_NORM at node i -> MUL(w) -> MUL_MAT(gate_inp, cur) -> the top-k chain, one token.
@@ -411,7 +424,7 @@ int fuse_moe_router(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map)
     const ggml_tensor * x = norm->src[0];
     const ggml_tensor * w = mul->src[0] == norm ? mul->src[1] : (mul->src[1] == norm ? mul->src[0] : nullptr);
     const int64_t K = x->ne[0];
-    if (!w || mx_nrows(x) != 1 || K % 32 || K > 8192 || !mx_is_contiguous(x) || !mx_are_same_shape(mul, norm)) return 0;
+    if (!w || mx_nrows(x) != 1 || K % 32 || K > 32 * 256 || !mx_is_contiguous(x) || !mx_are_same_shape(mul, norm)) return 0;
     if (w->type != GGML_TYPE_F32 || mx_nelements(w) != K || !mx_is_contiguous(w) || !mx_is_contiguous(mul)) return 0;
     if (((uintptr_t) x->data | (uintptr_t) w->data | (uintptr_t) mul->data) & 15) return 0;
     auto uses = [&](const ggml_tensor * t) { auto it = use_map.find(t); return it == use_map.end() ? 0 : it->second; };
@@ -461,9 +474,9 @@ int fuse_moe_router(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map)
     r.wr = (const char *) gi->data; r.wr1 = gi->nb[1]; r.wf16 = gi->type == GGML_TYPE_F16;
     r.logits = (float *) mm->data;
     r.tk = tk;
+    r.cnt = c.s->fa_cnt + MX_FA_CNT - 2;        // (the top counter slot is k_attn_o's)
     MX_KLOG("moe_router K=%d n_exp=%d k=%d norm=%d wf16=%d", (int) K, n_exp, tk.k, tk.wn != nullptr, r.wf16);
-    if (K <= 4096) k_moe_router<4096><<<1, 512, 0, c.st>>>(r);
-    else k_moe_router<8192><<<1, 512, 0, c.st>>>(r);
+    k_moe_router<<<(unsigned) n_exp, 256, 0, c.st>>>(r);
     return last - i + 1;
 }
 

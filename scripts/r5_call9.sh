@@ -1,0 +1,24 @@
+#!/bin/bash
+# MoE round: k_mmq4 Q8_0 op tests, router-head fusion test, Mixtral per-position test, the
+# Mixtral drop-in leg, its decode / prefill profiles
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_mmq4_gpu.py tests/test_ops_gpu.py -k "q8_0 or router" -x -q -s --timeout 300 \
+  --timeout-method thread > gpurun_out/r5_c9_ops.log 2>&1
+rc=$?; echo "ops rc=$rc"; tail -3 gpurun_out/r5_c9_ops.log; grep -E "^FAILED|Error|assert" gpurun_out/r5_c9_ops.log | head -10
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 900 python -u -m pytest tests/test_dropin_shapes_gpu.py -k mixtral -x -q -s --timeout 800 --timeout-method thread \
+   > gpurun_out/r5_c9_moe_test.log 2>&1
+rc=$?; echo "moe test rc=$rc"; grep -E "prefill:|decode:|passed|failed|Error|assert" gpurun_out/r5_c9_moe_test.log | head -20
+[ $rc -ge 124 ] && exit $rc
+timeout -k 10 1200 python bench.py --moe-only --dropin-reps 3 > gpurun_out/r5_moe_leg2.json 2> gpurun_out/r5_moe_leg2.err
+echo "moe leg rc=$?"; cut -c1-1500 gpurun_out/r5_moe_leg2.json
+G=$(python -c "import bench; print(bench.bench_gguf('mixtral_8x7b', 'q5_k_m'))") || exit 1
+ROOTDIR=$PWD; cd /tmp && export TMPDIR=/tmp && cd "$ROOTDIR"
+export GGML_BACKEND_PATH=$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
+for t in "tg -p 0 -n 64" "pp -p 512 -n 0"; do
+  set -- $t; name=$1; shift
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_moe2_$name -o run --output-format csv -- \
+    oracle/_ref/llama-bench -m $G -t 8 -ngl 99 -fa 1 "$@" -r 1 -o jsonl > gpurun_out/prof_moe2_$name.log 2>&1
+  echo "$name rc=$?"; head -14 gpurun_out/prof_moe2_$name/run_kernel_stats.csv | cut -c1-150
+done

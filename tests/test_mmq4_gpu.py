@@ -26,15 +26,16 @@ from qgen import NAMES, nmse, rand_quant
 
 pytestmark = pytest.mark.gpu
 
-BLOCK = {12: 144, 13: 176, 14: 210}
-BIG_D = {12: (0, 0.2), 13: (0, 0.1), 14: (208, 0.05)}   # (f16 d offset, d): |w| up to ~190-205
+BLOCK = {12: 144, 13: 176, 14: 210, 8: 34}
+QK = {12: 256, 13: 256, 14: 256, 8: 32}                # weights per block
+BIG_D = {12: (0, 0.2), 13: (0, 0.1), 14: (208, 0.05), 8: (0, 1.6)}   # (f16 d offset, d): |w| up to ~190-205
 
 
 def with_outliers(raw, tid, M, K, rng):
     """rows 5 (last super-block), 77 (first super-block) and M-3 (every block) get d so
     large that the dequantised weights reach |w| ~ 200; returns (raw, outlier row list)"""
     raw = raw.copy()
-    bs, nb = BLOCK[tid], K // 256
+    bs, nb = BLOCK[tid], K // QK[tid]
     off, d = BIG_D[tid]
     blocks = raw.reshape(M, nb, bs)
     sel = [(5, [nb - 1]), (77 % M, [0]), (M - 3, list(range(nb)))]
@@ -89,7 +90,7 @@ def klog_has(log, pred):
     return NO_KLOG or any(pred(l) for l in log)
 
 
-@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K"])
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K", "q8_0"])
 @pytest.mark.parametrize("ks", [1, 2, 4])
 @pytest.mark.parametrize("outlier", [False, True])
 def test_mmq4_plain(pkg, backend, orc, tname, ks, outlier):
@@ -138,7 +139,8 @@ def test_mmq4_residual(pkg, backend, orc, tname, ks):
 
 
 @pytest.mark.parametrize("types", [("q4_K", "q4_K", "q6_K"), ("q6_K", "q4_K"), ("q5_K", "q5_K", "q6_K"),
-                                   ("q5_K", "q5_K", "q5_K")])
+                                   ("q5_K", "q5_K", "q5_K"), ("q5_K", "q8_0", "q8_0"), ("q4_K", "q8_0", "q8_0"),
+                                   ("q8_0", "q8_0", "q8_0")])
 @pytest.mark.parametrize("ks", [1, 2])
 def test_mmq4_group(pkg, backend, orc, types, ks):
     """2-3 GEMMs sharing src1 in ONE k_mmq4 launch (segments, two weight types at most);
@@ -169,7 +171,7 @@ def test_mmq4_group(pkg, backend, orc, types, ks):
         check(y.reshape(N, M), orc.mul_mat(NAMES[t], w, rb, x, exact=True), ro)
 
 
-@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K"])
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K", "q8_0"])
 @pytest.mark.parametrize("N", [150, 40])
 def test_mmq4_glu(pkg, backend, orc, tname, N):
     """gate/up/SwiGLU in one k_mmq4 launch (EPI 1): gate and up waves keep separate weight
@@ -229,7 +231,7 @@ def test_mmq5_glu(pkg, backend, orc, M, N, outlier):
     check(y.reshape(N, M), orc.swiglu(g, u), rows_out)
 
 
-@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K"])
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K", "q8_0"])
 def test_mmq4_moe(pkg, backend, orc, tname):
     """MUL_MAT_ID prefill: items sorted by expert on the device, ONE k_mmq4 launch of
     expert-grouped tiles (EPI 2, activation rows gathered, outputs scattered); a skewed
