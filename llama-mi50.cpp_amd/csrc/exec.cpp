@@ -468,6 +468,9 @@ static bool try_fuse_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses, bool 
 // MUL_MAT_ID(gate), MUL_MAT_ID(up), GLU of a decode step (llama build_moe_ffn): one v2
 // GEMV over both expert streams per (slot, token) item, SwiGLU epilogue, and the q8 of
 // the result for the down projection's prologue
+bool mmq4_moe_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu);   // ops_mmq4.hip
+static const bool g_no_moe_glu_mm = getenv("GGML_MI355X_NO_MOE_GLU_MM") != nullptr;   // A/B
+
 static bool try_fuse_moe_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     if (i + 2 >= g->n_nodes) return false;
     ggml_tensor * a = g->nodes[i];
@@ -478,7 +481,7 @@ static bool try_fuse_moe_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     const ggml_tensor * gate = glu->src[0] == a && glu->src[1] == b ? a : (glu->src[0] == b && glu->src[1] == a ? b : nullptr);
     if (!gate) return false;
     const ggml_tensor * up = gate == a ? b : a;
-    if (gate->src[1] != up->src[1] || gate->src[2] != up->src[2] || up->src[2]->ne[1] > 8) return false;
+    if (gate->src[1] != up->src[1] || gate->src[2] != up->src[2]) return false;
     if (uses[a] != 1 || uses[b] != 1 || ((a->flags | b->flags) & GGML_TENSOR_FLAG_OUTPUT)) return false;
     if (!mx_are_same_shape(glu, gate) || glu->type != GGML_TYPE_F32 || !mx_is_contiguous(glu)) return false;
     for (const ggml_tensor * t : {gate->src[1], gate->src[2], gate->src[0], up->src[0]})
@@ -486,6 +489,8 @@ static bool try_fuse_moe_glu(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     deferred_guard_read(c, gate->src[1]);
     deferred_guard_write(c, glu);
     act_cache_invalidate(c.s, glu);
+    // prefill (round 5): the expert-grouped gate/up GEMM with the SwiGLU epilogue (k_mmq4 EPI 3)
+    if (up->src[2]->ne[1] > 8) return !g_no_moe_glu_mm && mmq4_moe_glu(c, gate, up, glu);
     ActQ * q8 = glu->ne[0] % 32 == 0 ? act_cache_alloc(c.s, glu) : nullptr;
     if (!gemv2_moe(c, gate, up->src[0], glu, q8)) {
         if (q8) act_cache_invalidate(c.s, glu);
@@ -815,7 +820,7 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
     size_t need = 0, slot = 0, f16need = 0;
     for (int i = 0; i < g->n_nodes; ++i) {
         need = std::max(need, scratch_bytes(g->nodes[i]));
-        if (g->nodes[i]->op == GGML_OP_MUL_MAT) f16need = std::max(f16need, mmq_act_bytes(g->nodes[i]));
+        if (g->nodes[i]->op == GGML_OP_MUL_MAT || g->nodes[i]->op == GGML_OP_MUL_MAT_ID) f16need = std::max(f16need, mmq_act_bytes(g->nodes[i]));
         if (g->nodes[i]->op == GGML_OP_MUL_MAT && mmvq_small_batch_ok(g->nodes[i])) slot = std::max(slot, act_slot_bytes(g->nodes[i]->src[1]));
         if (g->nodes[i]->op == GGML_OP_MUL && mx_nrows(g->nodes[i]) <= 8) slot = std::max(slot, act_slot_bytes(g->nodes[i]));
         // MoE decode: the q8 copy of the gate/up SwiGLU output (= this node's shape) and of src1

@@ -24,6 +24,7 @@ _Float16 * mmq_act_f16(OpCtx & c, const ggml_tensor * x, int64_t kp);
 bool mmq4_on();
 size_t mmq4_scratch(const ggml_tensor * dst);   // split-K partial sums
 size_t mmq4_moe_scratch(const ggml_tensor * dst);
+bool mmq4_moe_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu);   // + SwiGLU, prefill
 bool mmq4_moe(OpCtx & c, ggml_tensor * dst);     // MUL_MAT_ID prefill, expert-grouped
 bool mmq4_mul_mat(OpCtx & c, const ggml_tensor * w, const ggml_tensor * x, const _Float16 * xa, int64_t kp,
                   ggml_tensor * out, const ggml_tensor * res);

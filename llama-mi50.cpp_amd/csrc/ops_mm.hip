@@ -1208,6 +1208,9 @@ bool mm_skinny_run(OpCtx & c, ggml_tensor * dst);   // ops_mmvq.hip
 
 size_t mmq_act_bytes(const ggml_tensor * dst) {
     const ggml_tensor * x = dst->src[1];
+    // MoE prefill (round 5): the expert GEMMs' input, and the fused gate/up SwiGLU's f16
+    // output claimed for the down projection (ne0 x n_used x n_tok, ~29 MB for Mixtral pp512)
+    if (dst->op == GGML_OP_MUL_MAT_ID) return mmq4_moe_scratch(dst) ? (size_t) x->ne[0] * x->ne[1] * x->ne[2] * 2 : 0;
     if (dst->op != GGML_OP_MUL_MAT || x->ne[1] <= 8 || !mmq_ok(dst)) return 0;
     return (size_t) x->ne[1] * x->ne[2] * x->ne[3] * mmq_kp(dst) * 2;
 }

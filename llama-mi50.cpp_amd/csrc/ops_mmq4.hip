@@ -538,7 +538,8 @@ __device__ __forceinline__ void m4_kloop(const M4Args & p, const char * wrow, co
 
 // EPI 0: store (+ residual) to the segment; 1: SwiGLU of a gate/up pair (waves 0-3 gate
 // rows, 4-7 up rows of the same 128); 2: MoE expert tile — grid.z = expert, token slots
-// gathered through p.gather, outputs scattered through p.scatter.
+// gathered through p.gather, outputs scattered through p.scatter; 3 (round 5): both — the
+// MoE gate/up/SwiGLU of an expert's tokens in one launch (w / w2 = gate / up experts).
 // Split K (EPI 0, grid.z = p.ksplit > 1): each workgroup sums its share of the K chunks
 // into p.part[z][token][global row]; k_mmq4_reduce adds the shares in order.
 template <int QTA, int QTB, int TT, int EPI, int X = M4_XDEF>
@@ -546,24 +547,25 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
     extern __shared__ __align__(16) uint4 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     constexpr int BT = 32 * TT;
-    // MoE (EPI 2): grid.x = row tile, grid.y = token tile. Workgroups go to the XCDs
+    constexpr bool MOE = EPI == 2 || EPI == 3, GLU = EPI == 1 || EPI == 3;
+    // MoE (EPI 2, 3): grid.x = row tile, grid.y = token tile. Workgroups go to the XCDs
     // round-robin by linear index, and most token tiles of an expert are empty: with the
     // token tile fastest every busy workgroup (token tile 0) landed on XCD 0 (measured:
     // 1.8 ms instead of ~0.3 for a Mixtral pp512 gate projection)
-    const int by = EPI == 2 ? (int) blockIdx.x : (int) blockIdx.y;
-    const int bx = EPI == 2 ? (int) blockIdx.y : (int) blockIdx.x;
+    const int by = MOE ? (int) blockIdx.x : (int) blockIdx.y;
+    const int bx = MOE ? (int) blockIdx.y : (int) blockIdx.x;
     int si = 0;
 #pragma unroll
     for (int i = 1; i < M4_MAXSEG; ++i) if (i < p.nseg && by >= p.seg[i].tile0) si = i;
     const M4Seg & sg = p.seg[si];
     const int tile = by - sg.tile0;
     int tok0 = bx * BT, ntok = p.N, slot0 = 0;
-    const char * wb = sg.w;
+    const char * wb = sg.w, * wb2 = p.w2;
     const int nk = p.K / M4_KC;
     int c0 = 0, nc = nk;
     const size_t bid = blockIdx.x + (size_t) gridDim.x * (blockIdx.y + (size_t) gridDim.y * blockIdx.z);
     if (p.trace_blk && tid == 0 && bid < 65536) p.trace_blk[2 * bid] = __builtin_amdgcn_s_memrealtime();
-    if constexpr (EPI == 2) {
+    if constexpr (MOE) {
         const int e = (int) blockIdx.z;
         slot0 = p.tile_tab[2 * e];
         ntok = p.tile_tab[2 * e + 1];
@@ -572,23 +574,24 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
             return;
         }
         wb += (size_t) e * p.w_exp;
+        if constexpr (GLU) wb2 += (size_t) e * p.w_exp;
     } else if (p.ksplit > 1) {
         c0 = (int) blockIdx.z * nk / p.ksplit;
         nc = ((int) blockIdx.z + 1) * nk / p.ksplit - c0;
     }
     // rows of this wave
-    constexpr int RPT = EPI == 1 ? 32 * M4_WAVES / 2 : 32 * M4_WAVES;   // output rows per tile
-    const int wr = EPI == 1 ? (wave & (M4_WAVES / 2 - 1)) : wave;
+    constexpr int RPT = GLU ? 32 * M4_WAVES / 2 : 32 * M4_WAVES;   // output rows per tile
+    const int wr = GLU ? (wave & (M4_WAVES / 2 - 1)) : wave;
     const int row = tile * RPT + wr * 32 + r;
     const int rr = row < sg.M ? row : sg.M - 1;
-    const char * wrow = (EPI == 1 && wave >= M4_WAVES / 2 ? p.w2 : wb) + (size_t) rr * sg.w_row;
+    const char * wrow = (GLU && wave >= M4_WAVES / 2 ? wb2 : wb) + (size_t) rr * sg.w_row;
     // activation columns of this wave's DMA pieces (token row clamped into range)
     int cols[TT];
 #pragma unroll
     for (int i = 0; i < TT; ++i) {
         int t = tok0 + (wave * TT + i) * 4 + (lane >> 4);
         t = t < ntok ? t : ntok - 1;
-        cols[i] = EPI == 2 ? p.gather[slot0 + t] : t;
+        cols[i] = MOE ? p.gather[slot0 + t] : t;
     }
     f16v acc[TT];
     float ws = M4_WSCALE;                             // this lane's weight scale (m4_range)
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
 
     if (p.trace_blk && tid == 0 && bid < 65536) p.trace_blk[2 * bid + 1] = __builtin_amdgcn_s_memrealtime();
     const float inv = 1.0f / ws;
-    if constexpr (EPI == 1) {
+    if constexpr (GLU) {
         float * red = (float *) lds;                  // 4 waves x TT x 16 x 64 floats (<= the ring)
         m4_barrier();                                 // every wave is done with the ring
         if (wave >= M4_WAVES / 2) {
@@ -618,8 +621,9 @@ __global__ __launch_bounds__(512, 1) void k_mmq4(M4Args p) {
                 const float g = acc[t][e] * inv, u = red[((wave * TT + t) * 16 + e) * 64 + lane];
                 const float v = g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-g * 1.4426950408889634f)) * u;
                 if (tok < ntok && row < sg.M) {
-                    sg.dst[(size_t) tok * sg.d_col + row] = v;
-                    if (p.h) p.h[(size_t) tok * p.h_col + row] = (_Float16) v;
+                    const size_t oc = MOE ? (size_t) p.scatter[slot0 + tok] : (size_t) tok;
+                    sg.dst[oc * sg.d_col + row] = v;
+                    if (p.h) p.h[oc * p.h_col + row] = (_Float16) v;
                 }
             }
     } else if (EPI == 0 && p.ksplit > 1) {
@@ -1104,7 +1108,7 @@ static bool m4_dispatch(OpCtx & c, M4Args & a, int ta, int tb, int tiles_y, int 
             nz = ks;
         }
     }
-    const dim3 g = EPI == 2 ? dim3((unsigned) tiles_y, (unsigned) gx, (unsigned) nz) : dim3((unsigned) gx, (unsigned) tiles_y, (unsigned) nz);
+    const dim3 g = EPI >= 2 ? dim3((unsigned) tiles_y, (unsigned) gx, (unsigned) nz) : dim3((unsigned) gx, (unsigned) tiles_y, (unsigned) nz);
     const bool ok = tt == 4 ? m4_go<EPI, 4>(c.st, a, ta, tb, g) : m4_go<EPI, 2>(c.st, a, ta, tb, g);
     bool taken = false;
     if (ok && a.ksplit > 1 && g_m4_split && !a.h) {
@@ -1314,6 +1318,43 @@ bool mmq4_moe(OpCtx & c, ggml_tensor * dst) {
     // count exit at once
     MX_ASSERT(m4_dispatch<2>(c, a, as->type, as->type, tiles, n_exp, tt));
     return true;
+}
+
+// Round 5: MUL_MAT_ID(gate) , MUL_MAT_ID(up) , GLU(swiglu) of a prefill ubatch in ONE k_mmq4
+// launch (EPI 3): one expert sort, each expert's token tile multiplied by its gate rows
+// (waves 0-3) and up rows (waves 4-7) over the same activation tile, silu(g) * u written
+// to the GLU output and its f16 copy for the down projection's GEMM (claimed in the
+// activation cache, as the dense SwiGLU does). Before: two EPI 2 launches (each gathering
+// the activations) + a GLU pass + an f16 conversion pass.
+bool mmq4_moe_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu) {
+    if (!m4_moe_ok(gate) || !m4_moe_ok(up)) return false;
+    const ggml_tensor * wg = gate->src[0], * wu = up->src[0], * b = gate->src[1], * ids = gate->src[2];
+    if (up->src[1] != b || up->src[2] != ids || wg->type != wu->type) return false;
+    for (int i = 0; i < 4; ++i) if (wg->ne[i] != wu->ne[i] || wg->nb[i] != wu->nb[i]) return false;
+    if (!mx_are_same_shape(glu, gate) || glu->type != GGML_TYPE_F32 || glu->nb[0] != 4 || glu->nb[1] != gate->nb[1] ||
+        glu->nb[2] != gate->nb[2]) return false;
+    const int n_used = (int) ids->ne[0], n_tok = (int) ids->ne[1], n_exp = (int) wg->ne[2];
+    const int items = n_used * n_tok;
+    int32_t * gather = (int32_t *) c.scratch->take((size_t) items * 4);
+    int32_t * scatter = (int32_t *) c.scratch->take((size_t) items * 4);
+    int32_t * tab = (int32_t *) c.scratch->take((size_t) 2 * M4_MAXEXP * 4);
+    k_moe_sort<<<1, 1024, 0, c.st>>>((const char *) ids->data, ids->nb[0], ids->nb[1], n_used, n_tok, n_exp,
+                                     (int) b->ne[1], gather, scatter, tab);
+    const int64_t kp = wg->ne[0];
+    const _Float16 * xa = mmq_act_f16(c, b, kp);
+    M4Args a{};
+    a.nseg = 1;
+    a.seg[0] = M4Seg{(const char *) wg->data, wg->nb[1], (float *) glu->data, glu->nb[1] / 4, nullptr, 0, (int) wg->ne[1], 0, 0};
+    a.w2 = (const char *) wu->data;
+    a.x = xa; a.kp = kp; a.N = items; a.K = (int) wg->ne[0];
+    a.gather = gather; a.scatter = scatter; a.tile_tab = tab; a.w_exp = wg->nb[2];
+    // the down projection's f16 input, rows of glu->nb[1] bytes = one (slot, token) column each
+    a.h = mmq_act_claim(c, glu->data, glu->ne[0], (int64_t) glu->ne[1] * glu->ne[2], glu->nb[1]);
+    a.h_col = glu->ne[0];
+    const int tt = m4_tt(), tiles = (int) mx_ceil_div(wg->ne[1], 16 * M4_WAVES);
+    MX_KLOG("mmq4 moe_glu qt=%d tt=%d M=%lld items=%d experts=%d K=%d h=%d", (int) wg->type, tt, (long long) wg->ne[1], items, n_exp,
+            a.K, a.h != nullptr);
+    return m4_dispatch<3>(c, a, wg->type, wg->type, tiles, n_exp, tt);
 }
 
 }  // namespace mx

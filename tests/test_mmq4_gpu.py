@@ -264,3 +264,54 @@ def test_mmq4_moe(pkg, backend, orc, tname):
             continue
         ref = orc.mul_mat(tid, parts[e][0], rb, x[sel[:, 0], 0], exact=True)
         check(y[sel[:, 0], sel[:, 1]], ref, rows_out if e == 2 else ())
+
+
+@pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K", "q8_0"])
+def test_mmq4_moe_glu(pkg, backend, orc, tname):
+    """MoE prefill gate/up/SwiGLU (llama build_moe_ffn) in ONE k_mmq4 launch (EPI 3): the
+    expert-grouped tiles with gate waves and up waves over the same gathered activations,
+    silu(g) * u scattered to the GLU output and its f16 copy claimed for the down
+    projection's expert GEMM (checked through the down product too); skewed routing,
+    outliers in one expert's up rows"""
+    tid = NAMES[tname]
+    rng = np.random.default_rng(77 + tid)
+    K, M, Md, E, used, T = 2048, 512, 200, 4, 2, 70
+    wg = [rand_quant(tid, M, K, rng) for _ in range(E)]
+    wu = [rand_quant(tid, M, K, rng) for _ in range(E)]
+    rb = wg[0][1]
+    w2, rows_out = with_outliers(wu[2][0], tid, M, K, rng)
+    wu[2] = (w2, rb)
+    wd = [rand_quant(tid, Md, M, rng) for _ in range(E)]
+    rbd = wd[0][1]
+    x = rng.standard_normal((T, 1, K)).astype(np.float32)
+    ids = np.stack([np.where(rng.random(T) < 0.8, 1, 0), np.where(rng.random(T) < 0.3, 2, 0)], 1).astype(np.int32)
+    ids[:, 1] = np.where(ids[:, 1] == ids[:, 0], 2, ids[:, 1])
+
+    def build(ctx):
+        tg = ctx.new_tensor(tid, K, M, E)
+        tu = ctx.new_tensor(tid, K, M, E)
+        td = ctx.new_tensor(tid, M, Md, E)
+        tx = ctx.new_tensor("f32", K, 1, T)
+        ti = ctx.new_tensor("i32", used, T)
+        up = ctx.mul_mat_id(tu, tx, ti)
+        gate = ctx.mul_mat_id(tg, tx, ti)
+        glu = ctx.swiglu_split(gate, up)
+        down = ctx.mul_mat_id(td, glu, ti)
+        return [glu, down], [(tg, np.concatenate([w for w, _ in wg])), (tu, np.concatenate([w for w, _ in wu])),
+                             (td, np.concatenate([w for w, _ in wd])), (tx, x), (ti, ids)]
+
+    (y, yd), log = run(pkg, backend, build)
+    assert klog_has(log, lambda l: l.startswith(f"mmq4 moe_glu qt={tid} ") and l.endswith(" h=1")), log
+    assert klog_has(launch_lines(log), lambda l: "epi=3 " in l), log
+    y = y.reshape(T, used, M)
+    yd = yd.reshape(T, used, Md)
+    for e in range(E):
+        sel = np.argwhere(ids == e)
+        if not len(sel):
+            continue
+        xe = x[sel[:, 0], 0]
+        g = orc.mul_mat(tid, wg[e][0], rb, xe, exact=True)
+        u = orc.mul_mat(tid, wu[e][0], rb, xe, exact=True)
+        ye = y[sel[:, 0], sel[:, 1]]
+        check(ye, orc.swiglu(g, u), rows_out if e == 2 else ())
+        check(yd[sel[:, 0], sel[:, 1]], orc.mul_mat(tid, wd[e][0], rbd, ye, exact=True), ())
