@@ -184,7 +184,14 @@ void op_sum_rows(OpCtx & c, ggml_tensor * dst);
 void op_argsort(OpCtx & c, ggml_tensor * dst);
 void op_mul_mat(OpCtx & c, ggml_tensor * dst);
 void op_mul_mat_split(OpCtx & c, ggml_tensor * dst);
+void op_mul_mat_split_n(OpCtx & c, ggml_tensor * const * dsts, int n);   // 1-3 sharing src1, one fork / join
 int split_local_slices(const Stream * s, const ggml_tensor * w, void ** data, int64_t * lo, int64_t * hi);
+// every non-empty slice of a row-split weight whose device reads the main device's memory
+// directly (same GPU or peer access): data, rows, logical device; 0 when any slice cannot
+int split_slices(const Stream * s, const ggml_tensor * w, void ** data, int64_t * lo, int64_t * hi, int * dev);
+bool split_on_main(const Stream * s, const ggml_tensor * w, int dev);   // slice of w runs on the main stream itself
+OpCtx split_fork(OpCtx & c, int dev);             // the slice device's stream, after the main stream's work so far
+void split_join(OpCtx & c, int dev);              // the main stream, after the slice stream's work so far
 void split_stream_free(const Stream * main);   // be_free: drop the freed stream's row-split staging
 void op_mul_mat_id(OpCtx & c, ggml_tensor * dst);
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst);

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 
 #include "ggml_abi.h"
 
@@ -20,6 +21,14 @@
 [[noreturn]] void mx_abort(const char * file, int line, const char * fmt, ...);
 #define MX_ABORT(...) mx_abort(__FILE__, __LINE__, __VA_ARGS__)
 #define MX_ASSERT(x) do { if (!(x)) MX_ABORT("assert failed: %s", #x); } while (0)
+// dynamic-LDS opt-in of kernel f once per device (a static at the call site): the attribute
+// applies to the current device, and one process may drive several GPUs (layer / row split)
+#define MX_LDS_OPTIN(f, bytes) do { static std::atomic<unsigned> done_{0u}; int dev_ = 0; \
+    HIP_CHECK(hipGetDevice(&dev_)); const unsigned bit_ = 1u << (dev_ & 31); \
+    if (!(done_.load(std::memory_order_relaxed) & bit_)) { \
+        HIP_CHECK(hipFuncSetAttribute((const void *) (f), hipFuncAttributeMaxDynamicSharedMemorySize, (int) (bytes))); \
+        done_.fetch_or(bit_); } } while (0)
+
 #define HIP_CHECK(call) do { hipError_t err_ = (call); if (err_ != hipSuccess) \
     MX_ABORT("HIP error %d (%s) in %s", (int) err_, hipGetErrorString(err_), #call); } while (0)
 

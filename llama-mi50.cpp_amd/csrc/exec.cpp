@@ -190,9 +190,22 @@ void deferred_guard_read(OpCtx & c, const ggml_tensor * t) {
 }
 
 bool gemv2_stage(OpCtx & c, const ggml_tensor * x, std::initializer_list<const ggml_tensor *> outs,
-                 std::initializer_list<const ggml_tensor *> reads, XStage * xs) {
+                 std::initializer_list<const ggml_tensor *> reads, XStage * xs, int absorbs) {
     for (const ggml_tensor * t : reads) deferred_guard_read(c, t);
-    for (const ggml_tensor * t : outs) deferred_guard_write(c, t);
+    // A deferred norm this launch absorbs for its last pending consumers is never
+    // materialised: its output's memory is dead, and libllama's allocator hands it to this
+    // launch's own output once the gate/up MUL_MATs are its last readers (the GLU lands over
+    // the normed x whenever the graph's layout puts it there — at llama-bench -d 16384 in
+    // 30 of 32 layers). Writing there must not materialise the norm (round 4 did: an
+    // RMS-norm launch, then the q8 path, 30 us per layer)
+    for (const ggml_tensor * t : outs) {
+        for (size_t k = 0; k < c.s->deferred.size();) {
+            const DeferredNorm & d = c.s->deferred[k];
+            const bool absorbed = x->data == d.mul->data && mx_nelements(x) == mx_nelements(d.mul) && d.pending <= absorbs;
+            if (t_overlaps(t, d.norm->src[0]) || t_overlaps(t, d.w) || (!absorbed && t_overlaps(t, d.mul))) materialize(c, k);
+            else ++k;
+        }
+    }
     *xs = xstage_of(c.s, x);
     const size_t xb = (size_t) x->ne[0] * sizeof(float);
     for (const ggml_tensor * t : outs) {
@@ -620,6 +633,38 @@ static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q, bo
 // must not replay over freed memory
 static std::atomic<unsigned> g_buf_gen{0};
 
+// row split: MUL_MATs right after node i (views between) that share its src1 and whose
+// split weights have the same non-empty slices, all reachable directly: run as one group
+static int try_split_group(OpCtx & c, ggml_cgraph * g, int i, std::unordered_map<const ggml_tensor *, int> & done) {
+    ggml_tensor * n = g->nodes[i];
+    void * dt[MX_MAX_DEVICES];
+    int64_t lo[MX_MAX_DEVICES], hi[MX_MAX_DEVICES];
+    int dv0[MX_MAX_DEVICES], dv[MX_MAX_DEVICES];
+    const int ns = split_slices(c.s, n->src[0], dt, lo, hi, dv0);
+    if (!ns || n->type != GGML_TYPE_F32 || !mx_is_contiguous(n)) return 0;
+    ggml_tensor * grp[3] = {n, nullptr, nullptr};
+    int ng = 1;
+    for (int j = i + 1; j < g->n_nodes && ng < 3; ++j) {
+        ggml_tensor * m = g->nodes[j];
+        if (is_view_op(m->op) || mx_is_empty(m)) continue;
+        if (m->op != GGML_OP_MUL_MAT || m->src[1] != n->src[1] || !tensor_is_split(m->src[0]) || m->type != GGML_TYPE_F32 ||
+            !mx_is_contiguous(m)) break;
+        if (split_slices(c.s, m->src[0], dt, lo, hi, dv) != ns || memcmp(dv, dv0, sizeof(int) * ns)) break;
+        bool reads_group = false;   // (never: a MUL_MAT of the group reading another's output)
+        for (int k = 0; k < ng; ++k) reads_group = reads_group || m->src[0] == grp[k] || t_overlaps(m->src[1], grp[k]);
+        if (reads_group) break;
+        grp[ng++] = m;
+    }
+    if (ng < 2) return 0;
+    for (int k = 0; k < ng; ++k) {
+        deferred_guard_node(c, grp[k]);
+        act_cache_invalidate(c.s, grp[k]);
+        if (k) done[grp[k]] = 1;
+    }
+    op_mul_mat_split_n(c, grp, ng);
+    return ng;
+}
+
 static void run_nodes(Stream * s, ggml_cgraph * g) {
     OpCtx c{s, s->stream, &s->scratch};
     static thread_local UseMap uses;
@@ -655,6 +700,11 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
                 if (try_fuse_glu(c, g, i, uses, true)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
                 const int k = try_fuse_mm_add(c, g, i, uses);
                 if (k) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; continue; }
+            }
+            // q / k / v (split MUL_MATs sharing src1, only views between): one fork / join
+            if (!no_split_fusion && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0])) {
+                const int ng = try_split_group(c, g, i, done);
+                if (ng > 1) { s->n_nodes_run += ng; continue; }
             }
         } else if (s->use_fusion) {
             const int i0 = i;

@@ -55,8 +55,9 @@ void deferred_guard_write(OpCtx & c, const ggml_tensor * t);
 void deferred_guard_read(OpCtx & c, const ggml_tensor * t);
 // Activation staging for a fused GEMV that writes `outs` (and reads `reads`): guards the
 // deferred norms, then fails when an output overlaps what the prologue reads (the
-// workgroups would race) — the caller then takes the quantise-first path.
+// workgroups would race) — the caller then takes the quantise-first path. `absorbs`: the
+// consumers of x this launch stands for (2: a gate/up pair, 3: q/k/v).
 bool gemv2_stage(OpCtx & c, const ggml_tensor * x, std::initializer_list<const ggml_tensor *> outs,
-                 std::initializer_list<const ggml_tensor *> reads, XStage * xs);
+                 std::initializer_list<const ggml_tensor *> reads, XStage * xs, int absorbs = 1);
 
 }  // namespace mx

@@ -526,7 +526,11 @@ static FdCfg fd_cfg(int D, int Gt, int64_t n_kv, int64_t rows) {   // rows = Hkv
     return {g, 4, (int) mx_ceil_div(nch, cpw), true, cpw};
 }
 
+static size_t fd3_scratch(const ggml_tensor * dst);
+static bool fd3_run(OpCtx & c, ggml_tensor * dst);
+
 size_t fa_dec2_scratch(const ggml_tensor * dst) {
+    if (const size_t s3 = fd3_scratch(dst)) return s3;
     const ggml_tensor * q = dst->src[0], * k = dst->src[1];
     const int64_t D = k->ne[0];
     const FdCfg f = fd_cfg((int) D, (int) (q->ne[2] / k->ne[2]), k->ne[1], k->ne[2] * q->ne[1] * q->ne[3]);
@@ -534,6 +538,7 @@ size_t fa_dec2_scratch(const ggml_tensor * dst) {
 }
 
 void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
+    if (fd3_run(c, dst)) return;                 // long caches: the streaming form (k_fattn_dec3)
     const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
     FaDecArgs a{};
     a.q = (const char *) q->data; a.q1 = q->nb[1]; a.q2 = q->nb[2]; a.q3 = q->nb[3];
@@ -576,9 +581,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
             else k_fattn_dec2<DD, GG, 4, false, FD_LONG_NI, true, CP><<<grid, 256, 0, c.st>>>(a); }
 #define FLW(DD, GG, CPWS) if (D == DD && f.G == GG) { \
             CPWS \
-            static const bool attr = [] { HIP_CHECK(hipFuncSetAttribute((const void *) k_fattn_dec2_combine<DD, GG>, \
-                hipFuncAttributeMaxDynamicSharedMemorySize, FD_LONG_MAXSPLIT * (int) sizeof(float))); return true; }(); \
-            (void) attr; \
+            MX_LDS_OPTIN((k_fattn_dec2_combine<DD, GG>), FD_LONG_MAXSPLIT * (int) sizeof(float)); \
             k_fattn_dec2_combine<DD, GG><<<gc, 256, lds, c.st>>>(a); \
             return; }
         const int ni = D == 128 && g_tune[1] && a.n_kv <= 16 * FD_NI * (64 / (D / 8)) && a.n_kv > 4 * g_tune[1] * (64 / (D / 8)) ? g_tune[1] :
@@ -676,6 +679,354 @@ void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit) {
         if (kq) k_fattn_dec2<128, 1, 4, true, 4, true><<<grid, 256, 0, c.st>>>(a);
         else k_fattn_dec2<128, 1, 4, false, 4, true><<<grid, 256, 0, c.st>>>(a);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Round 5: long-context decode attention as a stream (k_fattn_dec3). The LONG geometry
+// above gives every workgroup one 128-key chunk held in registers (124 VGPRs: 4 waves per
+// SIMD), so 16k keys x 8 KV heads x 2 head pairs ran as two rounds of 1,024 workgroups
+// that all issue, wait, compute and leave together, and its 128 partials per head needed
+// a combine launch: 20.7 + 5.0 us per layer at depth 16384 (0.40 of HBM).
+// Here one workgroup per CU (Hkv x NS of them, ~256) streams a contiguous key range of
+// one KV head for ALL Gt query heads of its GQA group (K/V read once), through an LDS ring
+// filled by LDS-DMA (global_load_lds, no registers held): each wave owns its own slots of
+// the ring — it DMAs and later reads back only its own 16-key wave-stages — so the loop has
+// no barrier, only per-wave vmcnt waits, with S - 1 wave-stages (3 x 8 KB) ahead per wave.
+// Splits merge in the same launch (agent-scope partial stores, the last of a KV head's NS
+// workgroups to arrive combines, as k_fattn_dec2's short-cache form): no combine launch.
+// Semantics as k_fattn_dec2 (f16 K/V, D 128, log2-domain online softmax).
+// ---------------------------------------------------------------------------
+constexpr int FD3_SK = 16;                 // keys per wave-stage: 4 DMA rows x 4 keys
+constexpr int FD3_MAXNS = 64;              // splits per KV head (merge weights in LDS)
+constexpr int FD3_WST = 2 * 4 * 64 + 16;   // uint4 per wave-stage: K 4 KB, V 4 KB, mask 256 B
+
+template <int N>
+__device__ __forceinline__ void fd3_wait_vm() {   // s_waitcnt vmcnt(N) alone
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+typedef __attribute__((address_space(3))) void * fd3_lds_t;
+typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t fd3_lds_off(const void * p) {
+    return (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) p;
+}
+
+template <int G, int NW, int S>
+__global__ __launch_bounds__(64 * NW) void k_fattn_dec3(FaDecArgs p, int kps) {
+    constexpr int D = 128, LPK = 16, KPI = 4, NI = 4, NT = 64 * NW;
+    static_assert(S >= 2 && S <= 4, "ring depth");
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    extern __shared__ __align__(16) uint4 ring[];            // [NW][S][FD3_WST]
+    __shared__ float wm[NW][G], wl[NW][G];
+    __shared__ __align__(16) float wo[NW][G][D];
+    __shared__ int s_last;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c = lane % LPK, kq = lane / LPK;
+    const int hk = blockIdx.x % p.Hkv, split = blockIdx.x / p.Hkv;
+    const int Gt = p.H / p.Hkv, hb = hk * Gt;
+    const char * kb = p.k + (size_t) hk * p.k2 + c * 16;
+    const char * vb = p.v + (size_t) hk * p.v2 + c * 16;
+    const char * mrow = p.mask ? p.mask : p.k;               // (no mask: loads land unused)
+    const int ks0 = split * kps, nj = kps / (FD3_SK * NW);   // this wave's wave-stages
+    uint4 * my = ring + wave * S * FD3_WST;
+    unsigned long long * tr = blockIdx.x == 0 ? p.trace : nullptr;
+    MX_TRACE(tr, 0);
+    MX_TRACE_BLK(p.trace_blk, 0);
+
+    auto key0_of = [&](int j) { return ks0 + (j * NW + wave) * FD3_SK; };
+    // wave-stage j into slot j % S: 4 K rows-of-4, 4 V rows-of-4, the 16 mask values
+    // (lanes 0-7 one dword each; the others repeat lane 7's) — 9 DMA instructions
+    auto issue = [&](int j) {
+        uint4 * st = my + (j % S) * FD3_WST;
+        const int key0 = key0_of(j);
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+            const size_t r = (size_t) min(key0 + t * KPI + kq, p.n_kv - 1);
+            __builtin_amdgcn_global_load_lds(kb + r * p.k1, (fd3_lds_t) (st + t * 64), 16, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+            const size_t r = (size_t) min(key0 + t * KPI + kq, p.n_kv - 1);
+            __builtin_amdgcn_global_load_lds(vb + r * p.v1, (fd3_lds_t) (st + 256 + t * 64), 16, 0, 0);
+        }
+        const int mk = min(key0 + 2 * min(lane, 7), p.n_kv - 2);   // (n_kv even: fd3_cfg)
+        __builtin_amdgcn_global_load_lds(mrow + (size_t) mk * 2, (fd3_lds_t) (st + 512), 4, 0, 0);
+    };
+
+    float M[G], L[G], o[G][8];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        M[h] = -INFINITY; L[h] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[h][i] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < S - 1; ++j) if (j < nj) issue(j);
+    // q of the G heads, rounded to f16 (the K vec-dot type), loaded behind the ring's first
+    // stages (loaded first, its conversion held the DMA issue back one memory latency)
+    asm volatile("" ::: "memory");
+    h2v qh[G][4];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        const float * qp = (const float *) (p.q + (size_t) (hb + h) * p.q2) + 8 * c;
+        const float4 a = *(const float4 *) qp, b = *(const float4 *) (qp + 4);
+        qh[h][0] = h2v{(_Float16) a.x, (_Float16) a.y}; qh[h][1] = h2v{(_Float16) a.z, (_Float16) a.w};
+        qh[h][2] = h2v{(_Float16) b.x, (_Float16) b.y}; qh[h][3] = h2v{(_Float16) b.z, (_Float16) b.w};
+    }
+    MX_TRACE(tr, 1);
+    for (int j = 0; j < nj; ++j) {
+        if (j + S - 1 < nj) issue(j + S - 1);
+        const int rem = min(nj - 1 - j, S - 1);             // wave-stages issued after j
+        if (rem >= 3) fd3_wait_vm<27>();
+        else if (rem == 2) fd3_wait_vm<18>();
+        else if (rem == 1) fd3_wait_vm<9>();
+        else fd3_wait_vm<0>();
+        asm volatile("" ::: "memory");
+        if (j == 0) MX_TRACE(tr, 2);
+        const uint4 * st = my + (j % S) * FD3_WST;
+        const int key0 = key0_of(j);
+        // the wave-stage back from LDS in one batch (inline asm: through plain loads the
+        // compiler puts a vmcnt(0) for the LDS-DMA in front of them, draining the ring)
+        uint4 kr[NI], vr[NI];
+        float mk[NI];
+        {
+            v4u_t a0, a1, a2, a3, b0, b1, b2, b3;
+            uint32_t m0, m1, m2, m3;
+            const uint32_t ad = fd3_lds_off(st + lane), am = fd3_lds_off(st + 512) + 2 * kq;
+            asm volatile("ds_read_b128 %0, %12\n\tds_read_b128 %1, %12 offset:1024\n\tds_read_b128 %2, %12 offset:2048\n\t"
+                         "ds_read_b128 %3, %12 offset:3072\n\tds_read_b128 %4, %12 offset:4096\n\tds_read_b128 %5, %12 offset:5120\n\t"
+                         "ds_read_b128 %6, %12 offset:6144\n\tds_read_b128 %7, %12 offset:7168\n\tds_read_u16 %8, %13\n\t"
+                         "ds_read_u16 %9, %13 offset:8\n\tds_read_u16 %10, %13 offset:16\n\tds_read_u16 %11, %13 offset:24\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(b0), "=&v"(b1), "=&v"(b2), "=&v"(b3),
+                           "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(m3)
+                         : "v"(ad), "v"(am) : "memory");
+            const v4u_t av[NI] = {a0, a1, a2, a3}, bv[NI] = {b0, b1, b2, b3};
+            const uint32_t mr[NI] = {m0, m1, m2, m3};
+#pragma unroll
+            for (int t = 0; t < NI; ++t) {
+                kr[t] = make_uint4(av[t][0], av[t][1], av[t][2], av[t][3]);
+                vr[t] = make_uint4(bv[t][0], bv[t][1], bv[t][2], bv[t][3]);
+                const int key = key0 + t * KPI + kq;
+                mk[t] = key < p.n_kv ? (p.mask ? h2f((uint16_t) mr[t]) : 0.f) : -INFINITY;
+            }
+        }
+        float s[G][NI];
+#pragma unroll
+        for (int t = 0; t < NI; ++t)
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                float acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[h][0], 0.f, false);
+                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[h][1], acc, false);
+                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[h][2], acc, false);
+                acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[h][3], acc, false);
+                acc = dpp_sum_group<LPK>(acc);
+                s[h][t] = mk[t] == -INFINITY ? -INFINITY : (acc * p.scale + mk[t]) * 1.4426950408889634f;
+            }
+        float vf[NI][8];
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+            const uint32_t vw[4] = {vr[t].x, vr[t].y, vr[t].z, vr[t].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { vf[t][2 * i] = h2f((uint16_t) (vw[i] & 0xFFFF)); vf[t][2 * i + 1] = h2f((uint16_t) (vw[i] >> 16)); }
+        }
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            float mc = s[h][0];
+#pragma unroll
+            for (int t = 1; t < NI; ++t) mc = fmaxf(mc, s[h][t]);
+            mc = kr_max<LPK>(mc);
+            const float Mn = fmaxf(M[h], mc);
+            const float a = M[h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(M[h] - Mn);
+            float pr[NI], lc = 0.f;
+#pragma unroll
+            for (int t = 0; t < NI; ++t) { pr[t] = Mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[h][t] - Mn); lc += pr[t]; }
+            lc = kr_sum<LPK>(lc);
+            L[h] = L[h] * a + lc;
+            M[h] = Mn;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                float v = o[h][i] * a;
+#pragma unroll
+                for (int t = 0; t < NI; ++t) v += pr[t] * vf[t][i];
+                o[h][i] = v;
+            }
+        }
+    }
+    MX_TRACE(tr, 3);
+    // the NW waves' (O, M, L) -> this split's partial
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[h][i] = kr_sum<LPK>(o[h][i]);
+        if (lane == 0) { wm[wave][h] = M[h]; wl[wave][h] = L[h]; }
+        if (kq == 0) {
+            *(float4 *) &wo[wave][h][8 * c] = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
+            *(float4 *) &wo[wave][h][8 * c + 4] = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
+        }
+    }
+    __syncthreads();
+    constexpr int PW = G * (D + 2);
+    const int ns = p.nsplit;
+    float * part = p.part + ((size_t) hk * ns + split) * PW;
+    for (int i = tid; i < G * D; i += NT) {
+        const int h = i / D, d = i % D;
+        float Mw = wm[0][h];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) Mw = fmaxf(Mw, wm[w][h]);
+        float Lw = 0.f, O = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const float f = wm[w][h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(wm[w][h] - Mw);
+            Lw += wl[w][h] * f;
+            O += wo[w][h][d] * f;
+        }
+        if (ns == 1) {
+            ((float *) (p.dst + (size_t) (hb + h) * p.d1))[d] = Lw == 0.f ? 0.f : O / Lw;
+            continue;
+        }
+        // agent-scope (write-through) stores: visible to every XCD once completed
+        __hip_atomic_store(part + h * (D + 2) + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == 0) {   // (max, sum) as one 8-byte store: the merge reads them as one
+            const uint64_t ml = (uint64_t) __float_as_uint(Mw) | ((uint64_t) __float_as_uint(Lw) << 32);
+            __hip_atomic_store((uint64_t *) (part + h * (D + 2) + D), ml, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    MX_TRACE_BLK(p.trace_blk, 1);
+    if (ns == 1) return;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    MX_TRACE(tr, 4);
+    unsigned int * cnt = p.cnt + hk;
+    // relaxed count: the partials went out as agent-scope (write-through) atomic stores and
+    // have completed (waitcnt above); the merge reads them back with agent-scope loads. An
+    // acq_rel count adds an L2 writeback (buffer_wbl2) to every workgroup and an L2
+    // invalidate to the merging one, ~2 us of this launch's tail
+    if (tid == 0) s_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) (ns - 1);
+    __syncthreads();
+    if (!s_last) return;
+    // the merge in ONE memory round trip per 8 splits of a wave: wave w takes splits w,
+    // w + NW, ...; each lane loads (O of its 2 dimensions, max, sum) of every head for all of
+    // them at once, merges them under the wave's own max, and the NW wave results merge
+    // through LDS (a first version loaded the maxima, then the sums one split at a time,
+    // then O: ~30 dependent round trips, 33 us per launch at 16k keys)
+    const float * pb = p.part + (size_t) hk * ns * PW;
+    auto ld2 = [](const float * a) {      // two adjacent floats (8-byte aligned) in one agent-scope load
+        const uint64_t v = __hip_atomic_load((const uint64_t *) a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_float2(__uint_as_float((uint32_t) v), __uint_as_float((uint32_t) (v >> 32)));
+    };
+    float wmx[G], wls[G], acc[G][2];
+#pragma unroll
+    for (int h = 0; h < G; ++h) { wmx[h] = -INFINITY; wls[h] = 0.f; acc[h][0] = acc[h][1] = 0.f; }
+    for (int s0 = wave; s0 < ns; s0 += 8 * NW) {           // wave-uniform
+        float vo[8][G][2], vm[8][G], vl[8][G];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float * ps = pb + (size_t) min(s0 + u * NW, ns - 1) * PW;
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                const float2 o2 = ld2(ps + h * (D + 2) + 2 * lane), ml = ld2(ps + h * (D + 2) + D);
+                vo[u][h][0] = o2.x; vo[u][h][1] = o2.y;
+                vm[u][h] = ml.x; vl[u][h] = ml.y;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            float mn = wmx[h];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) if (s0 + u * NW < ns) mn = fmaxf(mn, vm[u][h]);
+            const float a = wmx[h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(wmx[h] - mn);
+            float l = wls[h] * a, o0 = acc[h][0] * a, o1 = acc[h][1] * a;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float f = s0 + u * NW < ns && vm[u][h] != -INFINITY ? __builtin_amdgcn_exp2f(vm[u][h] - mn) : 0.f;
+                l += f * vl[u][h];
+                o0 += f * vo[u][h][0];
+                o1 += f * vo[u][h][1];
+            }
+            wmx[h] = mn; wls[h] = l; acc[h][0] = o0; acc[h][1] = o1;
+        }
+    }
+    // (every wave has >= 1 split: ns >= NW is not guaranteed — empty waves carry -inf / 0)
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        if (lane == 0) { wm[wave][h] = wmx[h]; wl[wave][h] = wls[h]; }
+        *(float2 *) &wo[wave][h][2 * lane] = make_float2(acc[h][0], acc[h][1]);
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += NT) {
+        const int h = i / D, d = i % D;
+        float Mx = wm[0][h];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) Mx = fmaxf(Mx, wm[w][h]);
+        float Ls = 0.f, O = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const float f = wm[w][h] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(wm[w][h] - Mx);
+            Ls += wl[w][h] * f;
+            O += wo[w][h][d] * f;
+        }
+        ((float *) (p.dst + (size_t) (hb + h) * p.d1))[d] = Ls == 0.f ? 0.f : O / Ls;
+    }
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch / replay
+    MX_TRACE(tr, 5);
+    MX_TRACE_BLK(p.trace_blk, 1);                             // (the merging workgroup: its end after the merge)
+}
+
+// geometry: ~256 workgroups (one per CU), NS splits per KV head of kps keys each (a whole
+// number of 16 x NW-key workgroup stages). GGML_MI355X_FA_STREAM=0 / g_tune[34] = 1 off;
+// g_tune[35] = minimum cache length in units of 256 keys (default 2048 keys).
+struct Fd3Cfg { int ns = 0, kps = 0; };
+constexpr int FD3_NW = 4, FD3_S = 4;
+static Fd3Cfg fd3_cfg(const ggml_tensor * dst) {
+    static const bool off = [] { const char * v = getenv("GGML_MI355X_FA_STREAM"); return v && !strcmp(v, "0"); }();
+    const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
+    if (off || g_tune[34] == 1 || !fa_dec2_ok(dst)) return {};
+    if (k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16 || k->ne[0] != 128 || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1) return {};
+    if (m && (m->ne[3] != 1 || (uintptr_t) m->data % 4 || m->nb[1] % 4)) return {};
+    const int64_t n_kv = k->ne[1], Hkv = k->ne[2];
+    const int64_t min_kv = g_tune[35] > 0 ? (int64_t) g_tune[35] * 256 : 2048;
+    if (n_kv < min_kv || n_kv % 2 || Hkv > MX_FA_CNT / 2) return {};
+    const int64_t wst = FD3_SK * FD3_NW;
+    int64_t ns = std::max<int64_t>(1, 256 / Hkv);
+    ns = std::min<int64_t>({ns, FD3_MAXNS, mx_ceil_div(n_kv, wst)});
+    const int64_t kps = mx_ceil_div(mx_ceil_div(n_kv, ns), wst) * wst;
+    return {(int) mx_ceil_div(n_kv, kps), (int) kps};
+}
+
+static size_t fd3_scratch(const ggml_tensor * dst) {
+    const Fd3Cfg f = fd3_cfg(dst);
+    return f.ns ? (size_t) dst->src[0]->ne[2] * f.ns * (128 + 2) * sizeof(float) + 256 : 0;
+}
+
+static bool fd3_run(OpCtx & c, ggml_tensor * dst) {
+    const Fd3Cfg f = fd3_cfg(dst);
+    if (!f.ns) return false;
+    const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
+    FaDecArgs a{};
+    a.q = (const char *) q->data; a.q2 = q->nb[2];
+    a.k = (const char *) k->data; a.k1 = k->nb[1]; a.k2 = k->nb[2];
+    a.v = (const char *) v->data; a.v1 = v->nb[1]; a.v2 = v->nb[2];
+    if (m) a.mask = (const char *) m->data;
+    a.dst = (char *) dst->data; a.d1 = dst->nb[1];
+    a.n_q = 1; a.n_kv = (int) k->ne[1]; a.H = (int) q->ne[2]; a.Hkv = (int) k->ne[2]; a.ns_kv = 1;
+    a.scale = mx_op_param<float>(dst, 0);
+    a.nsplit = f.ns;
+    a.part = (float *) c.scratch->take(fd3_scratch(dst));
+    a.cnt = c.s->fa_cnt;
+    a.trace = mx_trace_slot(0);
+    a.trace_blk = mx_trace_blocks();
+    const int Gt = a.H / a.Hkv;
+    const dim3 grid((unsigned) (a.Hkv * f.ns));
+    constexpr size_t lds = (size_t) FD3_NW * FD3_S * FD3_WST * 16;
+    MX_KLOG("fattn_dec3 D=128 G=%d ns=%d kps=%d n_kv=%d H=%d Hkv=%d", Gt, f.ns, f.kps, a.n_kv, a.H, a.Hkv);
+#define F3(GG) if (Gt == GG) { \
+        MX_LDS_OPTIN((k_fattn_dec3<GG, FD3_NW, FD3_S>), lds); \
+        k_fattn_dec3<GG, FD3_NW, FD3_S><<<grid, 64 * FD3_NW, lds, c.st>>>(a, f.kps); return true; }
+    F3(1) F3(2) F3(4) F3(8)
+#undef F3
+    return false;
 }
 
 // ---------------------------------------------------------------------------
@@ -943,14 +1294,10 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         a.pf[r] = c.s->pf_ptr[r]; a.pf_eighth[r] = c.s->pf_len[r] / 8; a.pf_lines[r] = (unsigned) (c.s->pf_take[r] / 128);
     }
     if (a.pf_n) grid.y = 1 + (unsigned) mx_ceil_div(640, H);   // ~640 prefetch workgroups of 4 waves
-    static const bool attr = [] {
-        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<128>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
-        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<64>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
-        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<128, 16, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
-        HIP_CHECK(hipFuncSetAttribute((const void *) k_attn_nofa_dec<128, 4, 4, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, NF_MAX_KV * 4));
-        return true;
-    }();
-    (void) attr;
+    MX_LDS_OPTIN(k_attn_nofa_dec<128>, NF_MAX_KV * 4);
+    MX_LDS_OPTIN(k_attn_nofa_dec<64>, NF_MAX_KV * 4);
+    MX_LDS_OPTIN((k_attn_nofa_dec<128, 16, 16>), NF_MAX_KV * 4);
+    MX_LDS_OPTIN((k_attn_nofa_dec<128, 4, 4, 1024>), NF_MAX_KV * 4);
     // one pass over a cache of <= 256 keys with V and the mask loaded up front (D 128);
     // g_tune[2] = 10: the 256-thread one-pass form, 9: the round-3 two-pass form (A/B)
     if (D == 128 && n_kv <= 256 && n_kv % 64 == 0 && g_tune[2] != 9 && g_tune[2] != 10) k_attn_nofa_dec<128, 4, 4, 1024><<<grid, 1024, lds, c.st>>>(a);

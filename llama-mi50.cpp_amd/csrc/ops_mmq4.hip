@@ -1013,11 +1013,7 @@ static bool m4_plain_ok(int64_t K) { return m4_all() || K >= 8192; }
 template <int QTA, int QTB, int TT, int EPI, int X = M4_XDEF>
 static void m4_kernel_x(hipStream_t st, const M4Args & a, dim3 g) {
     constexpr int lds = m4_slots<X>() * 32 * TT * 256;
-    static const bool attr = [] {
-        HIP_CHECK(hipFuncSetAttribute((const void *) k_mmq4<QTA, QTB, TT, EPI, X>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        return true;
-    }();
-    (void) attr;
+    MX_LDS_OPTIN((k_mmq4<QTA, QTB, TT, EPI, X>), lds);
     k_mmq4<QTA, QTB, TT, EPI, X><<<g, 64 * M4_WAVES, lds, st>>>(a);
 }
 
@@ -1172,11 +1168,7 @@ bool mmq4_group(OpCtx & c, ggml_tensor * const * mms, int n, const _Float16 * xa
 
 template <int QT, int X>
 static void m5_launch(hipStream_t st, const M4Args & a, dim3 g) {
-    static const bool attr = [] {
-        HIP_CHECK(hipFuncSetAttribute((const void *) k_mmq5_glu<QT, X>, hipFuncAttributeMaxDynamicSharedMemorySize, M5_LDS));
-        return true;
-    }();
-    (void) attr;
+    MX_LDS_OPTIN((k_mmq5_glu<QT, X>), M5_LDS);
     k_mmq5_glu<QT, X><<<g, 64 * M5_WAVES, M5_LDS, st>>>(a);
 }
 

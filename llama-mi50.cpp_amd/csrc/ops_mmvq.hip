@@ -330,16 +330,21 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up,
     if (glu->type != GGML_TYPE_F32 || glu->nb[0] != 4 || !mx_are_same_shape(glu, gate)) return false;
     XStage xs;
     if (tensor_is_split(wg) || tensor_is_split(wu)) {
-        // round 4, row-split gate and up whose slices (the same row ranges) all lie on this
-        // GPU: one SwiGLU GEMV per slice on this stream, each writing its rows of the GLU and
-        // of its q8 copy (the down projection's input) — as the unsplit decode does
+        // row-split gate and up (the same row ranges): one SwiGLU GEMV per slice, each writing
+        // its rows of the GLU and of its q8 copy (the down projection's input) — as the
+        // unsplit decode does. Round 4 ran them only when every slice was this GPU's; round 5
+        // launches each on its own device's stream (split_fork / split_join), reading x and
+        // writing the rows on the main device through peer access
         void * dg[MX_MAX_DEVICES], * du[MX_MAX_DEVICES];
         int64_t lg[MX_MAX_DEVICES], hg[MX_MAX_DEVICES], lu[MX_MAX_DEVICES], hu[MX_MAX_DEVICES];
-        const int ns = split_local_slices(c.s, wg, dg, lg, hg);
-        if (!ns || ns != split_local_slices(c.s, wu, du, lu, hu) || !g_gemv2 || !mx_is_contiguous(glu)) return false;
+        int vg[MX_MAX_DEVICES], vu[MX_MAX_DEVICES];
+        const int ns = split_slices(c.s, wg, dg, lg, hg, vg);
+        if (!ns || ns != split_slices(c.s, wu, du, lu, hu, vu) || !g_gemv2 || !mx_is_contiguous(glu)) return false;
         ggml_tensor ws[2][MX_MAX_DEVICES], gv[MX_MAX_DEVICES];
+        int remote = 0;
         for (int k = 0; k < ns; ++k) {
-            if (lg[k] != lu[k] || hg[k] != hu[k] || lg[k] % 32) return false;
+            if (lg[k] != lu[k] || hg[k] != hu[k] || vg[k] != vu[k] || lg[k] % 32) return false;
+            remote += !split_on_main(c.s, wg, vg[k]);
             const int64_t rows = hg[k] - lg[k];
             for (int t = 0; t < 2; ++t) {
                 ggml_tensor & w = ws[t][k];
@@ -353,15 +358,19 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up,
         if (!gemv2_stage(c, x, {glu}, {}, &xs)) return false;
         ActQ * q8 = wg->ne[1] % 32 == 0 ? act_cache_alloc(c.s, glu) : nullptr;
         if (q8 && xs.q8 == q8->q) q8 = nullptr;
-        MX_KLOG("glu_split M=%lld K=%lld slices=%d q8o=%d", (long long) wg->ne[1], (long long) wg->ne[0], ns, q8 != nullptr);
+        MX_KLOG("glu_split M=%lld K=%lld slices=%d remote=%d q8o=%d", (long long) wg->ne[1], (long long) wg->ne[0], ns, remote, q8 != nullptr);
         for (int k = 0; k < ns; ++k) {
             ActQ qs{};
             if (q8) { qs = *q8; qs.q += lg[k]; qs.d += lg[k] / 32; qs.s += lg[k] / 32; }
-            gemv2_launch(c, &ws[0][k], &ws[1][k], xs, (float *) glu->data + lg[k], nullptr, q8 ? &qs : nullptr);
+            if (split_on_main(c.s, wg, vg[k])) { gemv2_launch(c, &ws[0][k], &ws[1][k], xs, (float *) glu->data + lg[k], nullptr, q8 ? &qs : nullptr); continue; }
+            OpCtx dc = split_fork(c, vg[k]);
+            gemv2_launch(dc, &ws[0][k], &ws[1][k], xs, (float *) glu->data + lg[k], nullptr, q8 ? &qs : nullptr);
         }
+        for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, wg, vg[k])) split_join(c, vg[k]);
+        HIP_CHECK(hipSetDevice(c.s->device));
         return true;
     }
-    if (g_gemv2 && gemv2_ok(wg, x, glu) && gemv2_stage(c, x, {glu}, {}, &xs)) {
+    if (g_gemv2 && gemv2_ok(wg, x, glu) && gemv2_stage(c, x, {glu}, {}, &xs, 2)) {
         // the q8 form of the output feeds the down projection's prologue (act cache)
         ActQ * q8 = (wg->ne[1] % 32 == 0 && mx_is_contiguous(glu)) ? act_cache_alloc(c.s, glu) : nullptr;
         if (q8 && xs.q8 == q8->q) q8 = nullptr;
@@ -383,16 +392,19 @@ bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, 
     if (res->nb[0] != 4 || add->nb[0] != 4 || w->ne[2] != 1 || w->ne[3] != 1) return false;
     XStage xs;
     if (tensor_is_split(w)) {
-        // round 4, row-split weights whose slices all lie on this GPU (split.cpp): one residual
-        // GEMV per slice on this stream, each writing its rows of the sum — the unsplit
-        // decode's fused launch instead of per-slice GEMVs + an ADD pass
+        // row-split weights: one residual GEMV per slice, each writing its rows of the sum —
+        // the unsplit decode's fused launch instead of per-slice GEMVs + an ADD pass; on the
+        // slice's own device's stream when it is not this GPU's (as mmvq_fused_glu)
         void * sd[MX_MAX_DEVICES];
         int64_t lo[MX_MAX_DEVICES], hi[MX_MAX_DEVICES];
-        const int ns = split_local_slices(c.s, w, sd, lo, hi);
+        int dv[MX_MAX_DEVICES];
+        const int ns = split_slices(c.s, w, sd, lo, hi, dv);
         if (!ns || !g_gemv2 || !mx_is_contiguous(res) || !mx_is_contiguous(add)) return false;
         ggml_tensor ws[MX_MAX_DEVICES], av[MX_MAX_DEVICES];
+        int remote = 0;
         for (int k = 0; k < ns; ++k) {
             const int64_t rows = hi[k] - lo[k];
+            remote += !split_on_main(c.s, w, dv[k]);
             ws[k] = *w; ws[k].ne[1] = rows; ws[k].nb[2] = ws[k].nb[3] = ws[k].nb[1] * rows; ws[k].data = sd[k];
             ws[k].buffer = nullptr; ws[k].extra = nullptr; ws[k].view_src = nullptr;
             av[k] = *add; av[k].ne[0] = rows; av[k].data = (char *) add->data + lo[k] * 4; av[k].buffer = nullptr; av[k].view_src = nullptr;
@@ -400,9 +412,14 @@ bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, 
             if (!gemv2_ok(&ws[k], x, &av[k])) return false;
         }
         if (!gemv2_stage(c, x, {add}, {res}, &xs)) return false;
-        MX_KLOG("mm_split_add M=%lld K=%lld slices=%d", (long long) w->ne[1], (long long) w->ne[0], ns);
-        for (int k = 0; k < ns; ++k)
-            gemv2_launch(c, &ws[k], nullptr, xs, (float *) add->data + lo[k], (const float *) res->data + lo[k]);
+        MX_KLOG("mm_split_add M=%lld K=%lld slices=%d remote=%d", (long long) w->ne[1], (long long) w->ne[0], ns, remote);
+        for (int k = 0; k < ns; ++k) {
+            if (split_on_main(c.s, w, dv[k])) { gemv2_launch(c, &ws[k], nullptr, xs, (float *) add->data + lo[k], (const float *) res->data + lo[k]); continue; }
+            OpCtx dc = split_fork(c, dv[k]);
+            gemv2_launch(dc, &ws[k], nullptr, xs, (float *) add->data + lo[k], (const float *) res->data + lo[k]);
+        }
+        for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, w, dv[k])) split_join(c, dv[k]);
+        HIP_CHECK(hipSetDevice(c.s->device));
         return true;
     }
     if (g_gemv2 && gemv2_ok(w, x, add) && mx_is_contiguous(res)) {

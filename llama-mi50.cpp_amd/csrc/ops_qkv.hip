@@ -472,7 +472,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     GEOS(GGML_TYPE_Q4_K, GGML_TYPE_Q4_K, XS_NORM) GEOS(GGML_TYPE_Q4_K, GGML_TYPE_Q6_K, XS_NORM)
     if (!kern) return 0;
     if (!fused_io_ok({rq, sk, sv}, {rq->src[1], rq->src[2], kix, vix})) return 0;
-    if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs)) return 0;
+    if (!gemv2_stage(c, x, {rq, sk, sv}, {}, &p.xs, 3)) return 0;
     const int mode = gemv_mode(p.xs, p.K, 0);
     if (mode != XS_NORM) {   // the fused block normally follows attn_norm; other sources
 #define QKV(TA, TK, TV) if (ta == TA && tk == TK && tv == TV) kern = mode == XS_Q8 ? k_qkv_rope_store<TA, TK, TV, XS_Q8, 16, 2, 32, 2> : \

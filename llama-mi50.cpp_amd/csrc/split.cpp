@@ -224,11 +224,22 @@ static SliceState & slice_state(const Stream * main, int main_l, int d) {
 // the main device's GPU (virtual devices): the fork / join events make the slice streams
 // part of the capture. Across GPUs a capture would have to span devices, which this
 // backend does not rely on: those graphs run eagerly. GGML_MI355X_SPLIT_GRAPHS=0 turns
-// the capture off, =2 tries it across GPUs as well (experiment).
+// the capture off, =2 tries it across GPUs as well (experiment) — but never when a slice
+// device lacks peer access to the main one: its staging copies (hipMemcpyPeerAsync) are
+// not captured into a graph, they would run once at capture time and never on replay.
 bool split_graph_capturable(int main_hip) {
     static const int mode = [] { const char * v = getenv("GGML_MI355X_SPLIT_GRAPHS"); return v ? atoi(v) : 1; }();
     if (mode == 0) return false;
-    if (mode == 2) return true;
+    if (mode == 2) {
+        for (int d = 0; d < mx_dev_count(); ++d) {
+            const int hip = mx_dev_hip(d);
+            if (hip != main_hip && !mx_peer_enabled(hip, main_hip)) {
+                MX_KLOG("split_graphs=2 refused: device %d has no peer access to %d (peer copies)", hip, main_hip);
+                return false;
+            }
+        }
+        return true;
+    }
     for (int d = 0; d < mx_dev_count(); ++d)
         if (mx_dev_hip(d) != main_hip) return false;
     return true;
@@ -259,96 +270,184 @@ int split_local_slices(const Stream * s, const ggml_tensor * w, void ** data, in
     return n;
 }
 
-void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) {
-    const ggml_tensor * w = dst->src[0];
-    const ggml_tensor * x = dst->src[1];
+// Round 5: the fused per-slice decode launches (SwiGLU, GEMV + residual: ops_mmvq.hip) on
+// every slice's own device — not only when all slices are this GPU's (split_local_slices).
+// A slice device with peer access reads x (or its q8 copy) from the main device and
+// writes its rows of the output there directly; the launches fork off the main stream and
+// join back by the same per-(main stream, device) events as op_mul_mat_split.
+int split_slices(const Stream * s, const ggml_tensor * w, void ** data, int64_t * lo, int64_t * hi, int * dev) {
+    if (!tensor_is_split(w) || !w->extra) return 0;
     const SplitExtra * e = (const SplitExtra *) w->extra;
-    MX_ASSERT(e && x->type == GGML_TYPE_F32 && mx_is_contiguous(x) && mx_is_contiguous(dst) && dst->type == GGML_TYPE_F32);
-    MX_ASSERT(x->ne[2] * x->ne[3] == dst->ne[2] * dst->ne[3]);
+    if (mx_dev_hip(split_main_device(w->buffer->buft)) != s->device) return 0;
+    int n = 0;
+    for (int d = 0; d < mx_dev_count(); ++d) {
+        if (e->hi[d] == e->lo[d]) continue;
+        const int hip = mx_dev_hip(d);
+        if (!mx_peer_enabled(hip, s->device)) return 0;      // (same GPU: mx_peer_enabled(h, h))
+        data[n] = e->data[d]; lo[n] = e->lo[d]; hi[n] = e->hi[d]; dev[n] = d;
+        ++n;
+    }
+    return n;
+}
+
+// GGML_MI355X_FORCE_PEER makes the other logical devices of this GPU behave as separate
+// GPUs; the main device's own slice stays on the main stream, as it would on real hardware
+bool split_on_main(const Stream * s, const ggml_tensor * w, int dev) {
+    return mx_dev_hip(dev) == s->device && (!mx_force_peer() || dev == split_main_device(w->buffer->buft));
+}
+
+OpCtx split_fork(OpCtx & c, int dev) {
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    int main_l = 0;
+    for (int d = 0; d < mx_dev_count(); ++d) if (mx_dev_hip(d) == c.s->device) { main_l = d; break; }
+    SliceState & st = slice_state(c.s, main_l, dev);
+    Stream * ds = mx_aux_stream(dev);
+    HIP_CHECK(hipSetDevice(c.s->device));
+    HIP_CHECK(hipEventRecord(st.ev_main, c.st));
+    HIP_CHECK(hipSetDevice(mx_dev_hip(dev)));
+    HIP_CHECK(hipStreamWaitEvent(ds->stream, st.ev_main, 0));
+    return OpCtx{ds, ds->stream, &ds->scratch};
+}
+
+void split_join(OpCtx & c, int dev) {
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    int main_l = 0;
+    for (int d = 0; d < mx_dev_count(); ++d) if (mx_dev_hip(d) == c.s->device) { main_l = d; break; }
+    SliceState & st = slice_state(c.s, main_l, dev);
+    Stream * ds = mx_aux_stream(dev);
+    HIP_CHECK(hipSetDevice(mx_dev_hip(dev)));
+    HIP_CHECK(hipEventRecord(st.ev_done, ds->stream));
+    HIP_CHECK(hipSetDevice(c.s->device));
+    HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));
+}
+
+// dsts: 1-3 MUL_MATs sharing src1 whose src0 are row-split alike (q / k / v). Every slice
+// device's stream forks off the main stream once, runs its slices of all of them, and joins
+// back once (round 4 forked and joined per matrix and per device in turn, so the slices of
+// one matrix ran one device after another: -ts 1,1,1,1 under FORCE_PEER measured 0.22x).
+void op_mul_mat_split_n(OpCtx & c, ggml_tensor * const * dsts, int n) {
+    MX_ASSERT(n >= 1 && n <= 3);
+    const ggml_tensor * w0 = dsts[0]->src[0];
+    const ggml_tensor * x = dsts[0]->src[1];
+    const SplitExtra * e0 = (const SplitExtra *) w0->extra;
+    for (int k = 0; k < n; ++k) {
+        const ggml_tensor * dst = dsts[k];
+        MX_ASSERT(dst->src[1] == x && dst->src[0]->extra && mx_is_contiguous(dst) && dst->type == GGML_TYPE_F32);
+        const SplitExtra * e = (const SplitExtra *) dst->src[0]->extra;
+        for (int d = 0; d < mx_dev_count(); ++d) MX_ASSERT((e->hi[d] == e->lo[d]) == (e0->hi[d] == e0->lo[d]));
+    }
+    MX_ASSERT(e0 && x->type == GGML_TYPE_F32 && mx_is_contiguous(x));
+    MX_ASSERT(x->ne[2] * x->ne[3] == dsts[0]->ne[2] * dsts[0]->ne[3]);
     const int64_t N = x->ne[1] * x->ne[2] * x->ne[3];
     const size_t xb = mx_nbytes(x);
     const int main_hip = c.s->device;
-    const int main_l = split_main_device(w->buffer->buft);
+    const int main_l = split_main_device(w0->buffer->buft);
     MX_ASSERT(mx_dev_hip(main_l) == main_hip);
     std::lock_guard<std::mutex> lk(g_split_mu);
     const bool force = mx_force_peer();
-    MX_KLOG("mm_split M=%d K=%d N=%d devices=%d peer=%d direct=%d", (int) w->ne[1], (int) w->ne[0], (int) N, mx_dev_count(), (int) force,
-            (int) mx_peer_enabled(main_hip, main_hip));
-    // src1 is ready on the main stream at this point
+    for (int k = 0; k < n; ++k)
+        MX_KLOG("mm_split M=%d K=%d N=%d devices=%d peer=%d direct=%d group=%d", (int) dsts[k]->src[0]->ne[1], (int) x->ne[0], (int) N,
+                mx_dev_count(), (int) force, (int) mx_peer_enabled(main_hip, main_hip), n);
+    struct Plan { int d, hip; bool local, direct; Stream * ds; };
+    Plan plan[MX_MAX_DEVICES];
+    int np = 0;
+    // fork: src1 is ready on the main stream at this point; every slice stream waits for it
     for (int d = 0; d < mx_dev_count(); ++d) {
-        const int64_t rows = e->hi[d] - e->lo[d];
-        if (rows == 0) continue;
-        SliceState & st = slice_state(c.s, main_l, d);
+        if (e0->hi[d] == e0->lo[d]) continue;
         const int hip = mx_dev_hip(d);
-        const bool cross = hip != main_hip || force;
+        // a slice on the main GPU itself runs on the main stream (no fork / join: each is a
+        // cross-queue barrier in a captured graph); other GPUs' slices — and under
+        // GGML_MI355X_FORCE_PEER the other logical devices' — on the slice device's stream
+        const bool cross = hip != main_hip || (force && d != main_l);
         const bool direct = !cross || mx_peer_enabled(hip, main_hip);   // slice device reaches main's memory itself
-        // a slice on the main GPU itself (virtual devices) runs on the main stream: no fork /
-        // join (each is a cross-queue barrier in a captured graph); other GPUs' slices (and
-        // GGML_MI355X_FORCE_PEER runs) fork onto the slice device's stream
         const bool local = !cross && direct;
-        Stream * ds = local ? c.s : mx_aux_stream(d);
-        if (!local) {
-            HIP_CHECK(hipSetDevice(main_hip));
-            HIP_CHECK(hipEventRecord(st.ev_main, c.st));
-            HIP_CHECK(hipSetDevice(hip));
-            HIP_CHECK(hipStreamWaitEvent(ds->stream, st.ev_main, 0));
-        }
-        ggml_tensor ws = *w, xs = *x, ys = *dst;
-        ws.ne[1] = rows; ws.nb[2] = ws.nb[3] = ws.nb[1] * rows; ws.data = e->data[d]; ws.buffer = nullptr; ws.extra = nullptr;
-        ws.view_src = nullptr;
-        xs.buffer = nullptr; xs.view_src = nullptr;
-        ys.ne[0] = rows; ys.buffer = nullptr; ys.view_src = nullptr;
-        ys.src[0] = &ws; ys.src[1] = &xs;
-        void * yd = nullptr;
-        if (direct) {
-            // round 4: the slice kernel reads src1 where it lies and writes its rows of every
-            // column straight into dst (over xGMI when the devices differ: peer access is on
-            // between them) — no staging copies, one kernel per device and matrix
-            ys.data = (char *) dst->data + e->lo[d] * 4;
-            if (N == 1) { ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[3] = ys.nb[1]; }   // one column: contiguous
-        } else {
-            // no peer access (GGML_MI355X_NO_PEER or no link): src1 by peer copy to the slice
-            // device, the partial dst there, one contiguous peer copy back into a staging
-            // buffer on main, scattered into dst on the main stream
-            void * xd = grow(st.x, st.xcap, hip, xb);
-            yd = grow(st.y, st.ycap, hip, (size_t) rows * N * 4);
-            HIP_CHECK(hipSetDevice(hip));
-            // (one GPU: a plain device copy — a peer copy between a device and itself is not
-            // captured into a graph, it runs once at capture time)
-            if (hip == main_hip) HIP_CHECK(hipMemcpyAsync(xd, x->data, xb, hipMemcpyDeviceToDevice, ds->stream));
-            else HIP_CHECK(hipMemcpyPeerAsync(xd, hip, x->data, main_hip, xb, ds->stream));
-            xs.data = xd;
-            ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[1] * ys.ne[1]; ys.nb[3] = ys.nb[2] * ys.ne[2];
-            ys.data = yd;
-        }
-        if (local) {   // the main stream's buffers are sized for the graph's nodes, this slice included
-            c.scratch->reset();
-            op_mul_mat(c, &ys);
-            continue;
-        }
-        stream_reserve_node(ds, &ys);
-        OpCtx dc{ds, ds->stream, &ds->scratch};
-        ds->scratch.reset();
-        act_cache_reset(ds);
+        Plan & pl = plan[np++];
+        pl = Plan{d, hip, local, direct, local ? c.s : mx_aux_stream(d)};
+        if (local) continue;
+        SliceState & st = slice_state(c.s, main_l, d);
+        HIP_CHECK(hipSetDevice(main_hip));
+        HIP_CHECK(hipEventRecord(st.ev_main, c.st));
         HIP_CHECK(hipSetDevice(hip));
-        op_mul_mat(dc, &ys);
-        if (direct) {
-            HIP_CHECK(hipEventRecord(st.ev_done, ds->stream));
-            HIP_CHECK(hipSetDevice(main_hip));
-            HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));
-        } else {
-            void * gm = grow(st.g, st.gcap, main_hip, (size_t) rows * N * 4);
-            HIP_CHECK(hipSetDevice(hip));
-            if (hip == main_hip) HIP_CHECK(hipMemcpyAsync(gm, yd, (size_t) rows * N * 4, hipMemcpyDeviceToDevice, ds->stream));
-            else HIP_CHECK(hipMemcpyPeerAsync(gm, main_hip, yd, hip, (size_t) rows * N * 4, ds->stream));
-            HIP_CHECK(hipEventRecord(st.ev_done, ds->stream));
-            HIP_CHECK(hipSetDevice(main_hip));
-            HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));
-            HIP_CHECK(hipMemcpy2DAsync((char *) dst->data + e->lo[d] * 4, dst->nb[1], gm, (size_t) rows * 4, (size_t) rows * 4, N,
+        HIP_CHECK(hipStreamWaitEvent(pl.ds->stream, st.ev_main, 0));
+    }
+    // the slices: each device's stream runs its rows of every matrix
+    for (int pi = 0; pi < np; ++pi) {
+        const Plan & pl = plan[pi];
+        SliceState & st = slice_state(c.s, main_l, pl.d);
+        Stream * ds = pl.ds;
+        if (!pl.local) { ds->scratch.reset(); act_cache_reset(ds); }   // (the slices share x: its q8 copy too)
+        void * xd = nullptr;
+        for (int k = 0; k < n; ++k) {
+            ggml_tensor * dst = dsts[k];
+            const ggml_tensor * w = dst->src[0];
+            const SplitExtra * e = (const SplitExtra *) w->extra;
+            const int64_t rows = e->hi[pl.d] - e->lo[pl.d];
+            ggml_tensor ws = *w, xs = *x, ys = *dst;
+            ws.ne[1] = rows; ws.nb[2] = ws.nb[3] = ws.nb[1] * rows; ws.data = e->data[pl.d]; ws.buffer = nullptr; ws.extra = nullptr;
+            ws.view_src = nullptr;
+            xs.buffer = nullptr; xs.view_src = nullptr;
+            ys.ne[0] = rows; ys.buffer = nullptr; ys.view_src = nullptr;
+            ys.src[0] = &ws; ys.src[1] = &xs;
+            void * yd = nullptr;
+            if (pl.direct) {
+                // the slice kernel reads src1 where it lies and writes its rows of every column
+                // straight into dst (over xGMI when the devices differ: peer access is on
+                // between them) — no staging copies
+                ys.data = (char *) dst->data + e->lo[pl.d] * 4;
+                if (N == 1) { ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[3] = ys.nb[1]; }   // one column: contiguous
+            } else {
+                // no peer access (GGML_MI355X_NO_PEER or no link): src1 by peer copy to the
+                // slice device (once per group), the partial dst there, one contiguous peer copy
+                // back into a staging buffer on main, scattered into dst on the main stream
+                MX_ASSERT(n == 1);
+                xd = grow(st.x, st.xcap, pl.hip, xb);
+                yd = grow(st.y, st.ycap, pl.hip, (size_t) rows * N * 4);
+                HIP_CHECK(hipSetDevice(pl.hip));
+                // (one GPU: a plain device copy — a peer copy between a device and itself is
+                // not captured into a graph, it runs once at capture time)
+                if (pl.hip == main_hip) HIP_CHECK(hipMemcpyAsync(xd, x->data, xb, hipMemcpyDeviceToDevice, ds->stream));
+                else HIP_CHECK(hipMemcpyPeerAsync(xd, pl.hip, x->data, main_hip, xb, ds->stream));
+                xs.data = xd;
+                ys.nb[1] = (size_t) rows * 4; ys.nb[2] = ys.nb[1] * ys.ne[1]; ys.nb[3] = ys.nb[2] * ys.ne[2];
+                ys.data = yd;
+            }
+            if (pl.local) {   // the main stream's buffers are sized for the graph's nodes, this slice included
+                c.scratch->reset();
+                op_mul_mat(c, &ys);
+                continue;
+            }
+            stream_reserve_node(ds, &ys);
+            OpCtx dc{ds, ds->stream, &ds->scratch};
+            ds->scratch.reset();
+            HIP_CHECK(hipSetDevice(pl.hip));
+            op_mul_mat(dc, &ys);
+            if (!pl.direct) {
+                void * gm = grow(st.g, st.gcap, main_hip, (size_t) rows * N * 4);
+                if (pl.hip == main_hip) HIP_CHECK(hipMemcpyAsync(gm, yd, (size_t) rows * N * 4, hipMemcpyDeviceToDevice, ds->stream));
+                else HIP_CHECK(hipMemcpyPeerAsync(gm, main_hip, yd, pl.hip, (size_t) rows * N * 4, ds->stream));
+            }
+        }
+    }
+    // join: the main stream waits for every slice stream once
+    for (int pi = 0; pi < np; ++pi) {
+        const Plan & pl = plan[pi];
+        if (pl.local) continue;
+        SliceState & st = slice_state(c.s, main_l, pl.d);
+        HIP_CHECK(hipSetDevice(pl.hip));
+        HIP_CHECK(hipEventRecord(st.ev_done, pl.ds->stream));
+        HIP_CHECK(hipSetDevice(main_hip));
+        HIP_CHECK(hipStreamWaitEvent(c.st, st.ev_done, 0));
+        if (!pl.direct) {   // (n == 1) the staged rows into dst
+            const ggml_tensor * dst = dsts[0];
+            const SplitExtra * e = (const SplitExtra *) dst->src[0]->extra;
+            const int64_t rows = e->hi[pl.d] - e->lo[pl.d];
+            HIP_CHECK(hipMemcpy2DAsync((char *) dst->data + e->lo[pl.d] * 4, dst->nb[1], st.g, (size_t) rows * 4, (size_t) rows * 4, N,
                                        hipMemcpyDeviceToDevice, c.st));
         }
     }
     HIP_CHECK(hipSetDevice(main_hip));
 }
+
+void op_mul_mat_split(OpCtx & c, ggml_tensor * dst) { op_mul_mat_split_n(c, &dst, 1); }
 
 }  // namespace mx

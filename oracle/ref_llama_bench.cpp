@@ -70,6 +70,7 @@ int main(int argc, char ** argv) {
     int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0, incremental = 0, last = 0, n_batch = 0, n_ubatch = 0, reps = 1;
     int ctk = -1;   // K/V cache type (ggml_type id), -1: default f16
     int depth = 0;
+    int prefix = 0;                    // logits mode, incremental: the first N tokens as one batch (no logits)
     std::string sm = "layer";          // -sm none|layer|row
     std::vector<float> ts;             // -ts a,b,...
     int mg = 0;
@@ -87,6 +88,7 @@ int main(int argc, char ** argv) {
         else if (a == "--logits") { tok_in = next(); logits_out = next(); }
         else if (a == "--incremental") incremental = 1;   // logits mode: one token per llama_decode
         else if (a == "--last") last = std::stoi(next());
+        else if (a == "--prefix") prefix = std::stoi(next());
         else if (a == "-b") n_batch = std::stoi(next());
         else if (a == "-ub") n_ubatch = std::stoi(next());
         else if (a == "-r") reps = std::max(1, std::stoi(next()));
@@ -147,14 +149,19 @@ int main(int argc, char ** argv) {
 
     if (!toks.empty() && incremental) {
         FILE * f = fopen(logits_out.c_str(), "wb");
-        for (size_t i = 0; i < toks.size(); ++i) {
+        size_t i0 = 0;
+        if (prefix > 0 && (size_t) prefix < toks.size()) {   // a cache of `prefix` positions, then one token at a time
+            if (llama_decode(ctx, llama_batch_get_one(toks.data(), prefix)) != 0) { fprintf(stderr, "decode failed\n"); return 1; }
+            i0 = (size_t) prefix;
+        }
+        for (size_t i = i0; i < toks.size(); ++i) {
             llama_token t = toks[i];
             if (llama_decode(ctx, llama_batch_get_one(&t, 1)) != 0) { fprintf(stderr, "decode failed\n"); return 1; }
             llama_synchronize(ctx);
             fwrite(llama_get_logits_ith(ctx, -1), sizeof(float), n_vocab, f);
         }
         fclose(f);
-        printf("{\"n_tokens\": %zu, \"n_vocab\": %d, \"incremental\": 1}\n", toks.size(), n_vocab);
+        printf("{\"n_tokens\": %zu, \"n_vocab\": %d, \"incremental\": 1, \"prefix\": %d}\n", toks.size() - i0, n_vocab, (int) i0);
     } else if (!toks.empty()) {
         llama_batch b = llama_batch_init((int) toks.size(), 0, 1);
         const size_t first = last > 0 && (size_t) last < toks.size() ? toks.size() - last : 0;

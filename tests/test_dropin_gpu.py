@@ -10,6 +10,7 @@ full graphs); prefill (one ubatch, MFMA GEMM path) and incremental d
 Synthetic GGUFs come from tools/gguf_synth.py (random weights, seeded)."""
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -140,39 +141,55 @@ def test_layer_split_handoff_cpy_tensor_async(tmp_path):
     assert '"mismatches": 0' in r.stdout and "MI355X" in r.stdout, r.stdout
 
 
-@pytest.mark.parametrize("incremental,no_peer,force_peer", [(False, False, True), (True, False, True), (True, True, True),
-                                                          (False, False, False), (True, False, False)])
-def test_dropin_row_split(ggufs, tmp_path, incremental, no_peer, force_peer):
-    """llama -sm row -ts 1,1: libllama puts every matrix in the backend's split buffer type
-    (proc ggml_backend_split_buffer_type), rows halved over two devices — here two logical
-    devices of the one MI355X (GGML_MI355X_VIRTUAL_DEVICES=2) — and every MUL_MAT runs its
-    slices on both and gathers them (split.cpp). Logits against the reference CPU backend.
-    force_peer False: the slices are local to the GPU, so decode's gate/up/SwiGLU and
-    MUL_MAT -> ADD run as per-slice fused GEMVs (klog glu_split / mm_split_add)."""
+@pytest.mark.parametrize("incremental,no_peer,force_peer,ts", [(False, False, True, "1,1"), (True, False, True, "1,1"),
+                                                             (True, True, True, "1,1"), (False, False, False, "1,1"),
+                                                             (True, False, False, "1,1"), (True, False, True, "1,1,1,1"),
+                                                             (False, False, True, "1,1,1,1"), (True, False, False, "1,1,1,1"),
+                                                             (True, False, True, "3,1")])
+def test_dropin_row_split(ggufs, tmp_path, incremental, no_peer, force_peer, ts):
+    """llama -sm row -ts 1,1 / 1,1,1,1 / 3,1: libllama puts every matrix in the backend's
+    split buffer type (proc ggml_backend_split_buffer_type), rows divided over the devices —
+    here logical devices of the one MI355X (GGML_MI355X_VIRTUAL_DEVICES) — and every
+    MUL_MAT runs its slices on each and gathers them (split.cpp). Logits against the
+    reference CPU backend. Decode's gate/up/SwiGLU and MUL_MAT -> ADD run as per-slice fused
+    GEMVs (klog glu_split / mm_split_add): on the main stream when the slices are this GPU's,
+    and (round 5) forked onto each other slice device's own stream under
+    GGML_MI355X_FORCE_PEER — the branch separate GPUs with peer access take (remote =
+    slices - 1: the main device's slice stays on the main stream). Without peer access
+    (GGML_MI355X_NO_PEER) they fall back to the staged per-matrix path."""
     _need_ref()
+    n_dev = len(ts.split(","))
     toks = np.random.default_rng(10).integers(0, 1000, 24 if incremental else 40)
     g = ggufs[("small", "q4_k_m")]
     klog = tmp_path / "klog.txt"
     cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental)
-    env = {"GGML_MI355X_VIRTUAL_DEVICES": "2"}
+    env = {"GGML_MI355X_VIRTUAL_DEVICES": str(n_dev)}
     if force_peer:
         env["GGML_MI355X_FORCE_PEER"] = "1"
     if no_peer:
         env["GGML_MI355X_NO_PEER"] = "1"
-    gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, klog=klog, extra=["-sm", "row", "-ts", "1,1"],
+    gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, klog=klog, extra=["-sm", "row", "-ts", ts],
                        env_extra=env)
     assert "MI355X" in log
     assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
     kl = klog.read_text()
-    assert "mm_split" in kl and "devices=2" in kl, kl[-2000:]
+    assert "mm_split" in kl and f"devices={n_dev}" in kl, kl[-2000:]
+    fused = [ln for ln in kl.splitlines() if ln.startswith(("glu_split ", "mm_split_add "))]
     if force_peer:
         # GGML_MI355X_FORCE_PEER: the cross-device broadcast / gather branches of split.cpp ran
         # (no_peer: the slices come back by one contiguous peer copy and a 2D copy on main)
         assert all("peer=1" in ln and f"direct={int(not no_peer)}" in ln for ln in kl.splitlines() if ln.startswith("mm_split ")), kl[-2000:]
-        assert "glu_split" not in kl and "mm_split_add" not in kl, kl[-2000:]
+        if no_peer:
+            assert not fused, kl[-2000:]
+        elif incremental:
+            assert any(ln.startswith("glu_split ") for ln in fused) and any(ln.startswith("mm_split_add ") for ln in fused), kl[-2000:]
+            sr = [re.search(r"slices=(\d+) remote=(\d+)", ln).groups() for ln in fused]
+            # every slice but the main device's own runs on its device's stream
+            assert all(int(b) == int(a) - 1 for a, b in sr) and any(int(a) == n_dev for a, _ in sr), fused[:4]
     elif incremental:
-        # one-token steps: the per-slice fused SwiGLU and residual GEMVs
-        assert "glu_split" in kl and "mm_split_add" in kl, kl[-2000:]
+        # one-token steps: the per-slice fused SwiGLU and residual GEMVs on this stream
+        assert any(ln.startswith("glu_split ") for ln in fused) and any(ln.startswith("mm_split_add ") for ln in fused), kl[-2000:]
+        assert all("remote=0" in ln for ln in fused), fused[:4]
 
 
 @pytest.mark.parametrize("ts", ["1,1", "1,1,1,1"])

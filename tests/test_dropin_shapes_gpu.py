@@ -156,6 +156,30 @@ def test_llama3_8b_width_decode(l8b, tmp_path, fa):
     assert k["mmvq1"] == 0, k                                  # no first-generation fallback GEMV
 
 
+def test_llama3_8b_width_decode_at_depth(l8b, tmp_path):
+    """decode against a 4096-position cache (llama-bench -d's regime): the streaming
+    attention (k_fattn_dec3) in every layer, and the decode fusions intact at depth — the
+    SwiGLU absorbs the deferred ffn norm even where libllama's allocator puts the GLU output
+    over the (never materialised) normed x (round 4 materialised the norm there and fell
+    back to the first-generation GEMV: 30 us per layer at -d 16384)"""
+    depth, n = 4096, 6
+    toks = np.random.default_rng(24).integers(0, 128000, depth + n)
+    extra = ("--prefix", str(depth))
+    cpu, _, _ = run_ref(tmp_path, l8b, toks, 0, 1, incremental=True, extra=extra)
+    gpu, log, klog = run_ref(tmp_path, l8b, toks, 99, 1, incremental=True, extra=extra,
+                             env_extra={"GGML_MI355X_DISABLE_GRAPHS": "1"})
+    assert cpu.shape[0] == n and gpu.shape[0] == n
+    assert np.all(np.isfinite(gpu))
+    err = nmse(gpu, cpu)
+    assert err < TOL, err
+    k = kinds(klog)
+    L = 2
+    assert k["fattn_dec3"] == n * L, k
+    # (+1: the prefix batch's last layer runs its one output row — llama's inp_out_ids)
+    assert k["gemv2 epi=1 mode=4 M=14336 q8o=1"] == n * L + 1, k
+    assert k["mmvq1"] == 0, k
+
+
 def test_llama3_8b_width_decode_graph_replay(l8b, tmp_path):
     """the production path: decode captured into a hipGraph and replayed per token"""
     toks = np.random.default_rng(22).integers(0, 128000, 10)

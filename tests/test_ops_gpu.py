@@ -332,6 +332,53 @@ def test_flash_attn_split_merge(pkg, backend, orc, n_q, n_kv, H, Hkv, D):
         lib.ggml_backend_mi355x_set_tune(10, 0)
 
 
+@pytest.mark.parametrize("n_kv,H,Hkv,masked", [(16384, 32, 8, True), (2048, 8, 8, True), (5000, 16, 2, True),
+                                                (33000, 8, 8, True), (8000, 64, 8, True), (4096, 4, 4, False),
+                                                (30000, 32, 4, True)])
+@pytest.mark.parametrize("stream", [True, False])
+def test_flash_attn_stream(pkg, backend, orc, n_kv, H, Hkv, masked, stream):
+    """long-cache decode attention: k_fattn_dec3 (one workgroup per CU streaming a key range
+    of one KV head through its LDS-DMA ring, all Gt query heads, splits merged in-launch by
+    the last arrival) — GQA 1 / 2 / 4 / 8, ragged last split, no mask; stream=False keeps
+    the round-3 LONG geometry + combine (g_tune[34] = 1) for comparison. Run twice: the
+    arrival counters must be back at zero for the next launch / replay"""
+    lib = pkg._lib.load()
+    lib.ggml_backend_mi355x_set_tune(34, 0 if stream else 1)
+    D = 128
+    rng = np.random.default_rng(n_kv + H)
+    q = rng.standard_normal((H, 1, D)).astype(np.float32)
+    k = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16)
+    v = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16).view(np.uint16)
+    mask = np.zeros((1, n_kv), np.float32)
+    if masked:
+        mask[0, n_kv - 37:] = -np.inf            # the padded tail of a KV cache view
+        mask[0, 100:300] = -np.inf               # a masked run inside one split
+    m16 = mask.astype(np.float16).view(np.uint16)
+    scale = 1.0 / np.sqrt(D)
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, 1, H)
+        tk = ctx.new_tensor("f16", D, n_kv, Hkv)
+        tv = ctx.new_tensor("f16", D, n_kv, Hkv)
+        if not masked:
+            return [ctx.flash_attn_ext(tq, tk, tv, None, scale)], [(tq, q), (tk, k), (tv, v)]
+        tm = ctx.new_tensor("f16", n_kv, 1)
+        return [ctx.flash_attn_ext(tq, tk, tv, tm, scale)], [(tq, q), (tk, k), (tv, v), (tm, m16)]
+
+    try:
+        backend.klog(True)
+        y = run(pkg, backend, build)[0].reshape(1, H, D)
+        log = backend.klog_read()
+        backend.klog(False)
+        y2 = run(pkg, backend, build)[0].reshape(1, H, D)
+    finally:
+        lib.ggml_backend_mi355x_set_tune(34, 0)
+    assert any(ln.startswith("fattn_dec3 ") for ln in log) == stream, log
+    ref = orc.flash_attn(q, k, v, m16, scale)
+    assert nmse(y, ref) < 5e-4
+    assert np.array_equal(y, y2)
+
+
 @pytest.mark.parametrize("kind", ["q8_0", "q4_0", "bf16", "f32"])
 @pytest.mark.parametrize("n_q,n_kv,H,Hkv,D,softcap", [
     (1, 256, 32, 8, 128, 0.0),      # tg128 decode step: k_fattn_dec2 (q8_0 native), tile kernel otherwise
