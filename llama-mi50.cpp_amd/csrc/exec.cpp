@@ -24,8 +24,11 @@ static bool is_view_op(int op) {
            op == GGML_OP_PERMUTE || op == GGML_OP_TRANSPOSE;
 }
 
+size_t nofa_long_scratch(const ggml_tensor * sm);   // ops_fattn_dec.hip: the long -fa 0 decode chain
+
 size_t scratch_bytes(const ggml_tensor * n) {
     switch (n->op) {
+        case GGML_OP_SOFT_MAX:       return nofa_long_scratch(n);
         case GGML_OP_MUL_MAT:        return mul_mat_scratch(n);
         case GGML_OP_MUL_MAT_ID:     return mul_mat_id_scratch(n);
         case GGML_OP_FLASH_ATTN_EXT: return flash_attn_scratch(n);

@@ -1191,6 +1191,239 @@ __global__ __launch_bounds__(NT) void k_attn_nofa_dec(NfArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Round 5: the -fa 0 decode chain for long caches. k_attn_nofa_dec keeps a head's scores in
+// LDS (<= 16384 keys) and runs one workgroup per query head; beyond that the chain fell to
+// the generic f16 GEMVs (llama-bench's default -fa 0 at -d 16384: 54 tok/s). Three launches
+// over the whole chip instead:
+//  k_nofa_scores: (KV head, 128-key chunk) workgroups for all Gt query heads of the group
+//    (K read once): s = f16(q)·k · scale + mask into scratch, and per chunk the (max,
+//    Σ exp(s - max)) of each head;
+//  k_nofa_pv: (KV head, 512-key block) workgroups: each head's global max and sum from the
+//    chunk partials, p = f16(exp(s - max) / sum) for the block — the softmax, then the
+//    second mul_mat's f16 conversion, as the node chain computes them — and Σ p·v over the
+//    block's keys of the transposed V rows (two threads per dimension) -> a partial O;
+//  k_nofa_sum: O = Σ of the block partials in block order (p is normalised: a plain,
+//    deterministic sum).
+// ---------------------------------------------------------------------------
+struct NlArgs {
+    const char * q; size_t q2;
+    const char * k; size_t k1, k2;
+    const char * v; size_t v1, v2;
+    const char * mask; int mask_f16;
+    float * s;            // [H][n_kv] scores
+    float2 * cp;          // [H][nc] chunk (max, sum)
+    float * op;           // [nb][H][D] block partials of O
+    float * dst;          // [H][D]
+    int n_kv, H, Hkv, nc, nb;
+    float scale;
+};
+constexpr int NL_CK = 128, NL_KB = 512;
+
+template <int G>
+__global__ __launch_bounds__(256) void k_nofa_scores(NlArgs p) {
+    constexpr int LPK = 16, KPI = 4, NI = 8;
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    __shared__ float rm[4][G], rl[4][G];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c = lane % LPK, kq = lane / LPK;
+    const int hk = blockIdx.x % p.Hkv, ch = blockIdx.x / p.Hkv, hb = hk * G;
+    const char * kb = p.k + (size_t) hk * p.k2 + c * 16;
+    uint4 kr[NI];
+    int key[NI];
+    float mv[NI];
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+        key[t] = ch * NL_CK + (wave * NI + t) * KPI + kq;
+        kr[t] = *(const uint4 *) (kb + (size_t) min(key[t], p.n_kv - 1) * p.k1);
+    }
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+        const int kk = min(key[t], p.n_kv - 1);
+        mv[t] = !p.mask ? 0.f : p.mask_f16 ? h2f(((const uint16_t *) p.mask)[kk]) : ((const float *) p.mask)[kk];
+    }
+    h2v qh[G][4];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        const float * qp = (const float *) (p.q + (size_t) (hb + h) * p.q2) + 8 * c;
+        const float4 a = *(const float4 *) qp, b = *(const float4 *) (qp + 4);
+        qh[h][0] = h2v{(_Float16) a.x, (_Float16) a.y}; qh[h][1] = h2v{(_Float16) a.z, (_Float16) a.w};
+        qh[h][2] = h2v{(_Float16) b.x, (_Float16) b.y}; qh[h][3] = h2v{(_Float16) b.z, (_Float16) b.w};
+    }
+    float sc[G][NI];
+#pragma unroll
+    for (int t = 0; t < NI; ++t)
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            float acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[h][0], 0.f, false);
+            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[h][1], acc, false);
+            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[h][2], acc, false);
+            acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[h][3], acc, false);
+            acc = dpp_sum_group<LPK>(acc);                    // (in every lane of the row)
+            sc[h][t] = key[t] < p.n_kv ? acc * p.scale + mv[t] : -INFINITY;
+            if (c == 0 && key[t] < p.n_kv) p.s[(size_t) (hb + h) * p.n_kv + key[t]] = sc[h][t];
+        }
+    // the chunk's (max, sum) per head: over t in the lane, the row groups kq, then the waves
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        float m = sc[h][0];
+#pragma unroll
+        for (int t = 1; t < NI; ++t) m = fmaxf(m, sc[h][t]);
+        m = kr_max<LPK>(m);
+        if (lane == 0) rm[wave][h] = m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        const float M = fmaxf(fmaxf(rm[0][h], rm[1][h]), fmaxf(rm[2][h], rm[3][h]));
+        float l = 0.f;
+#pragma unroll
+        for (int t = 0; t < NI; ++t) l += sc[h][t] == -INFINITY ? 0.f : expf(sc[h][t] - M);
+        l = kr_sum<LPK>(l);
+        if (lane == 0) rl[wave][h] = l;
+    }
+    __syncthreads();
+    if (tid < G) {
+        const float M = fmaxf(fmaxf(rm[0][tid], rm[1][tid]), fmaxf(rm[2][tid], rm[3][tid]));
+        p.cp[(size_t) (hb + tid) * p.nc + ch] = make_float2(M, (rl[0][tid] + rl[1][tid]) + (rl[2][tid] + rl[3][tid]));
+    }
+}
+
+// KB keys per workgroup (512, or 128 for shorter caches: >= ~256 workgroups); the V rows of
+// the block are loaded first, so their round trip overlaps the (max, sum) reductions
+template <int G, int KB>
+__global__ __launch_bounds__(256) void k_nofa_pv(NlArgs p) {
+    constexpr int D = 128, NV = KB / 16;                   // 16-byte V loads per thread
+    __shared__ float pl[G][KB];
+    __shared__ float red[4][G], sM[G], sInv[G];
+    __shared__ float oh[G][D];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hk = blockIdx.x % p.Hkv, blk = blockIdx.x / p.Hkv, hb = hk * G, k0 = blk * KB;
+    // P·V geometry: thread -> dimension d, key half (KB / 2 keys)
+    const int d = tid & (D - 1), half = tid >> 7;
+    const int kb0 = k0 + half * (KB / 2);
+    const char * vr = p.v + (size_t) hk * p.v2 + (size_t) d * p.v1 + (size_t) kb0 * 2;
+    uint4 vv[NV];
+    auto load_v = [&] {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) vv[j] = kb0 + 8 * j + 8 <= p.n_kv ? *(const uint4 *) (vr + 16 * j) : make_uint4(0, 0, 0, 0);
+    };
+    // (512-key blocks: after the probabilities — 128 VGPRs of V held across the reductions
+    // measured 23 vs 20 us per launch at 16k keys)
+    if constexpr (KB <= 128) load_v();
+    // global max and sum of each head (every workgroup of the head recomputes them: nc pairs)
+    float m[G], l[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        m[h] = -INFINITY;
+        for (int cc = tid; cc < p.nc; cc += 256) m[h] = fmaxf(m[h], p.cp[(size_t) (hb + h) * p.nc + cc].x);
+        m[h] = wave_max(m[h]);
+        if (lane == 0) red[wave][h] = m[h];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        m[h] = fmaxf(fmaxf(red[0][h], red[1][h]), fmaxf(red[2][h], red[3][h]));
+        l[h] = 0.f;
+        for (int cc = tid; cc < p.nc; cc += 256) {
+            const float2 v = p.cp[(size_t) (hb + h) * p.nc + cc];
+            l[h] += v.x == -INFINITY ? 0.f : v.y * expf(v.x - m[h]);
+        }
+        l[h] = wave_sum(l[h]);
+    }
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) red[wave][h] = l[h];
+    }
+    __syncthreads();
+    if (tid < G) { sM[tid] = m[tid]; sInv[tid] = 1.0f / ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])); }
+    __syncthreads();
+    // this block's probabilities, f16-rounded
+    for (int k = tid; k < KB; k += 256) {
+        const int key = k0 + k;
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const float sv = key < p.n_kv ? p.s[(size_t) (hb + h) * p.n_kv + key] : -INFINITY;
+            pl[h][k] = sv == -INFINITY ? 0.f : (float) (_Float16) (expf(sv - sM[h]) * sInv[h]);
+        }
+    }
+    __syncthreads();
+    if constexpr (KB > 128) load_v();
+    float o[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) o[h] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const uint32_t ww[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float x = h2f((uint16_t) (ww[e >> 1] >> (16 * (e & 1))));
+#pragma unroll
+            for (int h = 0; h < G; ++h) o[h] += pl[h][half * (KB / 2) + 8 * j + e] * x;
+        }
+    }
+    if (half == 1) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) oh[h][d] = o[h];
+    }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) p.op[((size_t) blk * p.H + hb + h) * D + d] = o[h] + oh[h][d];
+    }
+}
+
+__global__ __launch_bounds__(128) void k_nofa_sum(NlArgs p) {
+    const int h = blockIdx.x, d = threadIdx.x;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int b = 0; b < p.nb; ++b) acc += p.op[((size_t) b * p.H + h) * 128 + d];
+    p.dst[(size_t) h * 128 + d] = acc;
+}
+
+// the long-cache form: D 128, one query token, GQA 1/2/4/8, n_kv % 8 == 0, from
+// GGML_MI355X_NOFA_LONG_MIN keys (default 512: drop-in -fa 0 tg128 at -d 512 / 1024 / 4096 /
+// 16384 453 -> 499, 376 -> 507, 184 -> 461, 54 -> 362 tok/s; g_tune[36] in units of 1024) and for every
+// cache the one-workgroup kernel cannot hold (> 16384 keys)
+static int nl_min_kv() {
+    static const int env = [] { const char * v = getenv("GGML_MI355X_NOFA_LONG_MIN"); return v ? atoi(v) : 512; }();
+    return g_tune[36] > 0 ? g_tune[36] * 1024 : env;
+}
+static bool nl_ok(int D, int n_kv, int H, int Hkv) {
+    const int G = H / Hkv;
+    return D == 128 && n_kv % 8 == 0 && (n_kv > NF_MAX_KV || n_kv >= nl_min_kv()) && (G == 1 || G == 2 || G == 4 || G == 8);
+}
+static size_t nl_scratch(int n_kv, int H) {
+    const size_t nc = mx_ceil_div(n_kv, NL_CK), nb = mx_ceil_div(n_kv, NL_KB);
+    return (size_t) H * n_kv * 4 + 256 + (size_t) H * nc * 8 + 256 + 4 * nb * H * 128 * 4 + 256;   // (blocks of 128 keys: 4 nb)
+}
+// scratch of the chain, sized at its SOFT_MAX node (one query row of n_kv keys, H heads)
+size_t nofa_long_scratch(const ggml_tensor * sm) {
+    if (sm->op != GGML_OP_SOFT_MAX || sm->ne[1] != 1 || sm->ne[3] != 1 || sm->ne[0] % 8) return 0;
+    if (sm->ne[0] <= NF_MAX_KV && sm->ne[0] < nl_min_kv()) return 0;
+    return nl_scratch((int) sm->ne[0], (int) sm->ne[2]);
+}
+static void nl_run(OpCtx & c, const NfArgs & a, float * dst) {
+    NlArgs p{};
+    p.q = a.q; p.q2 = a.q2; p.k = a.k; p.k1 = a.k1; p.k2 = a.k2; p.v = a.v; p.v1 = a.v1; p.v2 = a.v2;
+    p.mask = a.mask; p.mask_f16 = a.mask_f16; p.dst = dst;
+    p.n_kv = a.n_kv; p.H = a.H; p.Hkv = a.Hkv; p.scale = a.scale;
+    p.nc = (int) mx_ceil_div(a.n_kv, NL_CK);
+    const int kb = a.Hkv * mx_ceil_div(a.n_kv, NL_KB) >= 256 ? NL_KB : 128;
+    p.nb = (int) mx_ceil_div(a.n_kv, kb);
+    p.s = (float *) c.scratch->take((size_t) a.H * a.n_kv * 4);
+    p.cp = (float2 *) c.scratch->take((size_t) a.H * p.nc * 8);
+    p.op = (float *) c.scratch->take((size_t) p.nb * a.H * 128 * 4);
+    const int G = a.H / a.Hkv;
+    MX_KLOG("attn_nofa_long D=128 n_kv=%d H=%d Hkv=%d chunks=%d blocks=%d kb=%d", a.n_kv, a.H, a.Hkv, p.nc, p.nb, kb);
+    const dim3 g1((unsigned) (a.Hkv * p.nc)), g2((unsigned) (a.Hkv * p.nb));
+#define NL(GG) if (G == GG) { k_nofa_scores<GG><<<g1, 256, 0, c.st>>>(p); \
+        if (kb == NL_KB) k_nofa_pv<GG, NL_KB><<<g2, 256, 0, c.st>>>(p); else k_nofa_pv<GG, 128><<<g2, 256, 0, c.st>>>(p); }
+    NL(1) NL(2) NL(4) NL(8)
+#undef NL
+    k_nofa_sum<<<(unsigned) a.H, 128, 0, c.st>>>(p);
+}
+
 static bool nf_view(const ggml_tensor * t) {
     return t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW || t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE;
 }
@@ -1221,7 +1454,9 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
     // decode P·V: 256/D threads per dimension, each a contiguous key range stepped by 8 keys
     // (16-byte V loads), so n_kv must split into 256/D parts of a multiple of 8 keys
     if (H % Hkv || k->nb[0] != 2 || k->nb[1] % 16 || k->nb[2] % 16 || (uintptr_t) k->data % 16) return 0;
-    if (pre ? (n_kv % 64 || n_kv < 64) : (n_kv % (8 * (256 / D)) || n_kv > NF_MAX_KV)) return 0;
+    const bool lng = !pre && nl_ok(D, n_kv, H, Hkv);
+    if (pre ? (n_kv % 64 || n_kv < 64) : lng ? false : (n_kv % (8 * (256 / D)) || n_kv > NF_MAX_KV)) return 0;
+    if (lng && c.scratch->avail() < nl_scratch(n_kv, H)) return 0;
     if (q->nb[0] != 4 || q->nb[2] % 16 || (uintptr_t) q->data % 16 || (pre && q->nb[1] % 16)) return 0;
     ggml_tensor * sm = nullptr, * kqv = nullptr, * out = nullptr;
     int last = i;
@@ -1286,6 +1521,7 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         deferred_guard_node_ext(c, g->nodes[j]);
         act_cache_invalidate(c.s, g->nodes[j]);
     }
+    if (lng) { nl_run(c, a, (float *) out->data); return last - i + 1; }
     MX_KLOG("attn_nofa D=%d n_kv=%d H=%d Hkv=%d mask=%d pf=%d", D, n_kv, H, Hkv, m ? (int) m->type : -1, H % 8 == 0 ? c.s->pf_n : 0);
     const size_t lds = (size_t) n_kv * 4;
     dim3 grid((unsigned) H, 1);

@@ -566,14 +566,20 @@ def test_moe_router_fusion(pkg, backend, n_tok, n_exp, producer):
 
 
 @pytest.mark.parametrize("n_kv,H,Hkv,D,mask_t", [(256, 32, 8, 128, "f32"), (512, 8, 8, 128, "f16"), (96, 4, 2, 64, "f32"),
-                                                 (256, 32, 8, 128, None), (48, 4, 2, 64, "f32"), (16384, 8, 8, 128, "f16")])
+                                                 (256, 32, 8, 128, None), (48, 4, 2, 64, "f32"), (16384, 8, 8, 128, "f16"),
+                                                 (16640, 32, 8, 128, "f16"), (17000, 16, 2, 128, "f32"), (8192, 64, 8, 128, "f16"),
+                                                 (20008, 4, 4, 128, None), (4096, 32, 8, 128, "f16"), (2056, 8, 2, 128, "f32")])
 def test_attn_nofa_decode_chain(pkg, backend, n_kv, H, Hkv, D, mask_t):
     """-fa 0 decode attention (llama-bench's default): MUL_MAT(k, q) -> SOFT_MAX(mask, scale)
     -> MUL_MAT(v^T, kq) -> PERMUTE -> CONT (src/llama-graph.cpp:1740-1796) as one launch
     (k_attn_nofa_dec), against the node-by-node semantics in float64: q and p rounded to
     f16 as the two mul_mats' vec_dot_type conversions do. n_kv = 48 at D 64 does not split
     into the kernel's 4 parts of 8-key steps: the chain must run unfused (and stay right);
-    n_kv = 16384 needs 64 KB of scores in LDS (max dynamic LDS raised past the default)."""
+    n_kv = 16384 needs 64 KB of scores in LDS (max dynamic LDS raised past the default).
+    Round 5: caches from 512 keys (and all beyond the one-workgroup kernel's 16384) take
+    the three-launch long form (klog attn_nofa_long: chunked scores + (max, sum) partials,
+    block P·V partials, their ordered sum) — llama-bench -d 16384 pads n_kv to 16640; GQA 8,
+    4, 2 and 1; a ragged last chunk and block (17000, 20008)."""
     rng = np.random.default_rng(n_kv + H + D)
     q = rng.standard_normal((H, 1, D)).astype(np.float32)
     k = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16)
@@ -600,8 +606,10 @@ def test_attn_nofa_decode_chain(pkg, backend, n_kv, H, Hkv, D, mask_t):
     y = run(pkg, backend, build)[0].reshape(H, D)
     log = backend.klog_read()
     backend.klog(False)
-    fused = n_kv % (8 * (256 // D)) == 0
+    lng = D == 128 and n_kv % 8 == 0 and n_kv >= 512
+    fused = lng or (n_kv % (8 * (256 // D)) == 0 and n_kv <= 16384)
     assert any(ln.startswith("attn_nofa") for ln in log) == fused, log
+    assert any(ln.startswith("attn_nofa_long ") for ln in log) == lng, log
     G = H // Hkv
     ref = np.empty((H, D))
     for h in range(H):
