@@ -909,7 +909,11 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         run_nodes(s, g);
         if (second) { s->split_graph = false; return; }
         HIP_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+        // (the kernel-choice log records the eager pass only: the capture repeats its choices)
+        const int klog_on = g_klog;
+        g_klog = 0;
         run_nodes(s, g);
+        g_klog = klog_on;
         s->split_graph = false;
         hipGraph_t graph = nullptr;
         HIP_CHECK(hipStreamEndCapture(s->stream, &graph));
