@@ -21,6 +21,7 @@
 //    replay) combines them — no second kernel, no second launch gap.
 #include "backend.h"
 #include "quants.cuh"
+#include "gemv.h"
 
 namespace mx { extern int g_tune[48]; }
 
@@ -718,8 +719,8 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec3(FaDecArgs p, int kps) {
     typedef _Float16 h2v __attribute__((ext_vector_type(2)));
     extern __shared__ __align__(16) uint4 ring[];            // [NW][S][FD3_WST]
     __shared__ float wm[NW][G], wl[NW][G];
-    __shared__ __align__(16) float wo[NW][G][D];
     __shared__ int s_last;
+    float (*wo)[G][D] = (float (*)[G][D]) ring;               // after the loop: the waves' O (ring reused)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c = lane % LPK, kq = lane / LPK;
@@ -855,6 +856,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec3(FaDecArgs p, int kps) {
         }
     }
     MX_TRACE(tr, 3);
+    __syncthreads();                                          // every wave is done with its ring slots
     // the NW waves' (O, M, L) -> this split's partial
 #pragma unroll
     for (int h = 0; h < G; ++h) {
@@ -977,8 +979,14 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec3(FaDecArgs p, int kps) {
 // geometry: ~256 workgroups (one per CU), NS splits per KV head of kps keys each (a whole
 // number of 16 x NW-key workgroup stages). GGML_MI355X_FA_STREAM=0 / g_tune[34] = 1 off;
 // g_tune[35] = minimum cache length in units of 256 keys (default 2048 keys).
-struct Fd3Cfg { int ns = 0, kps = 0; };
-constexpr int FD3_NW = 4, FD3_S = 4;
+struct Fd3Cfg { int ns = 0, kps = 0, nw = 4, st = 4; };
+// geometry: 4 waves x 4 ring stages (one wave per SIMD), or g_tune[37] = 1: 8 waves x 2
+// stages (two waves per SIMD: a lone wave issues VALU at half the SIMD's rate, and the
+// loop is VALU-bound — 0.56 of wave time issuing, pmc_decode_d16384_sq.json)
+static int fd3_geom() {
+    static const int env = [] { const char * v = getenv("GGML_MI355X_FA_STREAM_GEOM"); return v ? atoi(v) : 0; }();
+    return g_tune[37] ? g_tune[37] : env;
+}
 static Fd3Cfg fd3_cfg(const ggml_tensor * dst) {
     static const bool off = [] { const char * v = getenv("GGML_MI355X_FA_STREAM"); return v && !strcmp(v, "0"); }();
     const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
@@ -988,11 +996,12 @@ static Fd3Cfg fd3_cfg(const ggml_tensor * dst) {
     const int64_t n_kv = k->ne[1], Hkv = k->ne[2];
     const int64_t min_kv = g_tune[35] > 0 ? (int64_t) g_tune[35] * 256 : 2048;
     if (n_kv < min_kv || n_kv % 2 || Hkv > MX_FA_CNT / 2) return {};
-    const int64_t wst = FD3_SK * FD3_NW;
+    const int nw = fd3_geom() == 1 ? 8 : 4, st = fd3_geom() == 1 ? 2 : 4;
+    const int64_t wst = FD3_SK * nw;
     int64_t ns = std::max<int64_t>(1, 256 / Hkv);
     ns = std::min<int64_t>({ns, FD3_MAXNS, mx_ceil_div(n_kv, wst)});
     const int64_t kps = mx_ceil_div(mx_ceil_div(n_kv, ns), wst) * wst;
-    return {(int) mx_ceil_div(n_kv, kps), (int) kps};
+    return {(int) mx_ceil_div(n_kv, kps), (int) kps, nw, st};
 }
 
 static size_t fd3_scratch(const ggml_tensor * dst) {
@@ -1019,12 +1028,13 @@ static bool fd3_run(OpCtx & c, ggml_tensor * dst) {
     a.trace_blk = mx_trace_blocks();
     const int Gt = a.H / a.Hkv;
     const dim3 grid((unsigned) (a.Hkv * f.ns));
-    constexpr size_t lds = (size_t) FD3_NW * FD3_S * FD3_WST * 16;
-    MX_KLOG("fattn_dec3 D=128 G=%d ns=%d kps=%d n_kv=%d H=%d Hkv=%d", Gt, f.ns, f.kps, a.n_kv, a.H, a.Hkv);
-#define F3(GG) if (Gt == GG) { \
-        MX_LDS_OPTIN((k_fattn_dec3<GG, FD3_NW, FD3_S>), lds); \
-        k_fattn_dec3<GG, FD3_NW, FD3_S><<<grid, 64 * FD3_NW, lds, c.st>>>(a, f.kps); return true; }
-    F3(1) F3(2) F3(4) F3(8)
+    const size_t lds = (size_t) f.nw * f.st * FD3_WST * 16;
+    MX_KLOG("fattn_dec3 D=128 G=%d ns=%d kps=%d n_kv=%d H=%d Hkv=%d nw=%d", Gt, f.ns, f.kps, a.n_kv, a.H, a.Hkv, f.nw);
+#define F3(GG, NWW, SS) if (Gt == GG && f.nw == NWW) { \
+        MX_LDS_OPTIN((k_fattn_dec3<GG, NWW, SS>), lds); \
+        k_fattn_dec3<GG, NWW, SS><<<grid, 64 * NWW, lds, c.st>>>(a, f.kps); return true; }
+    F3(1, 4, 4) F3(2, 4, 4) F3(4, 4, 4) F3(8, 4, 4)
+    F3(1, 8, 2) F3(2, 8, 2) F3(4, 8, 2) F3(8, 8, 2)
 #undef F3
     return false;
 }
@@ -1424,6 +1434,88 @@ static void nl_run(OpCtx & c, const NfArgs & a, float * dst) {
     k_nofa_sum<<<(unsigned) a.H, 128, 0, c.st>>>(p);
 }
 
+// ---------------------------------------------------------------------------
+// Round 5: the -fa 0 decode chain of a short cache (<= 512 keys, D 128) as split partials
+// for the output projection's prologue (XS_FAP, as fa_dec2_partials does for -fa 1): one
+// 4-wave workgroup per (query head, 64-key split) computes the split's scores, its max
+// (log2 domain), Σ exp2(s - max) and the unnormalised Σ p·v over the transposed V rows,
+// all loads (K rows, mask, V row segments) issued before any arithmetic. The output
+// projection merges the splits while its weight loads are in flight: no one-workgroup-
+// per-head pass over the whole cache, no separate f32 x. Numerics: the probabilities stay
+// f32 here (the node chain rounds the normalised p to f16 for the second mul_mat).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_nofa_part(NfArgs p, float * part, int nsplit) {
+    constexpr int D = 128, LPK = 16, KPI = 4, NI = 4;
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    __shared__ float sc[64], red[4], oh[D];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c = lane % LPK, kq = lane / LPK;
+    const int h = blockIdx.x, sp = blockIdx.y, hk = h / (p.H / p.Hkv), k0 = sp * 64;
+    const char * kb = p.k + (size_t) hk * p.k2 + c * 16;
+    // K rows: wave w has keys k0 + 16 w + 4 t + kq
+    uint4 kr[NI];
+    int key[NI];
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+        key[t] = k0 + wave * 16 + t * KPI + kq;
+        kr[t] = *(const uint4 *) (kb + (size_t) min(key[t], p.n_kv - 1) * p.k1);
+    }
+    // V: thread -> dimension d, half of the split's keys (32 keys = 4 x 16 B)
+    const int d = tid & (D - 1), half = tid >> 7;
+    const int kv0 = k0 + half * 32;
+    const char * vr = p.v + (size_t) hk * p.v2 + (size_t) d * p.v1 + (size_t) kv0 * 2;
+    uint4 vv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vv[j] = kv0 + 8 * j + 8 <= p.n_kv ? *(const uint4 *) (vr + 16 * j) : make_uint4(0, 0, 0, 0);
+    float mv[NI];
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+        const int kk = min(key[t], p.n_kv - 1);
+        mv[t] = !p.mask ? 0.f : p.mask_f16 ? h2f(((const uint16_t *) p.mask)[kk]) : ((const float *) p.mask)[kk];
+    }
+    h2v qh[4];
+    {
+        const float * qp = (const float *) (p.q + (size_t) h * p.q2) + 8 * c;
+        const float4 a = *(const float4 *) qp, b = *(const float4 *) (qp + 4);
+        qh[0] = h2v{(_Float16) a.x, (_Float16) a.y}; qh[1] = h2v{(_Float16) a.z, (_Float16) a.w};
+        qh[2] = h2v{(_Float16) b.x, (_Float16) b.y}; qh[3] = h2v{(_Float16) b.z, (_Float16) b.w};
+    }
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+        float acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].x), qh[0], 0.f, false);
+        acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].y), qh[1], acc, false);
+        acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].z), qh[2], acc, false);
+        acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, kr[t].w), qh[3], acc, false);
+        acc = dpp_sum_group<LPK>(acc);
+        if (c == 0) {
+            const float sv = key[t] < p.n_kv ? acc * p.scale + mv[t] : -INFINITY;
+            sc[wave * 16 + t * KPI + kq] = sv == -INFINITY ? -INFINITY : sv * 1.4426950408889634f;   // log2 domain
+        }
+    }
+    __syncthreads();
+    // the split's max and Σ exp2 (wave 0), p into LDS
+    if (wave == 0) {
+        const float v = sc[lane];
+        const float m = wave_max(v);
+        const float e = m == -INFINITY || v == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(v - m);
+        sc[lane] = e;
+        const float l = wave_sum(e);
+        if (lane == 0) { red[0] = m; red[1] = l; }
+    }
+    __syncthreads();
+    float o = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t ww[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o += sc[half * 32 + 8 * j + e] * h2f((uint16_t) (ww[e >> 1] >> (16 * (e & 1))));
+    }
+    if (half == 1) oh[d] = o;
+    __syncthreads();
+    float * pw = part + ((size_t) h * nsplit + sp) * (D + 2);
+    if (half == 0) pw[d] = o + oh[d];
+    if (tid == 0) { pw[D] = red[0]; pw[D + 1] = red[1]; }
+}
+
 static bool nf_view(const ggml_tensor * t) {
     return t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW || t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE;
 }
@@ -1433,6 +1525,78 @@ static const ggml_tensor * nf_base(const ggml_tensor * t) {
 }
 
 static const bool g_no_attn_nofa_pp = getenv("GGML_MI355X_NO_ATTN_FUSION_PP") != nullptr;   // A/B: prefill chain node by node
+
+// the chain's CONT output feeding the output projection + residual ADD (decode, <= 512 keys,
+// D 128): split partials + the projection's FAP prologue; returns the nodes consumed from
+// i (0: not this shape — the caller runs the one-launch chain kernel)
+static const bool g_no_nofa_split_o = getenv("GGML_MI355X_NO_NOFA_SPLIT_O") != nullptr;   // A/B
+static int nofa_split_o(OpCtx & c, ggml_cgraph * g, int i, int last, const NfArgs & a, ggml_tensor * out, const UseCount & uses) {
+    if (g_no_nofa_split_o || g_tune[38] == 1 || !g_gemv2 || a.n_kv > 512 || a.n_kv % 64 || a.n_kv < 64) return 0;
+    auto use = [&](const ggml_tensor * t) { auto it = uses.find(t); return it == uses.end() ? 0 : it->second; };
+    const ggml_tensor * q = g->nodes[i]->src[1];
+    const int D = (int) q->ne[0], H = (int) q->ne[2], ns = a.n_kv / 64;
+    if (D != 128 || use(out) != 1 || (out->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    ggml_tensor * mm = nullptr;
+    int jm = -1;
+    for (int j = last + 1; j < g->n_nodes && j < last + 4; ++j) {
+        ggml_tensor * n = g->nodes[j];
+        if (nf_view(n)) { if (nf_base(n) != out) return 0; continue; }
+        if (n->op == GGML_OP_MUL_MAT && nf_base(n->src[1]) == out) { mm = n; jm = j; }
+        break;
+    }
+    if (!mm || jm + 1 >= g->n_nodes) return 0;
+    const ggml_tensor * x = mm->src[1];
+    if (x != out && (x->op != GGML_OP_RESHAPE || use(x) != 1 || (x->flags & GGML_TENSOR_FLAG_OUTPUT))) return 0;
+    if (mx_nelements(x) != (int64_t) D * H || mx_nrows(x) != 1) return 0;
+    const ggml_tensor * wo = mm->src[0];
+    if (tensor_is_split(wo) || !gemv2_ok(wo, x, mm) || !gemv2_fap_ok(wo->type, wo->ne[0], wo->ne[1])) return 0;
+    if (use(mm) != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    // the tail: ADD(mm, res) right after, or (the last layer) libllama's one-row inp_out_ids
+    // pair GET_ROWS(mm), GET_ROWS(res) -> ADD: one token, both GET_ROWS are the identity
+    ggml_tensor * add = nullptr, * g1 = nullptr, * g2 = nullptr;
+    const ggml_tensor * res = nullptr;
+    int lastn = -1;
+    if (g->nodes[jm + 1]->op == GGML_OP_ADD) {
+        add = g->nodes[jm + 1];
+        res = add->src[0] == mm ? add->src[1] : (add->src[1] == mm ? add->src[0] : nullptr);
+        lastn = jm + 1;
+    } else {
+        for (int j = jm + 1; j < g->n_nodes && j <= jm + 4; ++j) {
+            ggml_tensor * n = g->nodes[j];
+            if (nf_view(n)) continue;
+            if (n->op == GGML_OP_GET_ROWS && !g1 && n->src[0] == mm) { g1 = n; continue; }
+            if (n->op == GGML_OP_GET_ROWS && !g2 && n->src[0] != mm) { g2 = n; continue; }
+            if (n->op == GGML_OP_ADD && g1 && g2 && ((n->src[0] == g1 && n->src[1] == g2) || (n->src[0] == g2 && n->src[1] == g1))) {
+                add = n; lastn = j;
+            }
+            break;
+        }
+        if (!add) return 0;
+        for (const ggml_tensor * gr : {g1, g2}) {
+            if (gr->type != GGML_TYPE_F32 || gr->src[0]->type != GGML_TYPE_F32 || mx_nrows(gr->src[0]) != 1 || mx_nrows(gr) != 1 ||
+                mx_nelements(gr->src[1]) != 1 || use(gr) != 1 || (gr->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+        }
+        res = g2->src[0];
+    }
+    if (!res || res == mm || add->type != GGML_TYPE_F32 || res->type != GGML_TYPE_F32) return 0;
+    if (!mx_are_same_shape(res, mm) || !mx_are_same_shape(add, mm) || !mx_is_contiguous(res) || !mx_is_contiguous(add)) return 0;
+    const bool same = res->nb[1] == add->nb[1];
+    if (!fused_io_ok({add}, {res}, {{add, same ? res : nullptr}})) return 0;
+    const size_t part_bytes = (size_t) H * ns * (D + 2) * sizeof(float) + 256;
+    if (c.scratch->avail() < part_bytes) return 0;
+    for (int j = last + 1; j <= lastn; ++j) {
+        deferred_guard_node_ext(c, g->nodes[j]);
+        act_cache_invalidate(c.s, g->nodes[j]);
+    }
+    float * part = (float *) c.scratch->take(part_bytes);
+    MX_KLOG("attn_nofa_part D=128 n_kv=%d H=%d Hkv=%d nsplit=%d", a.n_kv, a.H, a.Hkv, ns);
+    k_nofa_part<<<dim3((unsigned) H, (unsigned) ns), 256, 0, c.st>>>(a, part, ns);
+    XStage xs{nullptr, nullptr, 0.0f, 0};
+    xs.xcd = g_tune[15] != 1;
+    xs.fap = part; xs.fap_ns = ns; xs.fap_d = D;
+    gemv2_launch(c, wo, nullptr, xs, (float *) add->data, (const float *) res->data);
+    return lastn - i + 1;
+}
 void fa_mma_nofa_launch(OpCtx & c, const ggml_tensor * q, const ggml_tensor * k, const ggml_tensor * v, const ggml_tensor * m,
                         float scale, ggml_tensor * out);   // ops_fattn_mma.hip
 
@@ -1522,6 +1686,7 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         act_cache_invalidate(c.s, g->nodes[j]);
     }
     if (lng) { nl_run(c, a, (float *) out->data); return last - i + 1; }
+    if (const int k = nofa_split_o(c, g, i, last, a, out, uses)) return k;
     MX_KLOG("attn_nofa D=%d n_kv=%d H=%d Hkv=%d mask=%d pf=%d", D, n_kv, H, Hkv, m ? (int) m->type : -1, H % 8 == 0 ? c.s->pf_n : 0);
     const size_t lds = (size_t) n_kv * 4;
     dim3 grid((unsigned) H, 1);
