@@ -978,7 +978,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec3(FaDecArgs p, int kps) {
 
 // geometry: ~256 workgroups (one per CU), NS splits per KV head of kps keys each (a whole
 // number of 16 x NW-key workgroup stages). GGML_MI355X_FA_STREAM=0 / g_tune[34] = 1 off;
-// g_tune[35] = minimum cache length in units of 256 keys (default 2048 keys).
+// g_tune[35] = minimum cache length in units of 256 keys (default 16384 keys).
 struct Fd3Cfg { int ns = 0, kps = 0, nw = 4, st = 4; };
 // geometry: 4 waves x 4 ring stages (one wave per SIMD), or g_tune[37] = 1: 8 waves x 2
 // stages (two waves per SIMD: a lone wave issues VALU at half the SIMD's rate, and the
@@ -994,7 +994,10 @@ static Fd3Cfg fd3_cfg(const ggml_tensor * dst) {
     if (k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16 || k->ne[0] != 128 || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1) return {};
     if (m && (m->ne[3] != 1 || (uintptr_t) m->data % 4 || m->nb[1] % 4)) return {};
     const int64_t n_kv = k->ne[1], Hkv = k->ne[2];
-    const int64_t min_kv = g_tune[35] > 0 ? (int64_t) g_tune[35] * 256 : 2048;
+    // (from 16384 keys: the LONG kernel + combine measured better at -d 4096 (547 vs 529
+    // tok/s) and -d 8192 (511.6 vs 498.2), this form at -d 16384 (453 vs 449.5) — same-box
+    // passes on two boxes, profiles/r05/fa_stream_ab.txt)
+    const int64_t min_kv = g_tune[35] > 0 ? (int64_t) g_tune[35] * 256 : 16384;
     if (n_kv < min_kv || n_kv % 2 || Hkv > MX_FA_CNT / 2) return {};
     const int nw = fd3_geom() == 1 ? 8 : 4, st = fd3_geom() == 1 ? 2 : 4;
     const int64_t wst = FD3_SK * nw;

@@ -344,6 +344,7 @@ def test_flash_attn_stream(pkg, backend, orc, n_kv, H, Hkv, masked, stream):
     arrival counters must be back at zero for the next launch / replay"""
     lib = pkg._lib.load()
     lib.ggml_backend_mi355x_set_tune(34, 0 if stream else 1)
+    lib.ggml_backend_mi355x_set_tune(35, 8)          # from 2048 keys (the default starts at 16384)
     D = 128
     rng = np.random.default_rng(n_kv + H)
     q = rng.standard_normal((H, 1, D)).astype(np.float32)
@@ -373,6 +374,7 @@ def test_flash_attn_stream(pkg, backend, orc, n_kv, H, Hkv, masked, stream):
         y2 = run(pkg, backend, build)[0].reshape(1, H, D)
     finally:
         lib.ggml_backend_mi355x_set_tune(34, 0)
+        lib.ggml_backend_mi355x_set_tune(35, 0)
     assert any(ln.startswith("fattn_dec3 ") for ln in log) == stream, log
     ref = orc.flash_attn(q, k, v, m16, scale)
     assert nmse(y, ref) < 5e-4
