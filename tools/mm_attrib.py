@@ -142,6 +142,60 @@ def main():
         rows.append(r)
         print(f"{r[0]:16s} {r[1]:22s} {r[2]:5s} {r[3]:6d} {r[4]:4d}  {r[5]:9.2e} {r[6]:9.2e} {r[7]:8.4f}  {r[8]:9.2e} {r[9]:9.2e}",
               flush=True)
+    # MUL_MAT_ID (MoE experts, round 5): each (token, slot) item against float64 W_e . x of
+    # that backend's own routing (ffn_moe_topk) and input; MOE_ROWS rows of every expert
+    # used (the full 14336 x 4096 x 8 tensors do not fit a float64 dequantisation)
+    moe_rows = int(os.environ.get("MOE_ROWS", "256"))
+    # (the routing: the first n_used columns of ffn_moe_argsort; the down projection's input:
+    # the layer's SWIGLU node, whatever its callback name)
+    MOE = {"ffn_moe_up": ("ffn_norm", "ffn_up_exps"), "ffn_moe_gate": ("ffn_norm", "ffn_gate_exps"),
+           "ffn_moe_down": ("@glu", "ffn_down_exps")}
+    seen = {}
+    for i, (name, op, ne) in enumerate(nc):
+        base, _, il = name.partition("-")
+        seen[name] = (i, ne)
+        if op in ("SWIGLU", "GLU") and il.isdigit():
+            seen[f"@glu-{il}"] = (i, ne)
+        if op != "MUL_MAT_ID" or base not in MOE or not il.isdigit():
+            continue
+        src, wn = MOE[base]
+        src, wname, tk = f"{src}-{il}", f"blk.{il}.{wn}.weight", f"ffn_moe_argsort-{il}"
+        if src not in seen or tk not in seen or wname not in tens:
+            continue
+        typ, wne, off = tens[wname]
+        K, M, E = wne[0], wne[1], wne[2]
+        be, bb = BLK[typ]
+        rb = K // be * bb
+        rows_ = min(moe_rows, M)
+        n_used, n_tok = ne[1], ne[2]
+        (jx, nex), (jt, net) = seen[src], seen[tk]
+        cache = {}
+
+        def wexp(e):
+            if e not in cache:
+                raw = np.fromfile(gguf, np.uint8, count=rb * rows_, offset=off + e * rb * M)
+                cache[e] = np.stack([orc.dequantize(typ, raw[r * rb:(r + 1) * rb], K) for r in range(rows_)]).astype(np.float64)
+            return cache[e]
+
+        errs, outs = [], []
+        for d in (cd, gd):
+            ids = np.fromfile(f"{d}/{jt:03d}.f32", np.float32).reshape(net[1], net[0]).astype(np.int64)[:, :n_used]
+            x = np.fromfile(f"{d}/{jx:03d}.f32", np.float32).astype(np.float64)
+            x = x.reshape(n_tok, -1, K)          # [n_tok, 1 or n_used, K]
+            y = np.fromfile(f"{d}/{i:03d}.f32", np.float32).astype(np.float64).reshape(n_tok, n_used, M)[:, :, :rows_]
+            ref = np.empty_like(y)
+            for t in range(n_tok):
+                for sl in range(n_used):
+                    ref[t, sl] = wexp(int(ids[t, sl])) @ x[t, sl % x.shape[1]]
+            errs.append(nmse(y, ref))
+            outs.append((ids, y))
+        same = outs[0][0] == outs[1][0]          # items both backends routed alike
+        og = nmse(outs[1][1][same], outs[0][1][same]) if same.any() else float("nan")
+        tname = {12: "q4_K", 13: "q5_K", 14: "q6_K", 8: "q8_0"}.get(typ, str(typ))
+        r = (name, wname, tname, rows_, n_tok * n_used, errs[0], errs[1], errs[1] / max(errs[0], 1e-300), float("nan"), og)
+        rows.append(r)
+        print(f"{r[0]:16s} {r[1][-22:]:22s} {r[2]:5s} {r[3]:6d} {r[4]:4d}  {r[5]:9.2e} {r[6]:9.2e} {r[7]:8.4f}  {'':9s} {r[9]:9.2e}"
+              f"  (items routed alike {int(same.sum())}/{same.size})", flush=True)
     # FLASH_ATTN_EXT: float64 causal attention of each backend's own roped q / k and v
     # (k, v rounded to f16 as the cache stores them: SET_ROWS is bit-exact on both)
     idx = {}
