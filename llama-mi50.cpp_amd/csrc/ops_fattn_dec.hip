@@ -1688,8 +1688,9 @@ int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses) {
         deferred_guard_node_ext(c, g->nodes[j]);
         act_cache_invalidate(c.s, g->nodes[j]);
     }
-    if (lng) { nl_run(c, a, (float *) out->data); return last - i + 1; }
+    // (split partials into the O projection first: at <= 512 keys they beat the long form)
     if (const int k = nofa_split_o(c, g, i, last, a, out, uses)) return k;
+    if (lng) { nl_run(c, a, (float *) out->data); return last - i + 1; }
     MX_KLOG("attn_nofa D=%d n_kv=%d H=%d Hkv=%d mask=%d pf=%d", D, n_kv, H, Hkv, m ? (int) m->type : -1, H % 8 == 0 ? c.s->pf_n : 0);
     const size_t lds = (size_t) n_kv * 4;
     dim3 grid((unsigned) H, 1);

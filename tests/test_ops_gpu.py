@@ -872,3 +872,75 @@ def test_moe_router_head_fusion(pkg, backend, orc, n_exp, E, wtype, knorm):
             assert np.array_equal(a.reshape(-1)[:k], b.reshape(-1)[:k])
         else:
             assert nmse(a.reshape(-1), b.reshape(-1)) < 1e-9
+
+
+@pytest.mark.parametrize("n_kv,H,Hkv,M,wt,mask_t", [(256, 32, 8, 4096, "q4_K", "f16"), (512, 8, 8, 1024, "q6_K", "f32"),
+                                                  (64, 16, 4, 2048, "q5_K", None), (448, 8, 2, 1024, "q4_K", "f16")])
+def test_attn_nofa_split_oproj_decode(pkg, backend, orc, n_kv, H, Hkv, M, wt, mask_t):
+    """Round 5: the -fa 0 decode chain MUL_MAT(k, q) -> SOFT_MAX -> MUL_MAT(v^T, p) ->
+    PERMUTE -> CONT -> RESHAPE -> MUL_MAT(wo) -> ADD(residual) of one token as split partials
+    of 64 keys (k_nofa_part) merged in the output projection's prologue (XStage::fap) —
+    the default for caches of <= 512 keys (ops_fattn_dec.hip nofa_split_o) — against the
+    node-by-node semantics in float64 (q rounded to f16, p normalised then rounded to f16 as
+    the node chain does; the partial form keeps p in f32) and against the chain kernel path
+    (g_tune[38] = 1)"""
+    D = 128
+    rng = np.random.default_rng(n_kv * 3 + H + M)
+    q = rng.standard_normal((H, 1, D)).astype(np.float32)
+    k = rng.standard_normal((Hkv, n_kv, D)).astype(np.float16)
+    vt = rng.standard_normal((Hkv, D, n_kv)).astype(np.float16)
+    mask = np.zeros((1, n_kv), np.float32)
+    mask[0, n_kv - 7:] = -np.inf
+    scale = 1.0 / np.sqrt(D)
+    K = D * H
+    tw_t = NAMES[wt]
+    w, rb = rand_quant(tw_t, M, K, rng)
+    r = rng.standard_normal((1, M)).astype(np.float32)
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, 1, H)
+        tk = ctx.new_tensor("f16", D, n_kv, Hkv)
+        tv = ctx.new_tensor("f16", n_kv, D, Hkv)
+        tm = ctx.new_tensor(mask_t, n_kv, 1) if mask_t else None
+        tw = ctx.new_tensor(tw_t, K, M)
+        tr = ctx.new_tensor("f32", M, 1)
+        kq = ctx.mul_mat(tk, tq)
+        sm = ctx.soft_max_ext(kq, tm, scale)
+        kqv = ctx.mul_mat(tv, sm)
+        out = ctx.cont(ctx.permute(kqv, 0, 2, 1, 3))
+        y = ctx.add(ctx.mul_mat(tw, ctx.reshape(out, K, 1)), tr)
+        feed = [(tq, q), (tk, k.view(np.uint16)), (tv, vt.view(np.uint16)), (tw, w), (tr, r)]
+        if mask_t:
+            feed.append((tm, mask if mask_t == "f32" else mask.astype(np.float16).view(np.uint16)))
+        return [y], feed
+
+    lib = pkg._lib.load()
+    try:
+        backend.klog(True)
+        y = run(pkg, backend, build)[0].reshape(M)
+        log = backend.klog_read()
+        backend.klog(False)
+        assert any(l.startswith("attn_nofa_part ") and f"nsplit={n_kv // 64}" in l for l in log), log
+        assert any(l.startswith("gemv2 ") and "epi=2" in l and (" mode=8 " in l or " mode=9 " in l) for l in log), log
+        lib.ggml_backend_mi355x_set_tune(38, 1)
+        backend.klog(True)
+        y2 = run(pkg, backend, build)[0].reshape(M)
+        log2 = backend.klog_read()
+        backend.klog(False)
+        assert not any(l.startswith("attn_nofa_part ") for l in log2), log2
+    finally:
+        lib.ggml_backend_mi355x_set_tune(38, 0)
+    G = H // Hkv
+    att = np.empty((H, D))
+    for h in range(H):
+        s_ = (q[h, 0].astype(np.float16).astype(np.float64) @ k[h // G].astype(np.float64).T) * scale
+        if mask_t:
+            s_ = s_ + mask[0]
+        e = np.exp(s_ - s_.max())
+        pr = (e / e.sum()).astype(np.float16).astype(np.float64)
+        att[h] = vt[h // G].astype(np.float64) @ pr
+    ref = orc.mul_mat(tw_t, w, rb, att.reshape(1, K).astype(np.float32), exact=True)[0] + r[0]
+    assert np.all(np.isfinite(y))
+    assert nmse(y, ref) < 5e-4, nmse(y, ref)
+    assert nmse(y2, ref) < 5e-4, nmse(y2, ref)
+    assert nmse(y, y2) < 1e-4, nmse(y, y2)
