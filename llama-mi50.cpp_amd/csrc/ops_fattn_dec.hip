@@ -977,7 +977,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec3(FaDecArgs p, int kps) {
 }
 
 // geometry: ~256 workgroups (one per CU), NS splits per KV head of kps keys each (a whole
-// number of 16 x NW-key workgroup stages). GGML_MI355X_FA_STREAM=0 / g_tune[34] = 1 off;
+// number of 16 x NW-key workgroup stages). GGML_MI355X_FA_STREAM=0 / g_tune[39] = 1 off;
 // g_tune[35] = minimum cache length in units of 256 keys (default 16384 keys).
 struct Fd3Cfg { int ns = 0, kps = 0, nw = 4, st = 4; };
 // geometry: 4 waves x 4 ring stages (one wave per SIMD), or g_tune[37] = 1: 8 waves x 2
@@ -990,7 +990,7 @@ static int fd3_geom() {
 static Fd3Cfg fd3_cfg(const ggml_tensor * dst) {
     static const bool off = [] { const char * v = getenv("GGML_MI355X_FA_STREAM"); return v && !strcmp(v, "0"); }();
     const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
-    if (off || g_tune[34] == 1 || !fa_dec2_ok(dst)) return {};
+    if (off || g_tune[39] == 1 || !fa_dec2_ok(dst)) return {};
     if (k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16 || k->ne[0] != 128 || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1) return {};
     if (m && (m->ne[3] != 1 || (uintptr_t) m->data % 4 || m->nb[1] % 4)) return {};
     const int64_t n_kv = k->ne[1], Hkv = k->ne[2];

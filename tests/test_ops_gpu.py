@@ -340,10 +340,10 @@ def test_flash_attn_stream(pkg, backend, orc, n_kv, H, Hkv, masked, stream):
     """long-cache decode attention: k_fattn_dec3 (one workgroup per CU streaming a key range
     of one KV head through its LDS-DMA ring, all Gt query heads, splits merged in-launch by
     the last arrival) — GQA 1 / 2 / 4 / 8, ragged last split, no mask; stream=False keeps
-    the round-3 LONG geometry + combine (g_tune[34] = 1) for comparison. Run twice: the
+    the round-3 LONG geometry + combine (g_tune[39] = 1) for comparison. Run twice: the
     arrival counters must be back at zero for the next launch / replay"""
     lib = pkg._lib.load()
-    lib.ggml_backend_mi355x_set_tune(34, 0 if stream else 1)
+    lib.ggml_backend_mi355x_set_tune(39, 0 if stream else 1)
     lib.ggml_backend_mi355x_set_tune(35, 8)          # from 2048 keys (the default starts at 16384)
     D = 128
     rng = np.random.default_rng(n_kv + H)
@@ -373,7 +373,7 @@ def test_flash_attn_stream(pkg, backend, orc, n_kv, H, Hkv, masked, stream):
         backend.klog(False)
         y2 = run(pkg, backend, build)[0].reshape(1, H, D)
     finally:
-        lib.ggml_backend_mi355x_set_tune(34, 0)
+        lib.ggml_backend_mi355x_set_tune(39, 0)
         lib.ggml_backend_mi355x_set_tune(35, 0)
     assert any(ln.startswith("fattn_dec3 ") for ln in log) == stream, log
     ref = orc.flash_attn(q, k, v, m16, scale)
