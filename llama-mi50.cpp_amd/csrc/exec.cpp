@@ -704,6 +704,11 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
                 const int k = try_fuse_mm_add(c, g, i, uses);
                 if (k) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; continue; }
             }
+            // q / k / v + RoPE + K/V stores of one token: one fused launch per slice (ops_qkv.hip)
+            if (!no_split_fusion && !g_no_qkv && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0]) && n->src[1]->ne[1] == 1) {
+                const int k = fuse_qkv_rope_store(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; continue; }
+            }
             // q / k / v (split MUL_MATs sharing src1, only views between): one fork / join
             if (!no_split_fusion && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0])) {
                 const int ng = try_split_group(c, g, i, done);

@@ -415,6 +415,28 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     else return 0;
     if (kq8 && (wk->ne[1] % 32 || wv->ne[1] % 32 || c.scratch->avail() < (size_t) 4 * (wk->ne[1] + wv->ne[1]) + 512)) return 0;
     for (const ggml_tensor * ix : {kix, vix}) if (ix->type != GGML_TYPE_I64) return 0;   // llama's KV indices
+    // Round 5, row-split weights (-sm row): q, k and v split alike, at head boundaries (the
+    // 256-row slice granule is a multiple of n_dims): one fused launch per slice on the
+    // slice device's own stream (split_fork / split_join), writing its q rows, its K / V
+    // cache columns and its RoPE on the main device through peer access — instead of 3
+    // GEMVs + 2 ROPE + 2 SET_ROWS launches per slice pair
+    const bool split = tensor_is_split(wq) || tensor_is_split(wk) || tensor_is_split(wv);
+    void * sd[3][MX_MAX_DEVICES];
+    int64_t slo[3][MX_MAX_DEVICES], shi[3][MX_MAX_DEVICES];
+    int sdev[3][MX_MAX_DEVICES], ns = 0;
+    if (split) {
+        const int n_dims_q = mx_op_param<int32_t>(rq, 1);
+        if (kq8 || !tensor_is_split(wq) || !tensor_is_split(wk) || !tensor_is_split(wv) || n_dims_q <= 0) return 0;
+        for (int t = 0; t < 3; ++t) {
+            const int n = split_slices(c.s, t == 0 ? wq : t == 1 ? wk : wv, sd[t], slo[t], shi[t], sdev[t]);
+            if (!n || (t && n != ns)) return 0;
+            ns = n;
+        }
+        for (int k = 0; k < ns; ++k) {
+            if (sdev[1][k] != sdev[0][k] || sdev[2][k] != sdev[0][k]) return 0;
+            if (slo[0][k] % n_dims_q || slo[1][k] % n_dims_q || (shi[0][k] - slo[0][k]) % 2 || (shi[1][k] - slo[1][k]) % 2) return 0;
+        }
+    }
 
     QkvArgs p{};
     const ggml_tensor * ws[3] = {wq, wk, wv};
@@ -514,6 +536,32 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     if (kq8) {
         p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
         p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
+    }
+    if (split) {
+        int remote = 0;
+        for (int k = 0; k < ns; ++k) remote += !split_on_main(c.s, wq, sdev[0][k]);
+        MX_KLOG("qkv_split qta=%d qtk=%d qtv=%d mode=%d K=%d slices=%d remote=%d", ta, tk, tv, mode, p.K, ns, remote);
+        for (int k = 0; k < ns; ++k) {
+            QkvArgs ps = p;
+            for (int t = 0; t < 3; ++t) { ps.w[t] = (const char *) sd[t][k]; ps.rows[t] = (int) (shi[t][k] - slo[t][k]); }
+            ps.nblk_q = (int) mx_ceil_div(ps.rows[0], rba);
+            ps.nblk_k = (int) mx_ceil_div(ps.rows[1], rba);
+            const int nbv = (int) mx_ceil_div(ps.rows[2], rbv);
+            ps.q_out = p.q_out + slo[0][k];
+            ps.kc = p.kc + slo[1][k] * 2;
+            if (v_trans) ps.vidx = p.vidx + slo[2][k] * 8;      // one I64 cache index per V element
+            else ps.vc = p.vc + slo[2][k] * 2;
+            const dim3 gs((unsigned) (ps.nblk_q + ps.nblk_k + nbv));
+            if (split_on_main(c.s, wq, sdev[0][k])) {
+                hipLaunchKernelGGL(kern, gs, dim3(nthr), gemv_lds_bytes(p.K, mode), c.st, ps);
+                continue;
+            }
+            OpCtx dc = split_fork(c, sdev[0][k]);
+            hipLaunchKernelGGL(kern, gs, dim3(nthr), gemv_lds_bytes(p.K, mode), dc.st, ps);
+        }
+        for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, wq, sdev[0][k])) split_join(c, sdev[0][k]);
+        HIP_CHECK(hipSetDevice(c.s->device));
+        return last - i + 1;
     }
     MX_KLOG("qkv qta=%d qtk=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d bal=%d", ta, tk, tv, mode, cfg, p.K, (int) kq8, (int) (nthr == 448));
     hipLaunchKernelGGL(kern, grid, dim3(nthr), gemv_lds_bytes(p.K, mode), c.st, p);

@@ -183,6 +183,34 @@ def test_llama3_8b_width_decode_at_depth(l8b, tmp_path):
     assert k["mmvq1"] == 0, k
 
 
+@pytest.mark.parametrize("fa", [1, 0])
+@pytest.mark.parametrize("ts", ["1,1", "1,1,1,1"])
+def test_llama3_8b_width_row_split_decode(l8b, tmp_path, ts, fa):
+    """-sm row at the 8B widths over 2 / 4 logical devices under GGML_MI355X_FORCE_PEER (the
+    branch separate GPUs with peer access take): q/k/v + RoPE + K/V stores run as ONE fused
+    launch per slice (round 5, ops_qkv.hip: slices split at head boundaries), the other
+    slices on their devices' own streams; -fa 0 stores V transposed (per-element cache
+    indices). Logits against the reference CPU backend; graph capture on (the production
+    path on one GPU)."""
+    n_dev = len(ts.split(","))
+    toks = np.random.default_rng(25).integers(0, 128000, 10)
+    cpu, _, _ = run_ref(tmp_path, l8b, toks, 0, fa, incremental=True)
+    env = {"GGML_MI355X_VIRTUAL_DEVICES": str(n_dev), "GGML_MI355X_FORCE_PEER": "1"}
+    gpu, log, klog = run_ref(tmp_path, l8b, toks, 99, fa, incremental=True, extra=("-sm", "row", "-ts", ts),
+                             env_extra=env, tag=f"rs{n_dev}")
+    assert "MI355X" in log, log[-2000:]
+    assert np.all(np.isfinite(gpu))
+    err = nmse(gpu, cpu)
+    assert err < TOL, err
+    qs = [ln for ln in klog if ln.startswith("qkv_split ")]
+    # one fused launch set per decoded token and layer (the capture repeats the eager pass's
+    # choices without logging them: at least one token's worth)
+    assert len(qs) >= 2, klog[-40:]
+    sr = [tuple(map(int, re.search(r"slices=(\d+) remote=(\d+)", ln).groups())) for ln in qs]
+    assert all(a == n_dev and b == n_dev - 1 for a, b in sr), sr[:4]
+    assert not any(ln.startswith("qkv ") for ln in klog), klog[-40:]
+
+
 def test_llama3_8b_width_decode_graph_replay(l8b, tmp_path):
     """the production path: decode captured into a hipGraph and replayed per token"""
     toks = np.random.default_rng(22).integers(0, 128000, 10)
