@@ -222,7 +222,9 @@ bool gemv2_stage(OpCtx & c, const ggml_tensor * x, std::initializer_list<const g
 // GEMV absorbs) and overwrites nothing a deferred norm still needs
 static void deferred_guard_node(OpCtx & c, const ggml_tensor * n) {
     if (c.s->deferred.empty()) return;
-    const bool absorbs = n->op == GGML_OP_MUL_MAT && g_gemv2 && gemv2_ok(n->src[0], n->src[1], n);
+    // (a row-split MUL_MAT's slices run through op_mul_mat on other streams, which see no
+    // deferred norm: it absorbs nothing; the fused per-slice launches stage x on this stream)
+    const bool absorbs = n->op == GGML_OP_MUL_MAT && g_gemv2 && gemv2_ok(n->src[0], n->src[1], n) && !tensor_is_split(n->src[0]);
     for (size_t k = 0; k < c.s->deferred.size();) {
         bool hit = false;
         for (int j = 0; j < GGML_MAX_SRC && !hit; ++j) {
@@ -693,26 +695,32 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         else if (n->op == GGML_OP_MUL_MAT && n->src[0]->type == GGML_TYPE_F16 && n->src[1]->ne[1] == 1) fa_prefetch_plan(s, g, i, 1, true);
         s->gpf_armed = s->gpf_node && n == s->gpf_node;
         if (s->use_fusion && s->split_graph) {
-            // row-split weights: the fusions that touch no MUL_MAT (split or not: a split
-            // slice runs on its device's own stream, which no deferred norm reaches)
+            // row-split weights: the RMS norm deferred into the fused per-slice launches that
+            // consume it (QKV, SwiGLU: their x staging runs on this stream and goes to every
+            // slice); any other consumer materialises it first (deferred_guard_node: a split
+            // MUL_MAT absorbs nothing). GGML_MI355X_NO_SPLIT_DEFER=1: the round-5 first form
+            // (RMS_NORM + MUL materialised by one launch)
+            static const bool no_split_defer = getenv("GGML_MI355X_NO_SPLIT_DEFER") != nullptr;
+            const int i0 = i;
+            if (!no_split_defer && n->op == GGML_OP_RMS_NORM && try_defer_norm(c, g, i, uses)) { i += 1; s->n_fused += 2; s->n_nodes_run += 2; continue; }
             if (n->op == GGML_OP_RMS_NORM && try_fuse_rms_mul(c, g, i, uses)) { i += 1; s->n_fused += 1; s->n_nodes_run += 2; continue; }
             // decode gate/up/SwiGLU and MUL_MAT -> ADD over row-split weights whose slices are
             // on this GPU: the SwiGLU / residual GEMV per slice (mmvq_fused_glu / _add)
             static const bool no_split_fusion = getenv("GGML_MI355X_NO_SPLIT_FUSION") != nullptr;   // A/B
             if (!no_split_fusion && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0]) && mmvq_small_batch_ok(n)) {
-                if (try_fuse_glu(c, g, i, uses, true)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
+                if (try_fuse_glu(c, g, i, uses, true)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
                 const int k = try_fuse_mm_add(c, g, i, uses);
-                if (k) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; continue; }
+                if (k) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; deferred_retire(s, g, i0, i); continue; }
             }
             // q / k / v + RoPE + K/V stores of one token: one fused launch per slice (ops_qkv.hip)
             if (!no_split_fusion && !g_no_qkv && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0]) && n->src[1]->ne[1] == 1) {
                 const int k = fuse_qkv_rope_store(c, g, i, uses);
-                if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; continue; }
+                if (k > 0) { i += k - 1; s->n_fused += 6; s->n_nodes_run += 7; deferred_retire(s, g, i0, i); continue; }
             }
             // q / k / v (split MUL_MATs sharing src1, only views between): one fork / join
             if (!no_split_fusion && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0])) {
                 const int ng = try_split_group(c, g, i, done);
-                if (ng > 1) { s->n_nodes_run += ng; continue; }
+                if (ng > 1) { s->n_nodes_run += ng; deferred_retire(s, g, i0, i); continue; }
             }
         } else if (s->use_fusion) {
             const int i0 = i;

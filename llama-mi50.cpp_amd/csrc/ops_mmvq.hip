@@ -355,7 +355,7 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up,
             gv[k].nb[1] = gv[k].nb[2] = gv[k].nb[3] = (size_t) rows * 4;
             if (!gemv2_ok(&ws[0][k], x, &gv[k])) return false;
         }
-        if (!gemv2_stage(c, x, {glu}, {}, &xs)) return false;
+        if (!gemv2_stage(c, x, {glu}, {}, &xs, 2)) return false;
         ActQ * q8 = wg->ne[1] % 32 == 0 ? act_cache_alloc(c.s, glu) : nullptr;
         if (q8 && xs.q8 == q8->q) q8 = nullptr;
         MX_KLOG("glu_split M=%lld K=%lld slices=%d remote=%d q8o=%d", (long long) wg->ne[1], (long long) wg->ne[0], ns, remote, q8 != nullptr);
