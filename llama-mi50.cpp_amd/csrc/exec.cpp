@@ -414,7 +414,7 @@ static int fuse_attn_split_o(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     }
     if (!mm || rs->op != GGML_OP_RESHAPE || rs->ne[0] != D * H || mx_nrows(rs) != 1 || uses[rs] != 1 || (rs->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
     const ggml_tensor * wo = mm->src[0];
-    if (tensor_is_split(wo) || !gemv2_ok(wo, rs, mm) || !gemv2_fap_ok(wo->type, wo->ne[0], wo->ne[1])) return 0;
+    if (!gemv2_fap_o_ok(c.s, wo, rs, mm)) return 0;
     if (uses[mm] != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
     // the tail: ADD(mm, res) right after, or GET_ROWS(mm) , GET_ROWS(res) -> ADD
     const ggml_tensor * res = nullptr;
@@ -458,8 +458,8 @@ static int fuse_attn_split_o(OpCtx & c, ggml_cgraph * g, int i, UseMap & uses) {
     XStage xs{nullptr, nullptr, 0.0f, 0};
     xs.xcd = g_tune[15] != 1;
     xs.fap = part; xs.fap_ns = ns; xs.fap_d = (int) D;
-    c.s->gpf_armed = c.s->gpf_node && c.s->gpf_node == mm;   // the second prefetch stage rides on this GEMV
-    gemv2_launch(c, wo, nullptr, xs, (float *) add->data, (const float *) res->data);
+    c.s->gpf_armed = c.s->gpf_node && c.s->gpf_node == mm && !tensor_is_split(wo);   // the second prefetch stage rides on this GEMV
+    gemv2_fap_o_launch(c, wo, xs, (float *) add->data, (const float *) res->data);
     return last - i + 1;
 }
 
@@ -711,6 +711,16 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
                 if (try_fuse_glu(c, g, i, uses, true)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
                 const int k = try_fuse_mm_add(c, g, i, uses);
                 if (k) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; deferred_retire(s, g, i0, i); continue; }
+            }
+            // decode attention as split partials merged in each O-projection slice's prologue
+            // (-fa 1: fuse_attn_split_o; -fa 0: the chain's split partials, ops_fattn_dec.hip)
+            if (!no_split_fusion && n->op == GGML_OP_FLASH_ATTN_EXT) {
+                const int k = fuse_attn_split_o(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
+            }
+            if (!no_split_fusion && !g_no_attn_nofa && n->op == GGML_OP_MUL_MAT && !tensor_is_split(n->src[0])) {
+                const int k = fuse_attn_nofa(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += 3; s->n_nodes_run += 4; deferred_retire(s, g, i0, i); continue; }
             }
             // q / k / v + RoPE + K/V stores of one token: one fused launch per slice (ops_qkv.hip)
             if (!no_split_fusion && !g_no_qkv && n->op == GGML_OP_MUL_MAT && tensor_is_split(n->src[0]) && n->src[1]->ne[1] == 1) {

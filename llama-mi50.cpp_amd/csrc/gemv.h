@@ -45,6 +45,10 @@ bool gemv2_ok(const ggml_tensor * w, const ggml_tensor * x, const ggml_tensor * 
 bool gemv2_moe(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * w2, ggml_tensor * dst, ActQ * q8out = nullptr);
 void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, const XStage & xs, float * dst,
                   const float * res, ActQ * q8out = nullptr);
+// the output projection over attention split partials (xs.fap) + residual, wo plain or
+// row-split (one launch per slice on its device's stream)
+bool gemv2_fap_o_ok(const Stream * s, const ggml_tensor * wo, const ggml_tensor * x, const ggml_tensor * mm);
+void gemv2_fap_o_launch(OpCtx & c, const ggml_tensor * wo, const XStage & xs, float * add, const float * res);
 
 // The activation a GEMV should stage for src1: the deferred RMS_NORM→MUL pair that
 // produces src1 when there is one (exec.cpp), else src1 itself.

@@ -1552,7 +1552,7 @@ static int nofa_split_o(OpCtx & c, ggml_cgraph * g, int i, int last, const NfArg
     if (x != out && (x->op != GGML_OP_RESHAPE || use(x) != 1 || (x->flags & GGML_TENSOR_FLAG_OUTPUT))) return 0;
     if (mx_nelements(x) != (int64_t) D * H || mx_nrows(x) != 1) return 0;
     const ggml_tensor * wo = mm->src[0];
-    if (tensor_is_split(wo) || !gemv2_ok(wo, x, mm) || !gemv2_fap_ok(wo->type, wo->ne[0], wo->ne[1])) return 0;
+    if (!gemv2_fap_o_ok(c.s, wo, x, mm)) return 0;
     if (use(mm) != 1 || (mm->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
     // the tail: ADD(mm, res) right after, or (the last layer) libllama's one-row inp_out_ids
     // pair GET_ROWS(mm), GET_ROWS(res) -> ADD: one token, both GET_ROWS are the identity
@@ -1597,7 +1597,7 @@ static int nofa_split_o(OpCtx & c, ggml_cgraph * g, int i, int last, const NfArg
     XStage xs{nullptr, nullptr, 0.0f, 0};
     xs.xcd = g_tune[15] != 1;
     xs.fap = part; xs.fap_ns = ns; xs.fap_d = D;
-    gemv2_launch(c, wo, nullptr, xs, (float *) add->data, (const float *) res->data);
+    gemv2_fap_o_launch(c, wo, xs, (float *) add->data, (const float *) res->data);
     return lastn - i + 1;
 }
 void fa_mma_nofa_launch(OpCtx & c, const ggml_tensor * q, const ggml_tensor * k, const ggml_tensor * v, const ggml_tensor * m,

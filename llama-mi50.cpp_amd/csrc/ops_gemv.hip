@@ -302,6 +302,46 @@ static void gemv2_launch_p(OpCtx & c, G2Args & p, int type, bool glu, bool res) 
 #undef TY
 }
 
+// The output projection that merges the decode attention's split partials (xs.fap) in its
+// prologue, + residual: one launch, or (round 5, -sm row) one per row-split slice of wo, each
+// on its device's own stream (split_fork / split_join, as mmvq_fused_add), every slice merging
+// the partials itself and writing its rows of `add` on the main device
+bool gemv2_fap_o_ok(const Stream * s, const ggml_tensor * wo, const ggml_tensor * x, const ggml_tensor * mm) {
+    if (!gemv2_ok(wo, x, mm)) return false;
+    if (!tensor_is_split(wo)) return gemv2_fap_ok(wo->type, wo->ne[0], wo->ne[1]);
+    void * sd[MX_MAX_DEVICES];
+    int64_t lo[MX_MAX_DEVICES], hi[MX_MAX_DEVICES];
+    int dv[MX_MAX_DEVICES];
+    const int ns = split_slices(s, wo, sd, lo, hi, dv);
+    for (int k = 0; k < ns; ++k) if (!gemv2_fap_ok(wo->type, wo->ne[0], hi[k] - lo[k])) return false;
+    return ns > 0;
+}
+
+void gemv2_fap_o_launch(OpCtx & c, const ggml_tensor * wo, const XStage & xs, float * add, const float * res) {
+    if (!tensor_is_split(wo)) { gemv2_launch(c, wo, nullptr, xs, add, res); return; }
+    void * sd[MX_MAX_DEVICES];
+    int64_t lo[MX_MAX_DEVICES], hi[MX_MAX_DEVICES];
+    int dv[MX_MAX_DEVICES];
+    const int ns = split_slices(c.s, wo, sd, lo, hi, dv);
+    MX_ASSERT(ns > 0);
+    ggml_tensor ws[MX_MAX_DEVICES];
+    int remote = 0;
+    for (int k = 0; k < ns; ++k) {
+        const int64_t rows = hi[k] - lo[k];
+        ws[k] = *wo; ws[k].ne[1] = rows; ws[k].nb[2] = ws[k].nb[3] = ws[k].nb[1] * rows; ws[k].data = sd[k];
+        ws[k].buffer = nullptr; ws[k].extra = nullptr; ws[k].view_src = nullptr;
+        remote += !split_on_main(c.s, wo, dv[k]);
+    }
+    MX_KLOG("fap_split M=%lld slices=%d remote=%d", (long long) wo->ne[1], ns, remote);
+    for (int k = 0; k < ns; ++k) {
+        if (split_on_main(c.s, wo, dv[k])) { gemv2_launch(c, &ws[k], nullptr, xs, add + lo[k], res + lo[k]); continue; }
+        OpCtx dc = split_fork(c, dv[k]);
+        gemv2_launch(dc, &ws[k], nullptr, xs, add + lo[k], res + lo[k]);
+    }
+    for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, wo, dv[k])) split_join(c, dv[k]);
+    HIP_CHECK(hipSetDevice(c.s->device));
+}
+
 // MUL_MAT_ID of a decode step (n_tok <= 8): one v2 GEMV launch, grid.y = (slot, token)
 // items, the expert of each read on the device. gate/up (w2 != null): silu(Wg x) * (Wu x)
 // of the two MUL_MAT_IDs in one pass (and the q8 of the result for the down projection's

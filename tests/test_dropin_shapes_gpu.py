@@ -190,7 +190,7 @@ def test_llama3_8b_width_row_split_decode(l8b, tmp_path, ts, fa):
     branch separate GPUs with peer access take): q/k/v + RoPE + K/V stores run as ONE fused
     launch per slice (round 5, ops_qkv.hip: slices split at head boundaries), the other
     slices on their devices' own streams; -fa 0 stores V transposed (per-element cache
-    indices). Logits against the reference CPU backend; graph capture on (the production
+    indices); the attention's split partials are merged by every O-projection slice. Logits against the reference CPU backend; graph capture on (the production
     path on one GPU)."""
     n_dev = len(ts.split(","))
     toks = np.random.default_rng(25).integers(0, 128000, 10)
@@ -209,6 +209,10 @@ def test_llama3_8b_width_row_split_decode(l8b, tmp_path, ts, fa):
     sr = [tuple(map(int, re.search(r"slices=(\d+) remote=(\d+)", ln).groups())) for ln in qs]
     assert all(a == n_dev and b == n_dev - 1 for a, b in sr), sr[:4]
     assert not any(ln.startswith("qkv ") for ln in klog), klog[-40:]
+    # the attention's split partials merged by every O-projection slice (-fa 1 and -fa 0)
+    fs = [ln for ln in klog if ln.startswith("fap_split ")]
+    assert len(fs) >= 2 and all(f"slices={n_dev} remote={n_dev - 1}" in ln for ln in fs), klog[-40:]
+    assert any(ln.startswith("fattn_dec2_part " if fa else "attn_nofa_part ") for ln in klog), klog[-40:]
 
 
 def test_llama3_8b_width_decode_graph_replay(l8b, tmp_path):
