@@ -158,6 +158,7 @@ XStage xstage_of(Stream * s, const ggml_tensor * x) {
             xs.dbg = MX_AB_VARIANTS ? g_tune[11] : 0;
             xs.xcd = g_tune[15] != 1;
             xs.drain = g_tune[14] == 1;
+            xs.postscale = g_tune[42] != 1;
             return xs;
         }
     XStage xs{(const float *) x->data, nullptr, 0.0f, 0};

@@ -420,6 +420,19 @@ __device__ __forceinline__ void stage_finish(const XStage & xs, int K, const Lds
         }
         ss = wave_sum(ss);
         if ((t & 63) == 0) red[t >> 6] = ss;
+        if (xs.postscale) {   // block-uniform: quantise x * nw now, s after the dots (XStage)
+#pragma unroll
+            for (int h = 0; h < HPT; ++h) {
+                const int hg = t + NT * h;
+                if (hg < nhg) {
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) r.v[h][j] *= r.w[h][j];
+                    q8_half(r.v[h], hg, a);
+                }
+            }
+            lds_barrier();    // the q8 image and the per-wave sums of squares
+            return;
+        }
         lds_barrier();
         ss = 0.f;
 #pragma unroll
@@ -734,6 +747,16 @@ __device__ __forceinline__ void gemv_rows_staged(const char * const (&rows)[NM],
     // (sub == LPR - 1) for LPR = 32, 64
 #pragma unroll
     for (int m = 0; m < NM; ++m) acc[m] = dpp_sum_group<LPR>(acc[m]);
+    if constexpr (xs_norm(MODE)) {
+        if (xs.postscale && !MX_DBG(xs.dbg & 1)) {   // the RMS scale of the prologue's quantisation (stage_finish)
+            float ss = 0.f;
+#pragma unroll
+            for (int wv = 0; wv < NT / 64; ++wv) ss += red[wv];
+            const float scale = __builtin_amdgcn_rsqf(ss / (float) K + xs.eps);
+#pragma unroll
+            for (int m = 0; m < NM; ++m) acc[m] *= scale;
+        }
+    }
 }
 
 template <int QT, int LPR, int UPL, int NM, int NT, int MODE, typename F = NoFence>

@@ -30,6 +30,14 @@ struct XStage {
     // and the sum
     const float * fap = nullptr;
     int fap_ns = 0, fap_d = 0;
+    // round 5: register-staged norm sources (XS_NORM / XS_NORM_H2: the QKV block) quantise x * nw without the
+    // RMS scale s and multiply the row sums by s after the dot products: the q8 values of
+    // (x s) nw and of x nw are the same (amax scales with them), only the block scales carry
+    // s, and the dot is linear in them — so the prologue needs no barrier for the sum of
+    // squares before quantising. 0: scale first (g_tune[42] = 1, A/B). The LDS-DMA-staged
+    // form (XS_NORM_LDS, the SwiGLU) keeps the scale first: post-scaled it ran 2 % slower
+    // (tg128 625-628 vs 641-642, profiles/r05/norm_postscale_ab.txt)
+    int postscale = 1;
 };
 
 extern int g_tune[48];      // launch-geometry overrides (ggml_backend_mi355x_set_tune)
