@@ -233,23 +233,28 @@ def ref_bench(gguf, env, flags, timeout=900):
     if bench_tool() == "llama-bench":
         fl = []
         i = 0
+        tname = {"8": "q8_0", "2": "q4_0", "1": "f16", "30": "bf16"}
+        has_ctv = "-ctv" in flags
         while i < len(flags):
             if flags[i] == "-c":
                 i += 2
                 continue
-            if flags[i] == "-ctk":   # the restatement takes a ggml_type id, llama-bench a name for K and V
-                name = {"8": "q8_0", "2": "q4_0", "1": "f16", "30": "bf16"}.get(flags[i + 1], flags[i + 1])
-                fl += ["-ctk", name, "-ctv", name]
+            if flags[i] in ("-ctk", "-ctv"):   # the restatement takes ggml_type ids (-ctk: K and V), llama-bench names
+                name = tname.get(flags[i + 1], flags[i + 1])
+                fl += [flags[i], name] + (["-ctv", name] if flags[i] == "-ctk" and not has_ctv else [])
                 i += 2
                 continue
             fl.append(flags[i])
             i += 1
-        r = subprocess.run([LLAMA_BENCH, "-m", gguf, "-o", "jsonl"] + fl, capture_output=True, text=True,
+        # -v: llama-bench keeps libllama's log (only that: llama-bench.cpp:2067), whose
+        # "graph splits = N" per context shows any node that fell back to the CPU backend
+        r = subprocess.run([LLAMA_BENCH, "-m", gguf, "-o", "jsonl", "-v"] + fl, capture_output=True, text=True,
                            timeout=timeout, env=env)
         lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
         if r.returncode != 0 or not lines:
             return f"failed rc={r.returncode}: {r.stderr[-300:]}", r.stderr
-        res = {"tool": "llama-bench", "pp_tok_s": 0.0, "tg_tok_s": 0.0, "pp_samples": [], "tg_samples": []}
+        res = {"tool": "llama-bench", "pp_tok_s": 0.0, "tg_tok_s": 0.0, "pp_samples": [], "tg_samples": [],
+               "graph_splits": graph_splits(r.stderr)}
         for t in lines:
             kind = "tg" if t["n_gen"] > 0 and t["n_prompt"] == 0 else "pp"
             res[f"{kind}_tok_s"] = t["avg_ts"]
@@ -262,7 +267,15 @@ def ref_bench(gguf, env, flags, timeout=900):
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not line:
         return f"failed rc={r.returncode}: {r.stderr[-300:]}", r.stderr
-    return json.loads(line[-1]), r.stderr
+    return dict(json.loads(line[-1]), graph_splits=graph_splits(r.stderr)), r.stderr
+
+
+def graph_splits(stderr):
+    """libllama's "graph splits = N" counts (src/llama-context.cpp:523-533), one per context
+    reserve: 2 = CPU input embedding + MI355X, i.e. no node fell back to the CPU backend"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dropin_util
+    return sorted(set(dropin_util.graph_splits(stderr)))
 
 
 def tg_from_samples(samples, n_tok):
@@ -288,7 +301,8 @@ def dropin_tg(args, env, flags, key):
     st = [json.loads(x.split("stats ", 1)[1]) for x in err.splitlines() if "[mi355x] stats" in x]
     st.sort(key=lambda e: -e.get("graph_compute", 0))   # the decode context's backend (llama-bench frees several)
     return {"key": key, "tok_s": value, "ms_per_step": ms, "samples": res["tg_samples"], "avg_ts": res["tg_tok_s"],
-            "tool": bench_tool(), "test": res.get("tg_test"), "wall_s_incl_load": round(wall, 2), "executor": st[0] if st else None}
+            "tool": bench_tool(), "test": res.get("tg_test"), "wall_s_incl_load": round(wall, 2), "executor": st[0] if st else None,
+            "graph_splits": res.get("graph_splits")}
 
 
 def dropin_bench(args, skip=()):
@@ -297,7 +311,8 @@ def dropin_bench(args, skip=()):
     tools/llama-bench/llama-bench.cpp:1962-2010, warmup + -r repetitions) loads
     libggml-mi355x.so through GGML_BACKEND_PATH with every layer offloaded (-ngl 99), on
     the same Llama-3-8B Q4_K_M GGUF. The extra legs beside the headline: tg128 at -fa 0
-    and with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv), pp512 at each, pp2048
+    and with a q8_0 KV cache (-ctk q8_0 -ctv q8_0: keys *_q8kv; -ctk q8_0 -ctv f16, the fork's
+    line: *_q8k_f16v), pp512 at each, pp2048
     (-b 2048 -ub 512, BASELINE configs[2]), tg128 at depth (-d: llama-bench.cpp:2191-2226,
     the KV cache filled with D tokens first)."""
     if not (os.path.exists(REF_BENCH) or os.path.exists(LLAMA_BENCH)) or args.no_dropin:
@@ -309,15 +324,17 @@ def dropin_bench(args, skip=()):
         env = dict(os.environ, GGML_BACKEND_PATH=LIB, GGML_MI355X_STATS="1")
         base = ["-t", "8", "-ngl", "99", "-r", args.dropin_reps]
         runs = []
-        for fa, ctk in ((1, None), (0, None), (1, 8)):        # 8 = GGML_TYPE_Q8_0
+        # K / V cache types (ggml ids, 8 = q8_0, 1 = f16): f16, q8_0 / q8_0, and (round 6) the
+        # fork's own line -ctk q8_0 -ctv f16 (AGENTS.md:166-176)
+        for fa, ctk, ctv, tag in ((1, None, None, ""), (0, None, None, ""), (1, 8, 8, "_q8kv"), (1, 8, 1, "_q8k_f16v")):
             for test, pp, tg in (("tg128", 0, args.tg), ("pp512", args.pp, 0)):
                 if (pp or tg) == 0:
                     continue
-                key = f"{test}_fa{fa}" + ("_q8kv" if ctk else "")
+                key = f"{test}_fa{fa}{tag}"
                 if key in skip:
                     continue
                 runs.append((key, tg > 0, ["-fa", fa, "-p", pp, "-n", tg, "-c", max(256, pp + tg)] +
-                             (["-ctk", ctk] if ctk else [])))
+                             (["-ctk", ctk, "-ctv", ctv] if ctk else [])))
         if args.pp2048:
             for fa in (1, 0):
                 runs.append((f"pp2048_fa{fa}", False, ["-fa", fa, "-p", 2048, "-n", 0, "-b", 2048, "-ub", 512, "-c", 2304]))
@@ -330,6 +347,7 @@ def dropin_bench(args, skip=()):
                 continue
             out[f"{key}_tok_s"] = res["tg_tok_s"] if is_tg else res["pp_tok_s"]
             out[f"{key}_samples"] = res["tg_samples"] if is_tg else res["pp_samples"]
+            out[f"{key}_graph_splits"] = res.get("graph_splits")
     except Exception as e:  # noqa: BLE001
         out["error"] = str(e)
     return out

@@ -10,6 +10,7 @@
 #include "backend.h"
 #include "ggml_mi355x.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <mutex>
@@ -166,9 +167,33 @@ static void staged_writes_pending_wait(int dev, hipStream_t stream) {
 // ---------------------------------------------------------------------------
 // device buffers
 // ---------------------------------------------------------------------------
+// Staged writes into this buffer that are still queued (be_sync no longer flushes, round 5)
+// or flushed but in flight must land before the memory goes back: otherwise the later
+// k_stage_flush writes into a freed range — or into the next allocation at that address.
+// Queued ranges inside the buffer are dropped (the buffer's contents die with it); any in
+// flight are waited for.
+static void stage_release_range(int dev, const char * lo, const char * hi) {
+    if (dev < 0 || dev >= MX_MAX_DEVICES) return;
+    Staging & st = g_stage[dev];
+    std::lock_guard<std::mutex> lk(st.mu);
+    st.queued.erase(std::remove_if(st.queued.begin(), st.queued.end(),
+                                   [&](const StageEntry & e) { return e.dst >= lo && e.dst + e.n <= hi; }),
+                    st.queued.end());
+    bool overlap = false;   // (a range straddling the buffer's edge: flush it, it writes a neighbour too)
+    for (const StageEntry & e : st.queued) overlap |= e.dst < hi && lo < e.dst + e.n;
+    if (overlap) stage_flush_locked(st);
+    if (st.pending) {
+        HIP_CHECK(hipEventSynchronize(st.ev));
+        st.pending = false;
+    }
+}
 static void buf_free(ggml_backend_buffer_t b) {
     BufferCtx * c = (BufferCtx *) b->context;
-    if (c->base) { hipSetDevice(c->device); hipFree(c->base); }
+    if (c->base) {
+        hipSetDevice(c->device);
+        stage_release_range(c->device, (const char *) c->base, (const char *) c->base + c->size);
+        hipFree(c->base);
+    }
     delete c;
 }
 static void * buf_base(ggml_backend_buffer_t b) { return ((BufferCtx *) b->context)->base; }
@@ -479,7 +504,24 @@ static ggml_backend_buffer_type_t dv_host_buft(ggml_backend_dev_t d) { return &d
 // Row-split weights (split.cpp) serve one op only: MUL_MAT's src0, a 2D matrix, run from
 // the split's main device with an f32 activation (the reference's CUDA rule,
 // ggml_backend_cuda_device_supports_op).
+// GGML_MI355X_REFUSE_OP=<op name> (ggml_op_name, e.g. FLASH_ATTN_EXT): report that op as
+// unsupported — test infrastructure for the graph-split assertions of the drop-in tests
+// (the scheduler then runs it on the CPU backend, which must show as extra splits)
+static bool refused_op(const ggml_tensor * op) {
+    static const int refuse = [] {
+        const char * r = getenv("GGML_MI355X_REFUSE_OP");
+        if (!r || !*r) return -1;
+        static const struct { const char * name; int op; } names[] = {
+            {"FLASH_ATTN_EXT", GGML_OP_FLASH_ATTN_EXT}, {"MUL_MAT", GGML_OP_MUL_MAT}, {"MUL_MAT_ID", GGML_OP_MUL_MAT_ID},
+            {"ROPE", GGML_OP_ROPE}, {"RMS_NORM", GGML_OP_RMS_NORM}, {"SOFT_MAX", GGML_OP_SOFT_MAX}, {"SET_ROWS", GGML_OP_SET_ROWS},
+        };
+        for (const auto & n : names) if (strcmp(r, n.name) == 0) return n.op;
+        return atoi(r);   // or the ggml_op enum value
+    }();
+    return refuse >= 0 && (int) op->op == refuse;
+}
 static bool dv_supports_op(ggml_backend_dev_t d, const ggml_tensor * op) {
+    if (refused_op(op)) return false;
     for (int i = 0; i < GGML_MAX_SRC; ++i) {
         const ggml_tensor * s = op->src[i];
         if (!s || !s->buffer || !buft_is_split(s->buffer->buft)) continue;

@@ -573,8 +573,8 @@ size_t flash_attn_scratch(const ggml_tensor * dst) {
     size_t need = nsplit * rows * (v->ne[0] + 2) * sizeof(float) + 4 * 256;
     if (fa_dec2_ok(dst)) need = std::max(need, fa_dec2_scratch(dst));
     const ggml_tensor * k = dst->src[1];
-    if (k->type != GGML_TYPE_F16 && fa_mma_ok(dst))      // f16 copies of quantised / bf16 K and V
-        need = std::max(need, (size_t) 2 * (mx_nelements(k) / k->ne[3]) * 2 + 512);
+    if ((k->type != GGML_TYPE_F16 || v->type != GGML_TYPE_F16) && fa_mma_ok(dst))   // f16 copies of quantised / bf16 K and / or V
+        need = std::max(need, (size_t) ((k->type != GGML_TYPE_F16) + (v->type != GGML_TYPE_F16)) * (mx_nelements(k) / k->ne[3]) * 2 + 512);
     return need;
 }
 
@@ -584,12 +584,18 @@ bool flash_attn_supported(const ggml_tensor * dst) {
     const ggml_tensor * v = dst->src[2];
     const ggml_tensor * m = dst->src[3];
     if (q->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
-    if (k->type != v->type) return false;
+    // K and V types: equal, or (round 6) any pair of f16 / q8_0 / q4_0 — the reference's
+    // GGML_CUDA_FA_ALL_QUANTS set the fork builds with (fattn.cu:220-260); its own llama-bench
+    // line is -ctk q8_0 -ctv f16 (AGENTS.md:166-176)
+    auto mixable = [](ggml_type t) { return t == GGML_TYPE_F16 || t == GGML_TYPE_Q8_0 || t == GGML_TYPE_Q4_0; };
+    if (k->type != v->type && !(mixable(k->type) && mixable(v->type))) return false;
     if (k->ne[0] != v->ne[0]) return false;
     const int64_t D = k->ne[0];
-    if (k->type == GGML_TYPE_F16 || k->type == GGML_TYPE_F32) {
+    auto plain = [](ggml_type t) { return t == GGML_TYPE_F16 || t == GGML_TYPE_F32; };
+    auto coded = [](ggml_type t) { return t == GGML_TYPE_BF16 || t == GGML_TYPE_Q8_0 || t == GGML_TYPE_Q4_0; };
+    if (plain(k->type) && plain(v->type)) {
         if (D != 32 && D != 40 && D != 48 && D != 64 && D != 80 && D != 96 && D != 112 && D != 128 && D != 256) return false;
-    } else if (k->type == GGML_TYPE_BF16 || k->type == GGML_TYPE_Q8_0 || k->type == GGML_TYPE_Q4_0) {
+    } else if ((plain(k->type) || coded(k->type)) && (plain(v->type) || coded(v->type))) {
         if (D != 64 && D != 128 && D != 256) return false;   // quantised / bf16 caches: the tile kernel's common head sizes
     } else return false;
     if (q->ne[2] % k->ne[2] != 0 || q->ne[2] / k->ne[2] > FA_MAXG) return false;
@@ -603,7 +609,9 @@ bool flash_attn_supported(const ggml_tensor * dst) {
 
 template <typename TK, typename TV>
 static void fa_launch(OpCtx & c, int D, dim3 grid, const FaArgs & a) {
-    if constexpr (!std::is_same<TK, uint16_t>::value && !std::is_same<TK, float>::value) {
+    constexpr bool plain = (std::is_same<TK, uint16_t>::value || std::is_same<TK, float>::value) &&
+                           (std::is_same<TV, uint16_t>::value || std::is_same<TV, float>::value);
+    if constexpr (!plain) {
         switch (D) {
             case 64:  k_fattn<TK, TV, 64><<<grid, 256, 0, c.st>>>(a); return;
             case 128: k_fattn<TK, TV, 128><<<grid, 256, 0, c.st>>>(a); return;
@@ -721,8 +729,24 @@ void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
 #undef DEC
         if (nsplit == 1) return;
     } else {
-        MX_KLOG("fattn_tile D=%d type=%d", D, (int) k->type);
-        switch (k->type) {
+        MX_KLOG("fattn_tile D=%d type=%d vtype=%d", D, (int) k->type, (int) v->type);
+        if (k->type != v->type) {   // mixed f16 / q8_0 / q4_0 pairs (flash_attn_supported)
+            auto vl = [&](auto ktag) {
+                using TK = decltype(ktag);
+                switch (v->type) {
+                    case GGML_TYPE_F16:  fa_launch<TK, uint16_t>(c, D, grid, b); break;
+                    case GGML_TYPE_Q8_0: fa_launch<TK, KvQ8>(c, D, grid, b); break;
+                    case GGML_TYPE_Q4_0: fa_launch<TK, KvQ4>(c, D, grid, b); break;
+                    default: MX_ABORT("fattn v type %d", (int) v->type);
+                }
+            };
+            switch (k->type) {
+                case GGML_TYPE_F16:  vl(uint16_t{}); break;
+                case GGML_TYPE_Q8_0: vl(KvQ8{}); break;
+                case GGML_TYPE_Q4_0: vl(KvQ4{}); break;
+                default: MX_ABORT("fattn k type %d", (int) k->type);
+            }
+        } else switch (k->type) {
             case GGML_TYPE_F16:  fa_launch<uint16_t, uint16_t>(c, D, grid, b); break;
             case GGML_TYPE_BF16: fa_launch<KvBF16, KvBF16>(c, D, grid, b); break;
             case GGML_TYPE_Q8_0: fa_launch<KvQ8, KvQ8>(c, D, grid, b); break;

@@ -22,6 +22,7 @@
 #include "backend.h"
 #include "quants.cuh"
 #include "gemv.h"
+#include <type_traits>
 
 namespace mx { extern int g_tune[48]; }
 
@@ -52,6 +53,25 @@ constexpr int FD_MAXSPLIT = 16;   // workgroups per (q row, KV head); longer cac
 // (its f16 scale first: block_q8_0), q is quantised to q8_0 per 32-block as the CPU's
 // vec_dot_type conversion does (amax over the block's 4 lanes by DPP, d = amax/127 kept
 // as f16), q·k = Σ_blocks d_q·d_k·Σ q_i k_i, V dequantised d·q_i into the f32 sums.
+// Round 6: K and V types are independent (template KV: fd_kv_code) — the fork's own line is
+// `-ctk q8_0 -ctv f16` (K q8_0, V f16; reference fattn.cu:220-226 under FA_ALL_QUANTS).
+// KV 0: f16 / f16, 1: q8_0 / q8_0, 2: q8_0 K / f16 V, 3: f16 K / q8_0 V.
+constexpr bool fd_kq(int kv) { return kv == 1 || kv == 2; }
+constexpr bool fd_vq(int kv) { return kv == 1 || kv == 3; }
+static int fd_kv_code(const ggml_tensor * k, const ggml_tensor * v) {
+    const bool kq = k->type == GGML_TYPE_Q8_0, vq = v->type == GGML_TYPE_Q8_0;
+    return kq ? (vq ? 1 : 2) : (vq ? 3 : 0);
+}
+// f(std::integral_constant<int, KV>{}) for the runtime code kv (one instantiation per pair)
+template <typename F>
+static void fd_kv_dispatch(int kv, F && f) {
+    switch (kv) {
+        case 1: f(std::integral_constant<int, 1>{}); break;
+        case 2: f(std::integral_constant<int, 2>{}); break;
+        case 3: f(std::integral_constant<int, 3>{}); break;
+        default: f(std::integral_constant<int, 0>{}); break;
+    }
+}
 __device__ __forceinline__ uint2 ldu8(const char * p) {   // 8 bytes, any 2-byte alignment
     uint2 v;
     __builtin_memcpy(&v, __builtin_assume_aligned(p, 2), 8);
@@ -96,8 +116,9 @@ __device__ __forceinline__ float kr_max(float v) {
 // (the looping split form paid one memory round trip per 64-key chunk: 34.5 us at 16k
 // keys), any number of splits; the (O, max, sum) partials are merged by
 // k_fattn_dec2_combine, a parallel second launch (one workgroup per query head).
-template <int D, int G, int NW, bool KQ = false, int NI = FD_NI, bool LONG = false, int CPW = 1>
+template <int D, int G, int NW, int KV = 0, int NI = FD_NI, bool LONG = false, int CPW = 1>
 __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
+    constexpr bool KQ = fd_kq(KV), VQ = fd_vq(KV);
     constexpr int NT = 64 * NW;
     constexpr int LPK = D / 8;            // lanes per key row
     constexpr int KPI = 64 / LPK;         // keys per wave instruction
@@ -136,10 +157,11 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     const int hb = hk * Gt + gb * G;                         // first query head
     const int hslot = hk * NGB + gb;                         // partial / counter slot
     // this lane's 8 dimensions of a row: f16 at 16 c; q8_0 at block c/4 (34 B), byte 8 (c%4)
-    const int lofs = KQ ? (c >> 2) * 34 + 2 + 8 * (c & 3) : c * 16;
+    const int lofs8 = (c >> 2) * 34 + 2 + 8 * (c & 3), lofs16 = c * 16;
+    const int lofsk = KQ ? lofs8 : lofs16, lofsv = VQ ? lofs8 : lofs16;
     const int dofs = (c >> 2) * 34;
-    const char * kb = p.k + (size_t) hk * p.k2 + (size_t) (iq3 % p.ns_kv) * p.k3 + lofs;
-    const char * vb = p.v + (size_t) hk * p.v2 + (size_t) (iq3 % p.ns_kv) * p.v3 + lofs;
+    const char * kb = p.k + (size_t) hk * p.k2 + (size_t) (iq3 % p.ns_kv) * p.k3 + lofsk;
+    const char * vb = p.v + (size_t) hk * p.v2 + (size_t) (iq3 % p.ns_kv) * p.v3 + lofsv;
     const uint16_t * mrow = (const uint16_t *) (p.mask ? p.mask + (size_t) iq1 * p.m1 + (size_t) (iq3 % p.mne3) * p.m3 : p.k);
     const int nch = (p.n_kv + CS - 1) / CS, cpb = LONG ? 1 : (nch + p.nsplit - 1) / p.nsplit;
     unsigned long long * tr = (blockIdx.x == 0 && blockIdx.y == 0) ? p.trace : nullptr;
@@ -205,18 +227,21 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
                 const size_t ko = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1;
                 const uint2 w = ldu8(kb + ko);
                 b.kr[t] = make_uint4(w.x, w.y, 0, 0);
-                b.kd[t] = ld_u16(kb - lofs + dofs + ko);
+                b.kd[t] = ld_u16(kb - lofsk + dofs + ko);
             }
+        } else {
+#pragma unroll
+            for (int t = 0; t < NI; ++t) b.kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
+        }
+        if constexpr (VQ) {
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
                 const size_t vo = (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1;
                 const uint2 w = ldu8(vb + vo);
                 b.vr[t] = make_uint4(w.x, w.y, 0, 0);
-                b.vd[t] = ld_u16(vb - lofs + dofs + vo);
+                b.vd[t] = ld_u16(vb - lofsv + dofs + vo);
             }
         } else {
-#pragma unroll
-            for (int t = 0; t < NI; ++t) b.kr[t] = *(const uint4 *) (kb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.k1);
 #pragma unroll
             for (int t = 0; t < NI; ++t) b.vr[t] = *(const uint4 *) (vb + (size_t) min(key0 + t * KPI, p.n_kv - 1) * p.v1);
         }
@@ -269,7 +294,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             for (int i = 0; i < 8; ++i) o[h][i] *= a;
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
-                if constexpr (KQ) {
+                if constexpr (VQ) {
                     const float dv = h2f(b.vd[t]);
                     const uint32_t vw[2] = {b.vr[t].x, b.vr[t].y};
 #pragma unroll
@@ -463,8 +488,8 @@ __global__ __launch_bounds__(256) void k_fattn_dec2_combine(FaDecArgs p) {
 // no softcap / ALiBi / sinks, few query rows (decode)
 bool fa_dec2_ok(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
-    const bool kq = k->type == GGML_TYPE_Q8_0 && v->type == GGML_TYPE_Q8_0;
-    if (q->ne[1] > 4 || !((k->type == GGML_TYPE_F16 && v->type == GGML_TYPE_F16) || kq)) return false;
+    const bool kq = k->type == GGML_TYPE_Q8_0, vq = v->type == GGML_TYPE_Q8_0;
+    if (q->ne[1] > 4 || !(k->type == GGML_TYPE_F16 || kq) || !(v->type == GGML_TYPE_F16 || vq)) return false;
     const int64_t D = k->ne[0];
     if ((D != 64 && D != 128) || v->ne[0] != D) return false;
     const int64_t G = q->ne[2] / k->ne[2];
@@ -472,16 +497,19 @@ bool fa_dec2_ok(const ggml_tensor * dst) {
     if (dst->src[4]) return false;                                        // sinks
     if (mx_op_param<float>(dst, 1) != 0.0f || mx_op_param<float>(dst, 2) != 0.0f) return false;   // ALiBi, softcap
     if (m && (m->type != GGML_TYPE_F16 || m->ne[2] > 1)) return false;
-    if (kq) {   // q8_0 rows: 2-byte aligned blocks, 8-byte loads at any 2-byte alignment
-        if (k->nb[1] % 2 || v->nb[1] % 2 || k->nb[2] % 2 || v->nb[2] % 2 || (uintptr_t) k->data % 2 || (uintptr_t) v->data % 2) return false;
-    } else if (k->nb[1] % 16 || v->nb[1] % 16 || k->nb[2] % 16 || v->nb[2] % 16 || (uintptr_t) k->data % 16 || (uintptr_t) v->data % 16) return false;
+    // q8_0 rows: 2-byte aligned blocks, 8-byte loads at any 2-byte alignment; f16 rows: 16-B loads
+    auto aligned = [](const ggml_tensor * t, bool q8) {
+        const size_t a = q8 ? 2 : 16;
+        return t->nb[1] % a == 0 && t->nb[2] % a == 0 && (uintptr_t) t->data % a == 0;
+    };
+    if (!aligned(k, kq) || !aligned(v, vq)) return false;
     if (q->nb[1] % 16 || q->nb[2] % 16 || (uintptr_t) q->data % 16) return false;
     if (q->ne[3] != k->ne[3] && k->ne[3] != 1) return false;
     // counters [0, MX_FA_CNT / 2): the upper half holds k_attn_o's row-chunk epochs (ops_attn_o.hip)
     if (k->ne[1] > INT32_MAX / 2 || q->ne[1] * q->ne[3] * q->ne[2] > MX_FA_CNT / 2) return false;
     // caches beyond one 16-wave chunk take the LONG geometry (fd_cfg); g_tune[10] = 4 keeps
     // them on the v1 kernel + combine (round-2 behaviour: 18.4 + 12.0 us at 16k keys)
-    if (g_tune[10] == 4 && !kq && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;
+    if (g_tune[10] == 4 && !kq && !vq && k->ne[1] > 16 * FD_NI * (64 / (D / 8))) return false;
     if (k->ne[1] > (int64_t) 32768 * 4 * 8 * (64 / (D / 8))) return false;   // FD_LONG_MAXSPLIT chunks
     return true;
 }
@@ -497,7 +525,7 @@ bool fa_dec2_ok(const ggml_tensor * dst) {
 struct FdCfg { int G, NW, nsplit; bool lng; int cpw = 1; };
 constexpr int FD_LONG_NI = 8;
 constexpr int FD_LONG_MAXSPLIT = 32768;   // the combine's split weights in LDS (128 KB): 4M keys at D 128
-static FdCfg fd_cfg(int D, int Gt, int64_t n_kv, int64_t rows) {   // rows = Hkv x n_q x sequences
+static FdCfg fd_cfg(int D, int Gt, int64_t n_kv, int64_t rows, int kv) {   // rows = Hkv x n_q x sequences; kv: fd_kv_code
     const int cs16 = 16 * FD_NI * (64 / (D / 8)), cs4 = 4 * FD_NI * (64 / (D / 8));
     // g_tune[1] = NI (2 / 4, experiment): short caches too take the LONG geometry — chunks of
     // 4 NI 64/(D/8) keys, one per workgroup, G = g_tune[29] (default 1) heads, plus the combine
@@ -523,7 +551,7 @@ static FdCfg fd_cfg(int D, int Gt, int64_t n_kv, int64_t rows) {   // rows = Hkv
     int cpw = 1;
     (void) rows;
     if (g_tune[2] == 2 || g_tune[2] == 4 || g_tune[2] == 8) cpw = g_tune[2];
-    if (ni != FD_LONG_NI || g > 2) cpw = 1;                   // (instantiated for the default NI, G <= 2)
+    if (ni != FD_LONG_NI || g > 2 || kv > 1) cpw = 1;         // (instantiated for the default NI, G <= 2, same K/V types)
     return {g, 4, (int) mx_ceil_div(nch, cpw), true, cpw};
 }
 
@@ -534,8 +562,17 @@ size_t fa_dec2_scratch(const ggml_tensor * dst) {
     if (const size_t s3 = fd3_scratch(dst)) return s3;
     const ggml_tensor * q = dst->src[0], * k = dst->src[1];
     const int64_t D = k->ne[0];
-    const FdCfg f = fd_cfg((int) D, (int) (q->ne[2] / k->ne[2]), k->ne[1], k->ne[2] * q->ne[1] * q->ne[3]);
+    const FdCfg f = fd_cfg((int) D, (int) (q->ne[2] / k->ne[2]), k->ne[1], k->ne[2] * q->ne[1] * q->ne[3], fd_kv_code(k, dst->src[2]));
     return (size_t) (q->ne[1] * q->ne[3] * q->ne[2]) * (f.lng ? f.nsplit : std::min(f.nsplit, FD_MAXSPLIT)) * (D + 2) * sizeof(float) + 256;
+}
+
+// the LONG geometry's launch: every K/V type pair at one chunk per workgroup; the CPW > 1
+// experiment (g_tune[2]) only for caches of one type (fd_cfg)
+template <int DD, int GG, int CP>
+static void fd_long_launch(int kv, dim3 grid, const FaDecArgs & a, hipStream_t st) {
+    if constexpr (CP == 1) fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<DD, GG, 4, decltype(KVC)::value, FD_LONG_NI, true, 1><<<grid, 256, 0, st>>>(a); });
+    else if (kv == 1) k_fattn_dec2<DD, GG, 4, 1, FD_LONG_NI, true, CP><<<grid, 256, 0, st>>>(a);
+    else k_fattn_dec2<DD, GG, 4, 0, FD_LONG_NI, true, CP><<<grid, 256, 0, st>>>(a);
 }
 
 void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
@@ -552,7 +589,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     a.ns_kv = (int) k->ne[3];
     a.scale = mx_op_param<float>(dst, 0);
     const int D = (int) k->ne[0], Gt = a.H / a.Hkv;
-    const FdCfg f = fd_cfg(D, Gt, a.n_kv, (int64_t) a.Hkv * a.n_q * q->ne[3]);
+    const FdCfg f = fd_cfg(D, Gt, a.n_kv, (int64_t) a.Hkv * a.n_q * q->ne[3], fd_kv_code(k, v));
     MX_ASSERT(f.lng ? f.nsplit <= 65535 : f.nsplit <= FD_MAXSPLIT);
     a.nsplit = f.nsplit;
     a.part = (float *) c.scratch->take(fa_dec2_scratch(dst));
@@ -571,15 +608,13 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
         while ((gx * pf_rows) % 8) ++pf_rows;
     } else a.pf_n = 0;
     const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
-    const bool kq = k->type == GGML_TYPE_Q8_0;
-    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u long=%d cpw=%d", D, f.G, f.NW, f.nsplit, a.n_kv,
-            a.H, a.Hkv, (int) kq, pf_rows, (int) f.lng, f.cpw);
+    const int kv = fd_kv_code(k, v);
+    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d vq8=%d pf_rows=%u long=%d cpw=%d", D, f.G, f.NW, f.nsplit,
+            a.n_kv, a.H, a.Hkv, (int) fd_kq(kv), (int) fd_vq(kv), pf_rows, (int) f.lng, f.cpw);
     if (f.lng) {
         const unsigned gc = gx * (unsigned) f.G;                     // one combine workgroup per query head
         const size_t lds = (size_t) f.nsplit * sizeof(float);
-#define FLC(DD, GG, CP) if (f.cpw == CP) { \
-            if (kq) k_fattn_dec2<DD, GG, 4, true, FD_LONG_NI, true, CP><<<grid, 256, 0, c.st>>>(a); \
-            else k_fattn_dec2<DD, GG, 4, false, FD_LONG_NI, true, CP><<<grid, 256, 0, c.st>>>(a); }
+#define FLC(DD, GG, CP) if (f.cpw == CP) fd_long_launch<DD, GG, CP>(kv, grid, a, c.st);
 #define FLW(DD, GG, CPWS) if (D == DD && f.G == GG) { \
             CPWS \
             MX_LDS_OPTIN((k_fattn_dec2_combine<DD, GG>), FD_LONG_MAXSPLIT * (int) sizeof(float)); \
@@ -587,7 +622,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
             return; }
         const int ni = D == 128 && g_tune[1] && a.n_kv <= 16 * FD_NI * (64 / (D / 8)) && a.n_kv > 4 * g_tune[1] * (64 / (D / 8)) ? g_tune[1] :
                        D == 128 && g_tune[28] ? g_tune[28] : FD_LONG_NI;
-        if (ni != FD_LONG_NI && !kq) {   // sweep geometries (f16, D 128)
+        if (ni != FD_LONG_NI && kv == 0) {   // sweep geometries (f16, D 128)
 #define FS(NI_, GG) if (ni == NI_ && f.G == GG) { \
                 k_fattn_dec2<128, GG, 4, false, NI_, true><<<grid, 256, 0, c.st>>>(a); \
                 k_fattn_dec2_combine<128, GG><<<gc, 256, lds, c.st>>>(a); return; }
@@ -603,8 +638,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
         MX_ABORT("fattn dec2 long D=%d G=%d", D, f.G);
     }
 #define FD(DD, GG, NWW) if (D == DD && f.G == GG && f.NW == NWW) { \
-        if (kq) k_fattn_dec2<DD, GG, NWW, true><<<grid, 64 * NWW, 0, c.st>>>(a); \
-        else k_fattn_dec2<DD, GG, NWW><<<grid, 64 * NWW, 0, c.st>>>(a); \
+        fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<DD, GG, NWW, decltype(KVC)::value><<<grid, 64 * NWW, 0, c.st>>>(a); }); \
         return; }
     FD(128, 1, 16) FD(64, 1, 16)
     FD(128, 4, 4) FD(128, 1, 4) FD(128, 2, 4) FD(128, 8, 4) FD(64, 1, 4) FD(64, 2, 4) FD(64, 4, 4) FD(64, 8, 4)
@@ -666,20 +700,13 @@ void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit) {
         while ((gx * pf_rows) % 8) ++pf_rows;
     } else a.pf_n = 0;
     const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
-    const bool kq = k->type == GGML_TYPE_Q8_0;
+    const int kv = fd_kv_code(k, v);
     const int ni = fa_split_ni();
-    MX_KLOG("fattn_dec2_part D=128 G=1 NI=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d pf_rows=%u", ni, nsplit, a.n_kv, a.H, a.Hkv,
-            (int) kq, pf_rows);
-    if (ni == 2) {
-        if (kq) k_fattn_dec2<128, 1, 4, true, 2, true><<<grid, 256, 0, c.st>>>(a);
-        else k_fattn_dec2<128, 1, 4, false, 2, true><<<grid, 256, 0, c.st>>>(a);
-    } else if (ni == 8) {
-        if (kq) k_fattn_dec2<128, 1, 4, true, 8, true><<<grid, 256, 0, c.st>>>(a);
-        else k_fattn_dec2<128, 1, 4, false, 8, true><<<grid, 256, 0, c.st>>>(a);
-    } else {
-        if (kq) k_fattn_dec2<128, 1, 4, true, 4, true><<<grid, 256, 0, c.st>>>(a);
-        else k_fattn_dec2<128, 1, 4, false, 4, true><<<grid, 256, 0, c.st>>>(a);
-    }
+    MX_KLOG("fattn_dec2_part D=128 G=1 NI=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d vq8=%d pf_rows=%u", ni, nsplit, a.n_kv, a.H, a.Hkv,
+            (int) fd_kq(kv), (int) fd_vq(kv), pf_rows);
+    if (ni == 2) fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<128, 1, 4, decltype(KVC)::value, 2, true><<<grid, 256, 0, c.st>>>(a); });
+    else if (ni == 8) fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<128, 1, 4, decltype(KVC)::value, 8, true><<<grid, 256, 0, c.st>>>(a); });
+    else fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<128, 1, 4, decltype(KVC)::value, 4, true><<<grid, 256, 0, c.st>>>(a); });
 }
 
 // ---------------------------------------------------------------------------

@@ -551,16 +551,19 @@ bool fa_mma_ok(const ggml_tensor * dst) {
     const ggml_tensor * m = dst->src[3];
     if (dst->src[4]) return false;                                        // sinks
     if (mx_op_param<float>(dst, 1) != 0.0f || mx_op_param<float>(dst, 2) != 0.0f) return false;   // ALiBi, softcap
-    if (q->type != GGML_TYPE_F32 || k->type != v->type) return false;
-    // bf16 / q8_0 / q4_0 caches run on f16 copies (fa_kv_to_f16)
-    const bool conv = k->type == GGML_TYPE_BF16 || k->type == GGML_TYPE_Q8_0 || k->type == GGML_TYPE_Q4_0;
-    if (k->type != GGML_TYPE_F16 && !conv) return false;
+    if (q->type != GGML_TYPE_F32) return false;
+    // bf16 / q8_0 / q4_0 caches run on f16 copies (fa_kv_to_f16), K and V each (round 6: the
+    // types may differ — -ctk q8_0 -ctv f16 converts K only)
+    auto cv = [](ggml_type t) { return t == GGML_TYPE_BF16 || t == GGML_TYPE_Q8_0 || t == GGML_TYPE_Q4_0; };
+    const bool convk = cv(k->type), convv = cv(v->type);
+    if ((k->type != GGML_TYPE_F16 && !convk) || (v->type != GGML_TYPE_F16 && !convv)) return false;
     const int64_t D = k->ne[0];
     if ((D != 64 && D != 128) || v->ne[0] != D) return false;
     if (q->ne[1] < 16 || q->ne[3] != 1 || k->ne[3] != 1 || q->ne[2] % k->ne[2]) return false;
     if (m && (m->type != GGML_TYPE_F16 || m->ne[2] != 1 || m->ne[3] != 1 || m->nb[1] % 16 || (uintptr_t) m->data % 16)) return false;
     if (q->nb[1] % 16 || q->nb[0] != 4 || (uintptr_t) q->data % 16) return false;
-    if (!conv && (k->nb[1] % 16 || v->nb[1] % 16 || ((uintptr_t) k->data | (uintptr_t) v->data) % 16)) return false;
+    if (!convk && (k->nb[1] % 16 || (uintptr_t) k->data % 16)) return false;
+    if (!convv && (v->nb[1] % 16 || (uintptr_t) v->data % 16)) return false;
     if (dst->nb[0] != 4 || k->ne[1] > INT32_MAX / 2 || q->ne[1] > INT32_MAX / 2) return false;
     return true;
 }
@@ -577,12 +580,13 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
     p.k = (const char *) k->data; p.k1 = k->nb[1]; p.k2 = k->nb[2];
     p.v = (const char *) v->data; p.v1 = v->nb[1]; p.v2 = v->nb[2];
     if (k->type != GGML_TYPE_F16) {
-        const size_t n = (size_t) k->ne[0] * k->ne[1] * k->ne[2];
-        uint16_t * kh = (uint16_t *) c.scratch->take(n * 2);
-        uint16_t * vh = (uint16_t *) c.scratch->take(n * 2);
+        uint16_t * kh = (uint16_t *) c.scratch->take((size_t) k->ne[0] * k->ne[1] * k->ne[2] * 2);
         fa_kv_to_f16(c, k, kh);
-        fa_kv_to_f16(c, v, vh);
         p.k = (const char *) kh; p.k1 = k->ne[0] * 2; p.k2 = k->ne[0] * k->ne[1] * 2;
+    }
+    if (v->type != GGML_TYPE_F16) {
+        uint16_t * vh = (uint16_t *) c.scratch->take((size_t) v->ne[0] * v->ne[1] * v->ne[2] * 2);
+        fa_kv_to_f16(c, v, vh);
         p.v = (const char *) vh; p.v1 = v->ne[0] * 2; p.v2 = v->ne[0] * v->ne[1] * 2;
     }
     if (m) { p.mask = (const char *) m->data; p.m1 = m->nb[1]; }

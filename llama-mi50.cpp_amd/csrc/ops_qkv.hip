@@ -402,18 +402,19 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     // only the fused consumers may read the intermediate results
     if ((mq->flags | mk->flags | mv->flags | rk->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
     if (uses(mq) != 1 || uses(mk) != 1 || uses(mv) != 1 || uses(rk) != 1) return 0;
-    // KV stores: f16 caches, or q8_0 caches (rows quantised by k_kv_store_q8), one token
-    const ggml_tensor * kcache = sk, * vcache = sv;
-    const bool kq8 = kcache->type == GGML_TYPE_Q8_0 && vcache->type == GGML_TYPE_Q8_0;
-    if (!kq8 && (kcache->type != GGML_TYPE_F16 || vcache->type != GGML_TYPE_F16)) return 0;
-    const size_t esz = kq8 ? 34 : 2;
+    // KV stores: f16 or q8_0 caches (q8_0 rows quantised by k_kv_store_q8), K and V types
+    // independent (round 6: -ctk q8_0 -ctv f16, the fork's own line), one token
+    const bool kq8 = sk->type == GGML_TYPE_Q8_0, vq8 = sv->type == GGML_TYPE_Q8_0;
+    if ((!kq8 && sk->type != GGML_TYPE_F16) || (!vq8 && sv->type != GGML_TYPE_F16)) return 0;
+    const size_t eszk = kq8 ? 34 : 2, eszv = vq8 ? 34 : 2;
     const ggml_tensor * kix = sk->src[1], * vix = sv->src[1];
-    if (sk->src[0]->ne[0] != wk->ne[1] || sk->src[0]->ne[1] != 1 || kix->ne[0] != 1 || sk->nb[0] != esz) return 0;
+    if (sk->src[0]->ne[0] != wk->ne[1] || sk->src[0]->ne[1] != 1 || kix->ne[0] != 1 || sk->nb[0] != eszk) return 0;
     int v_trans;
-    if (sv->src[0]->ne[0] == wv->ne[1] && sv->src[0]->ne[1] == 1 && vix->ne[0] == 1 && sv->nb[0] == esz) v_trans = 0;
-    else if (!kq8 && sv->src[0]->ne[0] == 1 && sv->src[0]->ne[1] == wv->ne[1] && vix->ne[0] == wv->ne[1] && sv->ne[0] == 1) v_trans = 1;
+    if (sv->src[0]->ne[0] == wv->ne[1] && sv->src[0]->ne[1] == 1 && vix->ne[0] == 1 && sv->nb[0] == eszv) v_trans = 0;
+    else if (!vq8 && sv->src[0]->ne[0] == 1 && sv->src[0]->ne[1] == wv->ne[1] && vix->ne[0] == wv->ne[1] && sv->ne[0] == 1) v_trans = 1;
     else return 0;
-    if (kq8 && (wk->ne[1] % 32 || wv->ne[1] % 32 || c.scratch->avail() < (size_t) 4 * (wk->ne[1] + wv->ne[1]) + 512)) return 0;
+    const bool anyq8 = kq8 || vq8;
+    if ((kq8 && wk->ne[1] % 32) || (vq8 && wv->ne[1] % 32) || (anyq8 && c.scratch->avail() < (size_t) 4 * (wk->ne[1] + wv->ne[1]) + 512)) return 0;
     for (const ggml_tensor * ix : {kix, vix}) if (ix->type != GGML_TYPE_I64) return 0;   // llama's KV indices
     // Round 5, row-split weights (-sm row): q, k and v split alike, at head boundaries (the
     // 256-row slice granule is a multiple of n_dims): one fused launch per slice on the
@@ -426,7 +427,7 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     int sdev[3][MX_MAX_DEVICES], ns = 0;
     if (split) {
         const int n_dims_q = mx_op_param<int32_t>(rq, 1);
-        if (kq8 || !tensor_is_split(wq) || !tensor_is_split(wk) || !tensor_is_split(wv) || n_dims_q <= 0) return 0;
+        if (anyq8 || !tensor_is_split(wq) || !tensor_is_split(wk) || !tensor_is_split(wv) || n_dims_q <= 0) return 0;
         for (int t = 0; t < 3; ++t) {
             const int n = split_slices(c.s, t == 0 ? wq : t == 1 ? wk : wv, sd[t], slo[t], shi[t], sdev[t]);
             if (!n || (t && n != ns)) return 0;
@@ -533,10 +534,8 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
 #undef QKB
         if (kb) { kern = kb; grid = dim3((unsigned) (wq->ne[1] / 16)); nthr = 448; }
     }
-    if (kq8) {
-        p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
-        p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
-    }
+    if (kq8) p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
+    if (vq8) p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
     if (split) {
         int remote = 0;
         for (int k = 0; k < ns; ++k) remote += !split_on_main(c.s, wq, sdev[0][k]);
@@ -563,10 +562,12 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
         HIP_CHECK(hipSetDevice(c.s->device));
         return last - i + 1;
     }
-    MX_KLOG("qkv qta=%d qtk=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d bal=%d", ta, tk, tv, mode, cfg, p.K, (int) kq8, (int) (nthr == 448));
+    MX_KLOG("qkv qta=%d qtk=%d qtv=%d mode=%d cfg=%d K=%d kq8=%d vq8=%d bal=%d", ta, tk, tv, mode, cfg, p.K, (int) kq8, (int) vq8,
+            (int) (nthr == 448));
     hipLaunchKernelGGL(kern, grid, dim3(nthr), gemv_lds_bytes(p.K, mode), c.st, p);
-    if (kq8) {
-        k_kv_store_q8<<<(unsigned) mx_ceil_div(wk->ne[1] + wv->ne[1], 256), 256, 0, c.st>>>(p, (int) wk->ne[1], (int) wv->ne[1]);
+    if (anyq8) {   // the q8_0 rows (nk / nv = 0: that cache took its f16 row in the launch above)
+        const int nk = kq8 ? (int) wk->ne[1] : 0, nv = vq8 ? (int) wv->ne[1] : 0;
+        k_kv_store_q8<<<(unsigned) mx_ceil_div(nk + nv, 256), 256, 0, c.st>>>(p, nk, nv);
     }
     return last - i + 1;
 }

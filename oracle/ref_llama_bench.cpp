@@ -10,6 +10,8 @@
 //                pp2048 as 4 ubatches with -b 2048 -ub 512);
 //   -r R       : bench mode repeats pp / tg R times and reports the mean and the
 //                per-repetition rates, llama-bench's avg_ts / samples_ts.
+//   -ctk T / -ctv T : K and V cache types (ggml_type ids; -ctk alone sets both, as the
+//                tests have always used it; -ctk 8 -ctv 1 = K q8_0 + V f16, AGENTS.md:166-176).
 //   -d D       : llama-bench's depth (tools/llama-bench/llama-bench.cpp:2191-2226): before
 //                every timed pp / tg repetition the cleared cache is filled with a
 //                D-token prompt (untimed), so tg runs against D + i keys.
@@ -69,6 +71,7 @@ int main(int argc, char ** argv) {
     std::string model, tok_in, logits_out;
     int threads = 8, pp = 32, tg = 16, ngl = 0, fa = 1, n_ctx = 0, incremental = 0, last = 0, n_batch = 0, n_ubatch = 0, reps = 1;
     int ctk = -1;   // K/V cache type (ggml_type id), -1: default f16
+    int ctv = -1;   // -ctv: the V cache type alone (default: as -ctk) — K q8_0 + V f16 is the fork's line
     int depth = 0;
     int prefix = 0;                    // logits mode, incremental: the first N tokens as one batch (no logits)
     std::string sm = "layer";          // -sm none|layer|row
@@ -94,6 +97,7 @@ int main(int argc, char ** argv) {
         else if (a == "-r") reps = std::max(1, std::stoi(next()));
         else if (a == "-d") depth = std::stoi(next());
         else if (a == "-ctk") ctk = std::stoi(next());
+        else if (a == "-ctv") ctv = std::stoi(next());
         else if (a == "-sm") sm = next();
         else if (a == "-mg") mg = std::stoi(next());
         else if (a == "-mmp") use_mmap = std::stoi(next());
@@ -110,7 +114,12 @@ int main(int argc, char ** argv) {
         else if (a == "--dump-dir") g_dump_dir = next();
         else if (a == "--dump-filter") g_dump_filter = next();
     }
-    llama_log_set([](ggml_log_level, const char *, void *) {}, nullptr);
+    // libllama's log is silenced except its scheduler summary (src/llama-context.cpp:523-533,
+    // "graph splits = N"): the drop-in tests assert the split count, which shows any node
+    // the MI355X backend refused (it runs on the CPU backend as an extra split)
+    llama_log_set([](ggml_log_level, const char * text, void *) {
+        if (strstr(text, "graph splits") || strstr(text, "graph nodes")) fprintf(stderr, "[llama] %s", text);
+    }, nullptr);
     llama_backend_init();
     ggml_backend_load_all();
     for (size_t i = 0; i < ggml_backend_dev_count(); ++i)
@@ -139,6 +148,7 @@ int main(int argc, char ** argv) {
     cp.n_batch = n_batch > 0 ? n_batch : std::max<int>({pp, (int) toks.size(), 1, std::min(depth, 2048)});
     cp.n_ubatch = n_ubatch > 0 ? n_ubatch : std::min<int>(512, cp.n_batch);
     if (ctk >= 0) { cp.type_k = (ggml_type) ctk; cp.type_v = (ggml_type) ctk; }
+    if (ctv >= 0) cp.type_v = (ggml_type) ctv;
     cp.n_threads = threads;
     cp.n_threads_batch = threads;
     cp.flash_attn_type = fa ? LLAMA_FLASH_ATTN_TYPE_ENABLED : LLAMA_FLASH_ATTN_TYPE_DISABLED;

@@ -18,7 +18,7 @@
 //   E  GPU context: set_data(blob_c) (CPU state into the GPU), generation -> logits_e
 // Everything is written to --out; tests/test_dropin_gpu.py compares.
 //
-//   state-probe -m model.gguf -fa 1 [-ctk type] --prompt p.i32 --gen g.i32 --out dir
+//   state-probe -m model.gguf -fa 1 [-ctk type] [-ctv type] --prompt p.i32 --gen g.i32 --out dir
 #include "llama.h"
 #include "ggml-backend.h"
 
@@ -45,13 +45,14 @@ static void write_bytes(const std::string & p, const void * d, size_t n) {
 
 int main(int argc, char ** argv) {
     std::string model, prompt_f, gen_f, out;
-    int fa = 1, ctk = -1;
+    int fa = 1, ctk = -1, ctv = -1;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() { return std::string(argv[++i]); };
         if (a == "-m") model = next();
         else if (a == "-fa") fa = std::stoi(next());
         else if (a == "-ctk") ctk = std::stoi(next());
+        else if (a == "-ctv") ctv = std::stoi(next());   // V cache type alone (K q8_0 + V f16)
         else if (a == "--prompt") prompt_f = next();
         else if (a == "--gen") gen_f = next();
         else if (a == "--out") out = next();
@@ -80,6 +81,7 @@ int main(int argc, char ** argv) {
         cp.n_threads = cp.n_threads_batch = 8;
         cp.flash_attn_type = fa ? LLAMA_FLASH_ATTN_TYPE_ENABLED : LLAMA_FLASH_ATTN_TYPE_DISABLED;
         if (ctk >= 0) { cp.type_k = (ggml_type) ctk; cp.type_v = (ggml_type) ctk; }
+        if (ctv >= 0) cp.type_v = (ggml_type) ctv;
         cp.offload_kqv = gpu;
         cp.op_offload = gpu;
         cp.no_perf = true;

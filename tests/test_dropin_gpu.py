@@ -17,6 +17,7 @@ import sys
 import numpy as np
 import pytest
 
+from dropin_util import assert_unsplit, graph_splits
 from qgen import nmse
 
 pytestmark = pytest.mark.gpu
@@ -44,7 +45,11 @@ def ggufs(tmp_path_factory):
     return out
 
 
-def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False, ctk=None, klog=None, extra=(), env_extra=None):
+def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False, ctk=None, klog=None, extra=(), env_extra=None, ctv=None,
+            splits="auto"):
+    """splits: the graph-split count libllama must report on the MI355X run ("auto": 2 —
+    CPU input embedding + MI355X — unless a multi-device split mode is requested; None:
+    not checked)"""
     tf = tmp_path / "toks.i32"
     of = tmp_path / f"logits_{ngl}_{fa}_{int(incremental)}.f32"
     np.asarray(toks, np.int32).tofile(tf)
@@ -58,11 +63,17 @@ def run_ref(tmp_path, gguf, toks, ngl, fa, incremental=False, ctk=None, klog=Non
         cmd.append("--incremental")
     if ctk is not None:
         cmd += ["-ctk", str(ctk)]        # K and V cache type (ggml type id)
+    if ctv is not None:
+        cmd += ["-ctv", str(ctv)]        # V cache type alone
     cmd += list(extra)
     if env_extra and ngl > 0:
         env.update(env_extra)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
+    if splits == "auto":
+        splits = 2 if "-sm" not in extra else None
+    if ngl > 0 and splits is not None:
+        assert_unsplit(r.stderr, splits)
     n_vocab = int(r.stdout.strip().splitlines()[-1].split('"n_vocab": ')[1].split(",")[0].rstrip("}"))
     return np.fromfile(of, np.float32).reshape(len(toks), n_vocab), r.stderr
 
@@ -110,6 +121,64 @@ def test_dropin_q8_0_kv_cache(ggufs, tmp_path, incremental):
         kl = klog.read_text()
         assert "kq8=1" in kl and any(ln.startswith("qkv ") and "kq8=1" in ln for ln in kl.splitlines()), kl[-2000:]
         assert any(ln.startswith("fattn_dec2") and "kq8=1" in ln for ln in kl.splitlines()), kl[-2000:]
+
+
+@pytest.mark.parametrize("ctk,ctv", [(8, 1), (1, 8), (8, 2), (2, 1)])
+@pytest.mark.parametrize("incremental", [False, True])
+def test_dropin_mixed_kv_cache(ggufs, tmp_path, incremental, ctk, ctv):
+    """Round 6: K and V caches of different types. -ctk q8_0 -ctv f16 is the fork's own
+    llama-bench line (AGENTS.md:166-176; the reference enables the K-q8_0 / V-f16 kernels
+    with GGML_CUDA_FA_ALL_QUANTS, fattn.cu:220-226) — SET_ROWS into each cache in its own
+    type, FLASH_ATTN_EXT over the pair, against the reference CPU backend with the same
+    caches. The graph must stay in two splits (no CPU fallback of the attention), decode
+    must take the fused QKV (q8_0 rows for the q8_0 side only) and, for f16 / q8_0 pairs,
+    the split-partials decode attention; q4_0 pairs run the tile kernel."""
+    _need_ref()
+    toks = np.random.default_rng(9).integers(0, 1000, 24 if incremental else 40)
+    g = ggufs[("small", "q4_k_m")]
+    klog = tmp_path / "klog.txt"
+    cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental, ctk=ctk, ctv=ctv)
+    gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, ctk=ctk, ctv=ctv, klog=klog)
+    assert "MI355X" in log
+    assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+    kl = klog.read_text().splitlines()
+    if incremental and {ctk, ctv} <= {1, 8}:
+        kq, vq = int(ctk == 8), int(ctv == 8)
+        assert any(ln.startswith("qkv ") and f"kq8={kq} vq8={vq}" in ln for ln in kl), kl[-40:]
+        assert any(ln.startswith("fattn_dec2") and f"kq8={kq} vq8={vq}" in ln for ln in kl), kl[-40:]
+    elif incremental:
+        assert any(ln.startswith("fattn_tile") and f"type={ctk} vtype={ctv}" in ln for ln in kl), kl[-40:]
+    else:
+        assert any(ln.startswith("fa_mma") for ln in kl), kl[-40:]
+
+
+@pytest.mark.parametrize("incremental", [False, True])
+def test_dropin_nofa_q8_0_k_cache(ggufs, tmp_path, incremental):
+    """-fa 0 -ctk q8_0 (V stays f16: libllama refuses a quantised V cache without flash
+    attention): the KQ MUL_MAT reads the q8_0 K cache view, V is stored transposed in f16"""
+    _need_ref()
+    toks = np.random.default_rng(19).integers(0, 1000, 24 if incremental else 40)
+    g = ggufs[("small", "q4_k_m")]
+    cpu, _ = run_ref(tmp_path, g, toks, 0, 0, incremental=incremental, ctk=8, ctv=1)
+    gpu, log = run_ref(tmp_path, g, toks, 99, 0, incremental=incremental, ctk=8, ctv=1)
+    assert "MI355X" in log
+    assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+
+
+def test_dropin_split_count_catches_cpu_fallback(ggufs, tmp_path):
+    """The split assertion itself: with FLASH_ATTN_EXT refused by supports_op
+    (GGML_MI355X_REFUSE_OP, a test knob) libllama schedules every layer's attention on the
+    CPU backend — logits still match, and only the split count shows it"""
+    _need_ref()
+    toks = np.random.default_rng(9).integers(0, 1000, 24)
+    g = ggufs[("small", "q4_k_m")]
+    env = {"GGML_MI355X_REFUSE_OP": "FLASH_ATTN_EXT"}
+    cpu, _ = run_ref(tmp_path, g, toks, 0, 1)
+    with pytest.raises(AssertionError, match="graph splits"):
+        run_ref(tmp_path, g, toks, 99, 1, env_extra=env)
+    gpu, log = run_ref(tmp_path, g, toks, 99, 1, env_extra=env, splits=None)
+    assert nmse(gpu, cpu) < TOL
+    assert graph_splits(log) and min(graph_splits(log)) > 2, graph_splits(log)
 
 
 @pytest.mark.parametrize("shape,recipe", [("small", "q4_k_m"), ("tiny_moe", "q4_k_m")])
@@ -284,8 +353,9 @@ def _kld_stats(p_logits, q_logits):
     return kld, same_top
 
 
-@pytest.mark.parametrize("shape,recipe,ctk", [("small", "q4_k_m", None), ("small", "q8_0", None), ("small", "q4_k_m", 8)])
-def test_dropin_kl_divergence(ggufs, tmp_path, shape, recipe, ctk):
+@pytest.mark.parametrize("shape,recipe,ctk,ctv", [("small", "q4_k_m", None, None), ("small", "q8_0", None, None),
+                                                   ("small", "q4_k_m", 8, None), ("small", "q4_k_m", 8, 1)])
+def test_dropin_kl_divergence(ggufs, tmp_path, shape, recipe, ctk, ctv):
     """End-to-end parity the way the fork checks a backend: KL divergence of the token
     distributions (the reference CPU backend's as P) over a 64-token prompt, prefill and
     incremental decode, and top-1 agreement. Bounds: mean KLD 5e-4, max 5e-3 (measured
@@ -295,10 +365,10 @@ def test_dropin_kl_divergence(ggufs, tmp_path, shape, recipe, ctk):
     toks = np.random.default_rng(11).integers(0, 1000, 64)
     g = ggufs[(shape, recipe)]
     for inc in (False, True):
-        cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=inc, ctk=ctk)
-        gpu, _ = run_ref(tmp_path, g, toks, 99, 1, incremental=inc, ctk=ctk)
+        cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=inc, ctk=ctk, ctv=ctv)
+        gpu, _ = run_ref(tmp_path, g, toks, 99, 1, incremental=inc, ctk=ctk, ctv=ctv)
         kld, top = _kld_stats(cpu, gpu)
-        print(f"kld {shape} {recipe} ctk={ctk} inc={inc}: mean {kld.mean():.3e} p99 {np.percentile(kld, 99):.3e} "
+        print(f"kld {shape} {recipe} ctk={ctk} ctv={ctv} inc={inc}: mean {kld.mean():.3e} p99 {np.percentile(kld, 99):.3e} "
               f"max {kld.max():.3e} top1 {top:.3f}")
         assert kld.mean() < 5e-4 and kld.max() < 5e-3 and top >= 0.90, (kld.mean(), kld.max(), top)
 
@@ -350,8 +420,8 @@ def parse_seq_state(blob):
     return exact, payload
 
 
-@pytest.mark.parametrize("fa,ctk", [(1, None), (0, None), (1, 8)])
-def test_dropin_kv_state(ggufs, tmp_path, fa, ctk):
+@pytest.mark.parametrize("fa,ctk,ctv", [(1, None, None), (0, None, None), (1, 8, None), (1, 8, 1), (0, 8, 1)])
+def test_dropin_kv_state(ggufs, tmp_path, fa, ctk, ctv):
     """KV state save / restore through this backend (SURVEY §5 checkpoint/resume):
     llama_state_seq_get_data / set_data and llama_state_save_file / load_file
     (src/llama-context.cpp:3416-3431) read and write the raw KV rows through get_tensor /
@@ -362,7 +432,7 @@ def test_dropin_kv_state(ggufs, tmp_path, fa, ctk):
     state file), and the cell occupancy (positions, sequence ids, row headers) against the
     reference CPU backend's state; the K/V rows themselves (computed by two backends) and
     the cross-backend continuations within the whole-graph bound. fa 0 stores V
-    transposed; ctk 8 is the q8_0 cache."""
+    transposed; ctk 8 is the q8_0 cache; ctk 8 ctv 1 (round 6) K q8_0 with V f16."""
     probe = os.path.join(ROOT, "oracle", "_ref", "state-probe")
     if not os.path.exists(probe):
         pytest.skip("oracle/_ref/state-probe not built")
@@ -370,7 +440,8 @@ def test_dropin_kv_state(ggufs, tmp_path, fa, ctk):
     rng.integers(0, 1000, 37).astype(np.int32).tofile(tmp_path / "p.i32")
     rng.integers(0, 1000, 6).astype(np.int32).tofile(tmp_path / "g.i32")
     cmd = [probe, "-m", ggufs[("small", "q4_k_m")], "-fa", str(fa), "--prompt", str(tmp_path / "p.i32"),
-           "--gen", str(tmp_path / "g.i32"), "--out", str(tmp_path)] + (["-ctk", str(ctk)] if ctk else [])
+           "--gen", str(tmp_path / "g.i32"), "--out", str(tmp_path)] + (["-ctk", str(ctk)] if ctk else []) + \
+          (["-ctv", str(ctv)] if ctv else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, GGML_BACKEND_PATH=LIB))
     assert r.returncode == 0, r.stderr[-2000:]
     info = json.loads(r.stdout.strip().splitlines()[-1])
