@@ -361,6 +361,7 @@ static void be_free(ggml_backend_t b) {
     if (s->f16.base) hipFree(s->f16.base);
     if (s->rope_tab) hipFree(s->rope_tab);
     if (s->fa_cnt) hipFree(s->fa_cnt);
+    if (s->kvq8_stage) hipFree(s->kvq8_stage);
     if (s->cpy_ev) hipEventDestroy(s->cpy_ev);
     hipStreamDestroy(s->stream);
     delete s;  // the ggml_backend struct lives inside Stream
@@ -463,6 +464,7 @@ static ggml_backend_t make_backend(Device * d) {
     HIP_CHECK(hipMalloc((void **) &s->rope_tab, MX_ROPE_TAB * sizeof(float2)));   // never inside a capture
     HIP_CHECK(hipMalloc((void **) &s->fa_cnt, MX_FA_CNT * sizeof(unsigned int)));
     HIP_CHECK(hipMemset(s->fa_cnt, 0, MX_FA_CNT * sizeof(unsigned int)));
+    HIP_CHECK(hipMalloc((void **) &s->kvq8_stage, MX_KVQ8_STAGE * sizeof(float)));
     s->use_graphs = !env_flag("GGML_MI355X_DISABLE_GRAPHS");
     s->use_fusion = !env_flag("GGML_MI355X_DISABLE_FUSION");
     s->backend.guid = (ggml_guid_t) kGuid;

@@ -95,6 +95,20 @@ struct DeferredNorm {
 };
 
 constexpr int MX_ROPE_TAB = 512;   // RoPE dimension pairs the per-token table holds
+constexpr int MX_KVQ8_STAGE = 32768;   // floats of Stream::kvq8_stage (a K + a V row of one token)
+
+// Round 6: this token's q8_0 K / V cache row(s), staged in f32 by the fused decode QKV launch
+// (ops_qkv.hip) and not yet in the cache: the next decode attention over those caches
+// quantises and stores them (k_fattn_dec2, FaDecArgs::nr_*) — one k_kv_store_q8 launch per
+// layer less; any other consumer first runs that launch (kv_new_row_flush)
+struct KvNewRow {
+    bool on = false;
+    const float * k = nullptr, * v = nullptr;   // staged rows (null: that cache took its row already)
+    char * kc = nullptr, * vc = nullptr;        // cache (view) bases, row strides
+    size_t kc_nb1 = 0, vc_nb1 = 0;
+    const int64_t * kidx = nullptr, * vidx = nullptr;
+    int nk = 0, nv = 0;                          // row lengths (elements)
+};
 constexpr int MX_FA_CNT = 4096;    // decode flash-attn split counters (q rows x KV heads)
 
 struct Stream {
@@ -122,6 +136,8 @@ struct Stream {
     // pass by the first fused QKV block, read by all layers' (same position, same params)
     float * rope_tab = nullptr;        // device, float2 [MX_ROPE_TAB]
     unsigned int * fa_cnt = nullptr;   // device, zeroed; each decode FA launch leaves it zero
+    float * kvq8_stage = nullptr;      // device, MX_KVQ8_STAGE floats (KvNewRow's staged rows)
+    KvNewRow kvnew;
     // weight ranges the next decode attention launch touches while HBM is otherwise idle
     // (fa_prefetch_plan in exec.cpp; consumed by fa_dec2_run)
     const char * pf_ptr[4] = {};
@@ -233,6 +249,10 @@ using UseCount = std::unordered_map<const ggml_tensor *, int>;
 int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 // MoE router chain / expert combine in one launch each (ops_moe.hip); nodes consumed
 int fuse_topk_moe(OpCtx & c, ggml_cgraph * g, int i);
+// the pending q8_0 KV row(s) of KvNewRow: stored by one k_kv_store_q8 launch (ops_qkv.hip)
+void kv_new_row_flush(OpCtx & c);
+// the decode attention `fa` will consume Stream::kvnew itself (ops_fattn_dec.hip)
+bool fa_takes_new_row(const Stream * s, const ggml_tensor * fa);
 // -fa 0 decode attention chain (ops_fattn_dec.hip)
 int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 // FLASH_ATTN_EXT -> RESHAPE -> MUL_MAT(wo) -> ADD(residual) of one decode token (ops_attn_o.hip)

@@ -683,6 +683,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
     act_cache_reset(s);
     s->deferred.clear();
     s->rope_valid = false;
+    s->kvnew.on = false;
     static thread_local std::unordered_map<const ggml_tensor *, int> done;   // run ahead by a group
     done.clear();
     for (int i = 0; i < g->n_nodes; ++i) {
@@ -690,6 +691,9 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         if (is_view_op(n->op) || mx_is_empty(n)) continue;
         if (!done.empty() && done.count(n)) continue;
         s->scratch.reset();
+        // a q8_0 KV row the fused QKV launch left pending: stored now unless this node is the
+        // decode attention that takes it (KvNewRow, backend.h)
+        if (s->kvnew.on && !fa_takes_new_row(s, n)) kv_new_row_flush(c);
         // (pf_n read by the attention launch and gpf_node; the non-FA chain starts at
         // MUL_MAT(k, q) and is matched by fuse_attn_nofa below)
         if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i, n->src[0]->ne[1], false);
@@ -786,6 +790,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
     }
     // every consumer of a deferred norm has run by now; nothing is left pending
     s->deferred.clear();
+    kv_new_row_flush(c);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -670,8 +670,11 @@ void fa_kv_to_f16(OpCtx & c, const ggml_tensor * t, uint16_t * dst) {
 }
 static bool g_fa_mma_off = getenv("GGML_MI355X_FA_TILE") != nullptr;
 
+bool fa_dec2_will_run(const ggml_tensor * dst) { return !g_fa_dec1 && g_tune[10] != 1 && fa_dec2_ok(dst); }
+
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst) {
-    if (!g_fa_dec1 && g_tune[10] != 1 && fa_dec2_ok(dst)) { fa_dec2_run(c, dst); return; }
+    if (fa_dec2_will_run(dst)) { fa_dec2_run(c, dst); return; }
+    kv_new_row_flush(c);   // (the executor flushes before any other consumer; the other kernels read the cache)
     if (!g_fa_mma_off && !fa_use_dec(dst) && fa_mma_ok(dst)) { fa_mma_run(c, dst); return; }
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * k = dst->src[1];

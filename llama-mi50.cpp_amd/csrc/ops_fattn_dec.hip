@@ -44,6 +44,11 @@ struct FaDecArgs {
     // weight prefetch (grid rows y >= nsplit, see fa_prefetch_plan in exec.cpp): one dword
     // per 128-B line of each range, so the next GEMV launches hit the Infinity Cache
     const char * pf[4]; size_t pf_eighth[4]; unsigned pf_lines[4]; int pf_n;   // lines per eighth
+    // round 6: this token's q8_0 K / V row, staged in f32 by the fused decode QKV launch
+    // (KvNewRow, ops_qkv.hip) instead of a k_kv_store_q8 launch: every workgroup quantises
+    // its head's part itself and uses it in place of the cache row (read stale), one per KV
+    // head writes it to the cache. null: the row is in the cache already
+    const float * nr_k; const float * nr_v; const int64_t * nr_ik; const int64_t * nr_iv;
 };
 
 constexpr int FD_NI = 4;          // key-row load instructions per wave per chunk
@@ -206,6 +211,31 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             qh[h][2] = h2v{(_Float16) qb[h].x, (_Float16) qb[h].y}; qh[h][3] = h2v{(_Float16) qb[h].z, (_Float16) qb[h].w};
         }
     }
+    // this token's new K / V row (q8_0 caches, FaDecArgs::nr_*): quantize_row_q8_0 of the
+    // lane's 8 values (the 32-block over 4 lanes: d = amax/127 as f16, q = round(x/d)), the
+    // bytes k_kv_store_q8 would have written
+    int64_t nrk = -1, nrv = -1;
+    uint2 nkq = {0, 0}, nvq = {0, 0};
+    uint16_t nkd = 0, nvd = 0;
+    auto nr_quant = [&](const float * src, uint2 & q8, uint16_t & dh) {
+        const float4 a0 = *(const float4 *) (src + hk * D + 8 * c), a1 = *(const float4 *) (src + hk * D + 8 * c + 4);
+        const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(x[j]));
+        amax = dpp_max_group<4>(amax);
+        const float d = amax / 127.0f, id = d != 0.0f ? 1.0f / d : 0.0f;
+        dh = f2h(d);
+        uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            w0 |= ((uint32_t) (int8_t) roundf(__fmul_rn(x[j], id)) & 0xFFu) << (8 * j);
+            w1 |= ((uint32_t) (int8_t) roundf(__fmul_rn(x[4 + j], id)) & 0xFFu) << (8 * j);
+        }
+        q8 = make_uint2(w0, w1);
+    };
+    if constexpr (KQ) if (p.nr_k) { nrk = *p.nr_ik; nr_quant(p.nr_k, nkq, nkd); }
+    if constexpr (VQ) if (p.nr_v) { nrv = *p.nr_iv; nr_quant(p.nr_v, nvq, nvd); }
     // running (max, sum, O) of this wave; O not yet reduced over the wave's key rows
     float M[G], L[G], o[G][8];
 #pragma unroll
@@ -258,12 +288,16 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         if (first) { asm volatile("" :: "v"(b.kr[0].x), "v"(b.vr[0].x), "v"(b.vr[NI - 1].w)); MX_TRACE(tr, 2); }
 #pragma unroll
         for (int t = 0; t < NI; ++t) {
+            // the new row replaces its stale cache copy (selects, no branch)
+            const bool isnk = key0 + t * KPI == nrk;
+            const uint32_t kx = isnk ? nkq.x : b.kr[t].x, ky = isnk ? nkq.y : b.kr[t].y;
+            const uint16_t kdd = isnk ? nkd : b.kd[t];
 #pragma unroll
             for (int h = 0; h < G; ++h) {
                 float acc;
                 if constexpr (KQ) {
-                    const int si = dot4_i8((int) b.kr[t].y, qq8[h][1], dot4_i8((int) b.kr[t].x, qq8[h][0], 0));
-                    acc = (float) si * (qd[h] * h2f(b.kd[t]));
+                    const int si = dot4_i8((int) ky, qq8[h][1], dot4_i8((int) kx, qq8[h][0], 0));
+                    acc = (float) si * (qd[h] * h2f(kdd));
                 } else {
                     acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, b.kr[t].x), qh[h][0], 0.f, false);
                     acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, b.kr[t].y), qh[h][1], acc, false);
@@ -295,8 +329,9 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
 #pragma unroll
             for (int t = 0; t < NI; ++t) {
                 if constexpr (VQ) {
-                    const float dv = h2f(b.vd[t]);
-                    const uint32_t vw[2] = {b.vr[t].x, b.vr[t].y};
+                    const bool isnv = key0 + t * KPI == nrv;
+                    const float dv = h2f(isnv ? nvd : b.vd[t]);
+                    const uint32_t vw[2] = {isnv ? nvq.x : b.vr[t].x, isnv ? nvq.y : b.vr[t].y};
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
                         o[h][i] += pr[t] * (dv * (float) (int8_t) ((vw[i >> 2] >> (8 * (i & 3))) & 0xFF));
@@ -336,6 +371,18 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             if (ci == 0) MX_TRACE(tr, 1);
             process(ch, b, ci == 0);
         }
+    }
+    // one workgroup per KV head stores the new q8_0 rows (the others read the stale copy and
+    // replaced it): lanes of key row 0 of wave 0, 8 quants each, the block scale by its first lane
+    if ((KQ || VQ) && gb == 0 && split == 0 && iq1 == 0 && iq3 == 0 && wave == 0 && kq == 0) {
+        auto put = [&](const char * base, size_t stride, int64_t row, uint2 q8, uint16_t dh) {
+            char * rp = const_cast<char *>(base) + (size_t) row * stride;
+            uint16_t * qp = (uint16_t *) (rp + lofs8);           // 2-byte aligned (34-B blocks)
+            qp[0] = (uint16_t) q8.x; qp[1] = (uint16_t) (q8.x >> 16); qp[2] = (uint16_t) q8.y; qp[3] = (uint16_t) (q8.y >> 16);
+            if ((c & 3) == 0) *(uint16_t *) (rp + dofs) = dh;
+        };
+        if (KQ && nrk >= 0) put(kb - lofsk, p.k1, nrk, nkq, nkd);
+        if (VQ && nrv >= 0) put(vb - lofsv, p.v1, nrv, nvq, nvd);
     }
 #pragma unroll
     for (int h = 0; h < G; ++h) {
@@ -486,6 +533,7 @@ __global__ __launch_bounds__(256) void k_fattn_dec2_combine(FaDecArgs p) {
 
 // eligibility: f16 K/V, D 64/128, GQA ratio 1-8, a plain f16 mask broadcast over heads,
 // no softcap / ALiBi / sinks, few query rows (decode)
+bool fa_dec2_will_run(const ggml_tensor * dst);   // ops_fattn.hip: op_flash_attn_ext's choice
 bool fa_dec2_ok(const ggml_tensor * dst) {
     const ggml_tensor * q = dst->src[0], * k = dst->src[1], * v = dst->src[2], * m = dst->src[3];
     const bool kq = k->type == GGML_TYPE_Q8_0, vq = v->type == GGML_TYPE_Q8_0;
@@ -558,6 +606,35 @@ static FdCfg fd_cfg(int D, int Gt, int64_t n_kv, int64_t rows, int kv) {   // ro
 static size_t fd3_scratch(const ggml_tensor * dst);
 static bool fd3_run(OpCtx & c, ggml_tensor * dst);
 
+// Round 6: the fused QKV launch's pending q8_0 row(s) (Stream::kvnew) belong to this
+// attention when it reads exactly those caches, one token of one sequence
+static bool fd_new_row_match(const KvNewRow & r, const ggml_tensor * fa) {
+    const ggml_tensor * q = fa->src[0], * k = fa->src[1], * v = fa->src[2];
+    if (!r.on || q->ne[1] != 1 || q->ne[3] != 1 || k->ne[3] != 1 || v->ne[3] != 1) return false;
+    const int64_t D = k->ne[0];
+    auto same = [&](const ggml_tensor * t, const char * base, size_t nb1, int n) {
+        return t->type == GGML_TYPE_Q8_0 && (const char *) t->data == base && t->nb[1] == nb1 && t->nb[2] == (size_t) (D / 32) * 34 &&
+               t->ne[0] * t->ne[2] == n;
+    };
+    if (r.k && !same(k, r.kc, r.kc_nb1, r.nk)) return false;
+    if (r.v && !same(v, r.vc, r.vc_nb1, r.nv)) return false;
+    // (a cache that took its row in the QKV launch must still be this attention's)
+    if (!r.k && (const char *) k->data != r.kc) return false;
+    if (!r.v && (const char *) v->data != r.vc) return false;
+    return true;
+}
+bool fa_takes_new_row(const Stream * s, const ggml_tensor * fa) {
+    return fa->op == GGML_OP_FLASH_ATTN_EXT && fd_new_row_match(s->kvnew, fa) && fa_dec2_will_run(fa);
+}
+static void fd_take_new_row(OpCtx & c, const ggml_tensor * dst, FaDecArgs & a) {
+    KvNewRow & r = c.s->kvnew;
+    if (!r.on) return;
+    if (!fd_new_row_match(r, dst)) { kv_new_row_flush(c); return; }   // (the executor normally did)
+    a.nr_k = r.k; a.nr_ik = r.kidx;
+    a.nr_v = r.v; a.nr_iv = r.vidx;
+    r.on = false;
+}
+
 size_t fa_dec2_scratch(const ggml_tensor * dst) {
     if (const size_t s3 = fd3_scratch(dst)) return s3;
     const ggml_tensor * q = dst->src[0], * k = dst->src[1];
@@ -594,6 +671,7 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     a.nsplit = f.nsplit;
     a.part = (float *) c.scratch->take(fa_dec2_scratch(dst));
     a.cnt = c.s->fa_cnt;
+    fd_take_new_row(c, dst, a);
     a.trace = mx_trace_slot(0);
     a.trace_blk = mx_trace_blocks();
     const unsigned gx = (unsigned) (a.Hkv * (Gt / f.G) * a.n_q * q->ne[3]);
@@ -609,8 +687,8 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
     } else a.pf_n = 0;
     const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
     const int kv = fd_kv_code(k, v);
-    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d vq8=%d pf_rows=%u long=%d cpw=%d", D, f.G, f.NW, f.nsplit,
-            a.n_kv, a.H, a.Hkv, (int) fd_kq(kv), (int) fd_vq(kv), pf_rows, (int) f.lng, f.cpw);
+    MX_KLOG("fattn_dec2 D=%d G=%d NW=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d vq8=%d pf_rows=%u long=%d cpw=%d newrow=%d", D, f.G, f.NW,
+            f.nsplit, a.n_kv, a.H, a.Hkv, (int) fd_kq(kv), (int) fd_vq(kv), pf_rows, (int) f.lng, f.cpw, (int) (a.nr_k || a.nr_v));
     if (f.lng) {
         const unsigned gc = gx * (unsigned) f.G;                     // one combine workgroup per query head
         const size_t lds = (size_t) f.nsplit * sizeof(float);
@@ -682,6 +760,7 @@ void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit) {
     a.part = part;
     a.to_part = 1;
     a.cnt = c.s->fa_cnt;
+    fd_take_new_row(c, dst, a);
     a.trace = mx_trace_slot(0);
     a.trace_blk = mx_trace_blocks();
     const unsigned gx = (unsigned) a.H;                          // G = 1: one query head per workgroup
@@ -702,8 +781,8 @@ void fa_dec2_partials(OpCtx & c, ggml_tensor * dst, float * part, int nsplit) {
     const dim3 grid(gx, (unsigned) a.nsplit + pf_rows);
     const int kv = fd_kv_code(k, v);
     const int ni = fa_split_ni();
-    MX_KLOG("fattn_dec2_part D=128 G=1 NI=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d vq8=%d pf_rows=%u", ni, nsplit, a.n_kv, a.H, a.Hkv,
-            (int) fd_kq(kv), (int) fd_vq(kv), pf_rows);
+    MX_KLOG("fattn_dec2_part D=128 G=1 NI=%d nsplit=%d n_kv=%d H=%d Hkv=%d kq8=%d vq8=%d pf_rows=%u newrow=%d", ni, nsplit, a.n_kv, a.H,
+            a.Hkv, (int) fd_kq(kv), (int) fd_vq(kv), pf_rows, (int) (a.nr_k || a.nr_v));
     if (ni == 2) fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<128, 1, 4, decltype(KVC)::value, 2, true><<<grid, 256, 0, c.st>>>(a); });
     else if (ni == 8) fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<128, 1, 4, decltype(KVC)::value, 8, true><<<grid, 256, 0, c.st>>>(a); });
     else fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<128, 1, 4, decltype(KVC)::value, 4, true><<<grid, 256, 0, c.st>>>(a); });

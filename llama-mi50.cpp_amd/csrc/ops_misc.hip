@@ -155,6 +155,22 @@ __global__ void k_set_rows_q8_0(const char * __restrict__ src, const char * __re
     for (int b = threadIdx.x; b < nblk; b += blockDim.x) quantize_block_q8_0(in + 32 * b, out + 34 * b);
 }
 
+// q4_0 caches (-ctk / -ctv q4_0): the same with quantize_block_q4_0 (18-B blocks)
+template <typename TI>
+__global__ void k_set_rows_q4_0(const char * __restrict__ src, const char * __restrict__ idx, char * __restrict__ dst,
+                                T4 s0, T4 s1, T4 d) {
+    const int64_t r = blockIdx.x;
+    const int64_t i = r % s0.ne[1];
+    const int64_t i02 = (r / s0.ne[1]) % s0.ne[2];
+    const int64_t i03 = r / (s0.ne[1] * s0.ne[2]);
+    const int64_t i11 = i02 % s1.ne[1], i12 = i03 % s1.ne[2];
+    const int64_t i1 = (int64_t) *(const TI *) (idx + i * s1.nb[0] + i11 * s1.nb[1] + i12 * s1.nb[2]);
+    const float * in = (const float *) (src + i * s0.nb[1] + i02 * s0.nb[2] + i03 * s0.nb[3]);
+    char * out = dst + i1 * d.nb[1] + i02 * d.nb[2] + i03 * d.nb[3];
+    const int nblk = (int) (s0.ne[0] / 32);
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) quantize_block_q4_0(in + 32 * b, out + 18 * b);
+}
+
 // SET_ROWS of one-element rows: the transposed V cache store of the non-flash-attention
 // graph (src/llama-kv-cache.cpp cpy_v with v_trans: v_cur [n_embd_v, n_tokens] reshaped to
 // [1, n_embd_v * n_tokens], one index per element, element (d, t) -> row d * kv_size +
@@ -233,6 +249,10 @@ void op_set_rows(OpCtx & c, ggml_tensor * dst) {
         case GGML_TYPE_Q8_0:
             if (i64) k_set_rows_q8_0<int64_t><<<grid, dim3(64), 0, c.st>>>(a, ix, o, g0, g1, gd);
             else     k_set_rows_q8_0<int32_t><<<grid, dim3(64), 0, c.st>>>(a, ix, o, g0, g1, gd);
+            break;
+        case GGML_TYPE_Q4_0:
+            if (i64) k_set_rows_q4_0<int64_t><<<grid, dim3(64), 0, c.st>>>(a, ix, o, g0, g1, gd);
+            else     k_set_rows_q4_0<int32_t><<<grid, dim3(64), 0, c.st>>>(a, ix, o, g0, g1, gd);
             break;
         default: MX_ABORT("set_rows: dst type %d", (int) dst->type);
     }
@@ -989,7 +1009,7 @@ bool supports_op(const ggml_tensor * op) {
         case GGML_OP_SET_ROWS:
             return s0->type == GGML_TYPE_F32 && (s1->type == GGML_TYPE_I64 || s1->type == GGML_TYPE_I32) &&
                    (op->type == GGML_TYPE_F32 || op->type == GGML_TYPE_F16 || op->type == GGML_TYPE_BF16 ||
-                    (op->type == GGML_TYPE_Q8_0 && s0->ne[0] % 32 == 0));
+                    ((op->type == GGML_TYPE_Q8_0 || op->type == GGML_TYPE_Q4_0) && s0->ne[0] % 32 == 0));
         case GGML_OP_DUP: case GGML_OP_CONT: case GGML_OP_CPY: {
             const int ts = s0->type, td = op->type;
             if (ts == td && mx_is_contiguous(s0) && mx_is_contiguous(op)) return true;

@@ -142,6 +142,19 @@ __global__ __launch_bounds__(256) void k_kv_store_q8(QkvArgs p, int nk, int nv) 
     if ((i & 31) == 0) *(uint16_t *) blk = f2h(d);
 }
 
+void kv_new_row_flush(OpCtx & c) {
+    KvNewRow & r = c.s->kvnew;
+    if (!r.on) return;
+    r.on = false;
+    QkvArgs p{};
+    p.kq8f = const_cast<float *>(r.k); p.vq8f = const_cast<float *>(r.v);
+    p.kc = r.kc; p.kc_nb1 = r.kc_nb1; p.vc = r.vc; p.vc_nb1 = r.vc_nb1;
+    p.kidx = (const char *) r.kidx; p.vidx = (const char *) r.vidx;
+    const int nk = r.k ? r.nk : 0, nv = r.v ? r.nv : 0;
+    MX_KLOG("kv_store_q8 nk=%d nv=%d", nk, nv);
+    k_kv_store_q8<<<(unsigned) mx_ceil_div(nk + nv, 256), 256, 0, c.st>>>(p, nk, nv);
+}
+
 // (cos θ·m, sin θ·m) for every dimension pair of one position: rope_yarn
 // (ggml-cpu/ops.cpp:5529-5546) with theta by repeated multiplication as rope_cache_init
 // (ops.cpp:5548-5566) — the per-pair values of op_rope, computed once per token.
@@ -534,8 +547,18 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
 #undef QKB
         if (kb) { kern = kb; grid = dim3((unsigned) (wq->ne[1] / 16)); nthr = 448; }
     }
-    if (kq8) p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
-    if (vq8) p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
+    // round 6: the q8_0 rows go to the stream's persistent stage and are left to the decode
+    // attention (KvNewRow) unless GGML_MI355X_NO_KV_DEFER / g_tune[40] = 1 (A/B: a
+    // k_kv_store_q8 launch right after this one, the round-5 form)
+    static const bool no_defer = getenv("GGML_MI355X_NO_KV_DEFER") != nullptr;
+    const bool defer = anyq8 && !no_defer && g_tune[40] != 1 && wk->ne[1] + wv->ne[1] <= MX_KVQ8_STAGE;
+    if (defer) {
+        if (kq8) p.kq8f = c.s->kvq8_stage;
+        if (vq8) p.vq8f = c.s->kvq8_stage + wk->ne[1];
+    } else {
+        if (kq8) p.kq8f = (float *) c.scratch->take(4 * wk->ne[1]);
+        if (vq8) p.vq8f = (float *) c.scratch->take(4 * wv->ne[1]);
+    }
     if (split) {
         int remote = 0;
         for (int k = 0; k < ns; ++k) remote += !split_on_main(c.s, wq, sdev[0][k]);
@@ -567,7 +590,16 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
     hipLaunchKernelGGL(kern, grid, dim3(nthr), gemv_lds_bytes(p.K, mode), c.st, p);
     if (anyq8) {   // the q8_0 rows (nk / nv = 0: that cache took its f16 row in the launch above)
         const int nk = kq8 ? (int) wk->ne[1] : 0, nv = vq8 ? (int) wv->ne[1] : 0;
-        k_kv_store_q8<<<(unsigned) mx_ceil_div(nk + nv, 256), 256, 0, c.st>>>(p, nk, nv);
+        if (defer) {
+            KvNewRow & r = c.s->kvnew;
+            r.on = true;
+            r.k = p.kq8f; r.v = p.vq8f;
+            r.kc = p.kc; r.kc_nb1 = p.kc_nb1; r.vc = p.vc; r.vc_nb1 = p.vc_nb1;
+            r.kidx = (const int64_t *) kix->data; r.vidx = (const int64_t *) vix->data;
+            r.nk = nk; r.nv = nv;
+        } else {
+            k_kv_store_q8<<<(unsigned) mx_ceil_div(nk + nv, 256), 256, 0, c.st>>>(p, nk, nv);
+        }
     }
     return last - i + 1;
 }

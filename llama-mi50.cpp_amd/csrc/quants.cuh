@@ -107,4 +107,23 @@ __device__ __forceinline__ void quantize_block_q8_0(const float * x, char * out)
     for (int j = 0; j < 32; ++j) out[2 + j] = (int8_t) roundf(__fmul_rn(x[j], id));
 }
 
+// quantize_row_q4_0_ref (ggml-quants.c:36-71), one 32-element block -> block_q4_0 (18 B):
+// d = (the value of largest magnitude, first one on ties) / -8 as f16,
+// nibble = min(15, (int8) (x/d + 8.5)), elements 0-15 low nibbles, 16-31 high
+__device__ __forceinline__ void quantize_block_q4_0(const float * x, char * out) {
+    float amax = 0.0f, mx = 0.0f;
+    for (int j = 0; j < 32; ++j) {
+        const float v = x[j];
+        if (amax < fabsf(v)) { amax = fabsf(v); mx = v; }
+    }
+    const float d = mx / -8;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    const uint16_t dh = f2h(d);
+    memcpy(out, &dh, 2);
+    for (int j = 0; j < 16; ++j) {
+        const int8_t a0 = (int8_t) (__fmul_rn(x[j], id) + 8.5f), a1 = (int8_t) (__fmul_rn(x[16 + j], id) + 8.5f);
+        out[2 + j] = (char) ((uint8_t) min((int) a0, 15) | ((uint8_t) min((int) a1, 15) << 4));
+    }
+}
+
 }  // namespace mx

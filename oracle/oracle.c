@@ -194,6 +194,29 @@ void orc_quantize_row_q8_0(const float * x, void * vy, int64_t k) {
     }
 }
 
+/* quantize_row_q4_0_ref (ggml-quants.c:36-71): d = (the signed value of largest magnitude)
+ * / -8 as f16, nibble = min(15, (int8) (x/d + 8.5)); low nibbles hold elements 0-15, high
+ * nibbles 16-31 (a q4_0 V / K cache row: SET_ROWS's from_float) */
+void orc_quantize_row_q4_0(const float * x, void * vy, int64_t k) {
+    uint8_t * y = (uint8_t *) vy;
+    for (int64_t i = 0; i < k / 32; ++i) {
+        float amax = 0.0f, max = 0.0f;
+        for (int j = 0; j < 32; ++j) {
+            const float v = x[32 * i + j];
+            if (amax < fabsf(v)) { amax = fabsf(v); max = v; }
+        }
+        const float d = max / -8, id = d ? 1.0f / d : 0.0f;
+        const uint16_t dh = orc_fp32_to_fp16(d);
+        memcpy(y + 18 * i, &dh, 2);
+        for (int j = 0; j < 16; ++j) {
+            const float x0 = x[32 * i + j] * id, x1 = x[32 * i + 16 + j] * id;
+            const int8_t a0 = (int8_t) (x0 + 8.5f), a1 = (int8_t) (x1 + 8.5f);
+            const uint8_t q0 = (uint8_t) (a0 < 15 ? a0 : 15), q1 = (uint8_t) (a1 < 15 ? a1 : 15);
+            y[18 * i + 2 + j] = (uint8_t) (q0 | (q1 << 4));
+        }
+    }
+}
+
 /* quantize_row_q8_1_ref (ggml-quants.c:229-258): 36-byte blocks {d, s=d·Σq, qs[32]} */
 void orc_quantize_row_q8_1(const float * x, void * vy, int64_t k) {
     uint8_t * y = (uint8_t *) vy;
@@ -501,9 +524,19 @@ static float orc_round_bf16(float f) {
 int orc_flash_attn_t(const float * q, const void * k, const void * v, const uint16_t * mask,
                      float * out, int64_t D, int64_t n_q, int64_t n_kv, int64_t H, int64_t Hkv,
                      float scale, float max_bias, float softcap, int kv_type) {
+    return orc_flash_attn_kv(q, k, v, mask, out, D, n_q, n_kv, H, Hkv, scale, max_bias, softcap, kv_type, kv_type);
+}
+
+/* K and V of different types (ops.cpp:8045-8260 takes q_to_vec_dot from K's type and
+ * v_to_float from V's: -ctk q8_0 -ctv f16 and the like) */
+int orc_flash_attn_kv(const float * q, const void * k, const void * v, const uint16_t * mask,
+                      float * out, int64_t D, int64_t n_q, int64_t n_kv, int64_t H, int64_t Hkv,
+                      float scale, float max_bias, float softcap, int kv_type, int v_type) {
     if (kv_type != T_F32 && kv_type != T_F16 && kv_type != T_BF16 && kv_type != T_Q8_0 && kv_type != T_Q4_0) return -1;
-    if (D % blck(kv_type)) return -1;
+    if (v_type != T_F32 && v_type != T_F16 && v_type != T_BF16 && v_type != T_Q8_0 && v_type != T_Q4_0) return -1;
+    if (D % blck(kv_type) || D % blck(v_type)) return -1;
     const size_t rb = (size_t) (D / blck(kv_type)) * bsize(kv_type);
+    const size_t rbv = (size_t) (D / blck(v_type)) * bsize(v_type);
     if (softcap != 0) scale /= softcap;
     const uint32_t n_head_log2 = 1u << (uint32_t) floor(log2((double) H));
     const float m0 = powf(2.0f, -(max_bias) / n_head_log2);
@@ -540,7 +573,7 @@ int orc_flash_attn_t(const float * q, const void * k, const void * v, const uint
                 double ms = 1, vs = 1;
                 if (sf > M) { const double Mold = M; M = sf; ms = isinf(Mold) ? 0 : exp(Mold - M); for (int64_t d = 0; d < D; ++d) acc[d] *= ms; }
                 else vs = exp(sf - M);
-                orc_dequantize_row(kv_type, (const uint8_t *) v + (size_t) (hk * n_kv + ic) * rb, vr, D);
+                orc_dequantize_row(v_type, (const uint8_t *) v + (size_t) (hk * n_kv + ic) * rbv, vr, D);
                 for (int64_t d = 0; d < D; ++d) acc[d] += vs * vr[d];
                 S = S * ms + vs;
             }

@@ -23,6 +23,8 @@ uint16_t orc_fp32_to_fp16(float f);
 int  orc_dequantize_row(int type, const void * x, float * y, int64_t k);
 /* quantize_row_q8_0_ref / q8_1_ref / q8_K_ref (ggml-quants.c:199-258, 2555-2592) */
 void orc_quantize_row_q8_0(const float * x, void * y, int64_t k);
+/* quantize_row_q4_0_ref (ggml-quants.c:36-71) */
+void orc_quantize_row_q4_0(const float * x, void * y, int64_t k);
 void orc_quantize_row_q8_1(const float * x, void * y, int64_t k);
 void orc_quantize_row_q8_K(const float * x, void * y, int64_t k);
 
@@ -65,6 +67,10 @@ void orc_flash_attn(const float * q, const uint16_t * k, const uint16_t * v, con
 int orc_flash_attn_t(const float * q, const void * k, const void * v, const uint16_t * mask,
                      float * out, int64_t D, int64_t n_q, int64_t n_kv, int64_t H, int64_t Hkv,
                      float scale, float max_bias, float softcap, int kv_type);
+/* the same with K and V of different types (kv_type: K, v_type: V) */
+int orc_flash_attn_kv(const float * q, const void * k, const void * v, const uint16_t * mask,
+                      float * out, int64_t D, int64_t n_q, int64_t n_kv, int64_t H, int64_t Hkv,
+                      float scale, float max_bias, float softcap, int kv_type, int v_type);
 
 #ifdef __cplusplus
 }

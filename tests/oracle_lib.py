@@ -18,7 +18,7 @@ class Oracle:
         L.orc_fp16_to_fp32.restype = ctypes.c_float; L.orc_fp16_to_fp32.argtypes = [ctypes.c_uint16]
         L.orc_fp32_to_fp16.restype = ctypes.c_uint16; L.orc_fp32_to_fp16.argtypes = [ctypes.c_float]
         L.orc_dequantize_row.restype = ctypes.c_int; L.orc_dequantize_row.argtypes = [ctypes.c_int, P, P, ctypes.c_int64]
-        for n in ("orc_quantize_row_q8_0", "orc_quantize_row_q8_1", "orc_quantize_row_q8_K"):
+        for n in ("orc_quantize_row_q8_0", "orc_quantize_row_q4_0", "orc_quantize_row_q8_1", "orc_quantize_row_q8_K"):
             getattr(L, n).restype = None; getattr(L, n).argtypes = [P, P, ctypes.c_int64]
         for n in ("orc_mul_mat", "orc_mul_mat_exact"):
             getattr(L, n).restype = ctypes.c_int
@@ -32,6 +32,8 @@ class Oracle:
         L.orc_flash_attn.argtypes = [P, P, P, P, P] + [ctypes.c_int64] * 5 + [ctypes.c_float] * 3
         L.orc_flash_attn_t.restype = ctypes.c_int
         L.orc_flash_attn_t.argtypes = [P, P, P, P, P] + [ctypes.c_int64] * 5 + [ctypes.c_float] * 3 + [ctypes.c_int]
+        L.orc_flash_attn_kv.restype = ctypes.c_int
+        L.orc_flash_attn_kv.argtypes = [P, P, P, P, P] + [ctypes.c_int64] * 5 + [ctypes.c_float] * 3 + [ctypes.c_int] * 2
 
     @staticmethod
     def _p(a):
@@ -47,6 +49,12 @@ class Oracle:
         x = np.ascontiguousarray(x, np.float32)
         y = np.zeros(len(x) // 32 * 34, np.uint8)
         self.lib.orc_quantize_row_q8_0(x.ctypes.data, y.ctypes.data, len(x))
+        return y
+
+    def quantize_q4_0(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros(len(x) // 32 * 18, np.uint8)
+        self.lib.orc_quantize_row_q4_0(x.ctypes.data, y.ctypes.data, len(x))
         return y
 
     def mul_mat(self, type_id, w, row_bytes, x, exact=False):
@@ -105,14 +113,16 @@ class Oracle:
                                 D, n_q, n_kv, H, Hkv, scale, max_bias, softcap)
         return out
 
-    def flash_attn_t(self, q, k, v, mask, scale, kv_type, max_bias=0.0, softcap=0.0):
-        """k, v: [Hkv, n_kv, row_bytes] uint8 rows of ggml type kv_type (f32 0, f16 1, q4_0 2, q8_0 8, bf16 30)"""
+    def flash_attn_t(self, q, k, v, mask, scale, kv_type, max_bias=0.0, softcap=0.0, v_type=None):
+        """k, v: [Hkv, n_kv, row_bytes] uint8 rows of ggml type kv_type (f32 0, f16 1, q4_0 2, q8_0 8, bf16 30);
+        v_type: V's own type when it differs from K's"""
         H, n_q, D = q.shape
         Hkv, n_kv = k.shape[:2]
         out = np.empty((n_q, H, D), np.float32)
         q = np.ascontiguousarray(q, np.float32); k = np.ascontiguousarray(k); v = np.ascontiguousarray(v)
-        assert self.lib.orc_flash_attn_t(q.ctypes.data, k.ctypes.data, v.ctypes.data, self._p(mask), out.ctypes.data,
-                                         D, n_q, n_kv, H, Hkv, scale, max_bias, softcap, kv_type) == 0
+        vt = kv_type if v_type is None else v_type
+        assert self.lib.orc_flash_attn_kv(q.ctypes.data, k.ctypes.data, v.ctypes.data, self._p(mask), out.ctypes.data,
+                                          D, n_q, n_kv, H, Hkv, scale, max_bias, softcap, kv_type, vt) == 0
         return out
 
 

@@ -121,6 +121,10 @@ def test_dropin_q8_0_kv_cache(ggufs, tmp_path, incremental):
         kl = klog.read_text()
         assert "kq8=1" in kl and any(ln.startswith("qkv ") and "kq8=1" in ln for ln in kl.splitlines()), kl[-2000:]
         assert any(ln.startswith("fattn_dec2") and "kq8=1" in ln for ln in kl.splitlines()), kl[-2000:]
+        # round 6: the token's q8_0 rows are quantised and stored by the attention launch
+        # (KvNewRow), not by a k_kv_store_q8 launch of their own
+        assert all("newrow=1" in ln for ln in kl.splitlines() if ln.startswith("fattn_dec2")), kl[-2000:]
+        assert not any(ln.startswith("kv_store_q8") for ln in kl.splitlines()), kl[-2000:]
 
 
 @pytest.mark.parametrize("ctk,ctv", [(8, 1), (1, 8), (8, 2), (2, 1)])
@@ -145,7 +149,8 @@ def test_dropin_mixed_kv_cache(ggufs, tmp_path, incremental, ctk, ctv):
     if incremental and {ctk, ctv} <= {1, 8}:
         kq, vq = int(ctk == 8), int(ctv == 8)
         assert any(ln.startswith("qkv ") and f"kq8={kq} vq8={vq}" in ln for ln in kl), kl[-40:]
-        assert any(ln.startswith("fattn_dec2") and f"kq8={kq} vq8={vq}" in ln for ln in kl), kl[-40:]
+        assert any(ln.startswith("fattn_dec2") and f"kq8={kq} vq8={vq} " in ln and "newrow=1" in ln for ln in kl), kl[-40:]
+        assert not any(ln.startswith("kv_store_q8") for ln in kl), kl[-40:]
     elif incremental:
         assert any(ln.startswith("fattn_tile") and f"type={ctk} vtype={ctv}" in ln for ln in kl), kl[-40:]
     else:

@@ -118,6 +118,36 @@ def test_set_rows_f16_bit_exact(pkg, backend, orc, idx_type):
     assert not out[untouched].any()
 
 
+@pytest.mark.parametrize("kind,idx_type", [("q8_0", "i64"), ("q4_0", "i64"), ("q4_0", "i32")])
+def test_set_rows_quantised_bit_exact(pkg, backend, orc, kind, idx_type):
+    """SET_ROWS into a q8_0 / q4_0 KV cache (-ctk / -ctv q8_0 / q4_0): every stored row equals
+    the oracle's quantize_row_<type>_ref bytes (tests/test_oracle.py pins those to the
+    reference's C quantiser); cells not indexed stay untouched"""
+    rng = np.random.default_rng(6)
+    D, cells, n = 1024, 48, 5
+    src = (rng.standard_normal((n, D)) * np.array([1e-3, 1, 5, 200, 1])[:, None]).astype(np.float32)
+    src[1, :32] = 0.0                               # an all-zero block: d = 0
+    idx = rng.permutation(cells)[:n].astype(np.int64 if idx_type == "i64" else np.int32)
+    bs = 34 if kind == "q8_0" else 18
+    row = D // 32 * bs
+
+    ctx = pkg.Context()
+    cache = ctx.new_tensor(kind, D, cells)
+    ts = ctx.new_tensor("f32", D, n)
+    ti = ctx.new_tensor(idx_type, n)
+    g = ctx.build(ctx.set_rows(cache, ts, ti))
+    ctx.alloc(backend)
+    cache.set(np.zeros(cells * row, np.uint8)); ts.set(src); ti.set(idx)
+    ctx.compute(backend, g)
+    out = cache.get_bytes().reshape(cells, row)
+    ctx.free()
+    quant = orc.quantize_q8_0 if kind == "q8_0" else orc.quantize_q4_0
+    for j, cidx in enumerate(idx):
+        assert np.array_equal(out[cidx], quant(src[j])), j
+    untouched = np.setdiff1d(np.arange(cells), idx)
+    assert not out[untouched].any()
+
+
 @pytest.mark.parametrize("idx_type,n_tok,dtype", [("i64", 512, "f16"), ("i64", 7, "f16"), ("i32", 100, "f32")])
 def test_set_rows_transposed_v(pkg, backend, orc, idx_type, n_tok, dtype):
     """the non-flash-attention V store (llama_kv_cache::cpy_v, v_trans): v_cur [D, n_tok]
@@ -424,6 +454,47 @@ def test_flash_attn_kv_types(pkg, backend, orc, kind, n_q, n_kv, H, Hkv, D, soft
         assert any(ln.startswith("fattn_dec2") and "kq8=1" in ln for ln in log), log
     if n_q >= 16 and softcap == 0.0 and kind != "f32":
         assert any(ln.startswith("fa_kv_to_f16") for ln in log) and any(ln.startswith("fa_mma") for ln in log), log
+
+
+@pytest.mark.parametrize("kt,vt", [("q8_0", "f16"), ("f16", "q8_0"), ("q4_0", "f16"), ("q8_0", "q4_0")])
+@pytest.mark.parametrize("n_q,n_kv,H,Hkv,D", [
+    (1, 256, 32, 8, 128),      # tg128 decode step (f16 / q8_0 pairs: k_fattn_dec2, KV 2 / 3)
+    (1, 1500, 32, 8, 128),     # long cache: the LONG geometry + combine
+    (512, 512, 32, 8, 128),    # pp512 prefill: the quantised side copied to f16, k_fa_mma2
+    (3, 130, 8, 2, 64),        # a few query rows, D 64
+])
+def test_flash_attn_mixed_kv_types(pkg, backend, orc, kt, vt, n_q, n_kv, H, Hkv, D):
+    """Round 6: K and V caches of different types (-ctk q8_0 -ctv f16, the fork's own line,
+    AGENTS.md:166-176; the reference's FA_ALL_QUANTS pairs, fattn.cu:220-260) against the
+    oracle with K's and V's own dequantisation (orc_flash_attn_kv)"""
+    from qgen import KV_TYPES, kv_rows
+    rng = np.random.default_rng(n_q * 1000 + n_kv + D + 7)
+    q = rng.standard_normal((H, n_q, D)).astype(np.float32)
+    k = kv_rows(kt, Hkv, n_kv, D, rng, orc)
+    v = kv_rows(vt, Hkv, n_kv, D, rng, orc)
+    mask = np.zeros((n_q, n_kv), np.float32)
+    for i in range(n_q):
+        mask[i, n_kv - n_q + i + 1:] = -np.inf
+    m16 = mask.astype(np.float16).view(np.uint16)
+    scale = 1.0 / np.sqrt(D)
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, n_q, H)
+        tk = ctx.new_tensor(KV_TYPES[kt], D, n_kv, Hkv)
+        tv = ctx.new_tensor(KV_TYPES[vt], D, n_kv, Hkv)
+        tm = ctx.new_tensor("f16", n_kv, n_q)
+        return [ctx.flash_attn_ext(tq, tk, tv, tm, scale, 0.0, 0.0)], [(tq, q), (tk, k), (tv, v), (tm, m16)]
+
+    backend.klog(True)
+    y = run(pkg, backend, build)[0].reshape(n_q, H, D)
+    log = backend.klog_read()
+    backend.klog(False)
+    ref = orc.flash_attn_t(q, k, v, m16, scale, KV_TYPES[kt], v_type=KV_TYPES[vt])
+    assert nmse(y, ref) < 5e-4, nmse(y, ref)
+    if n_q <= 4 and {kt, vt} <= {"f16", "q8_0"}:
+        assert any(ln.startswith("fattn_dec2") and f"kq8={int(kt == 'q8_0')} vq8={int(vt == 'q8_0')}" in ln for ln in log), log
+    if n_q >= 16:
+        assert any(ln.startswith("fa_mma") for ln in log), log
 
 
 def test_mul_mat_id(pkg, backend, orc):

@@ -59,6 +59,39 @@ def test_q8_0_quantiser_matches_golden(orc):
         assert diff.max() <= 1 and (diff > 0).mean() < 0.01
 
 
+def test_q4_0_quantiser_matches_golden(orc):
+    """orc_quantize_row_q4_0 (SET_ROWS into a q4_0 KV cache) against gguf-py's Q4_0
+    quantiser (tests/golden/quant_q4_0.npz): scales exact, nibbles equal but for rounding
+    ties of the +8.5 truncation"""
+    z = np.load(os.path.join(GOLD, "quant_q4_0.npz"), allow_pickle=False)
+    x, q = z["x"], z["q"].reshape(z["x"].shape[0], -1)
+    for r in range(x.shape[0]):
+        a = orc.quantize_q4_0(x[r]).reshape(-1, 18)
+        b = q[r].reshape(-1, 18)
+        assert np.array_equal(a[:, :2], b[:, :2])
+        na = np.concatenate([a[:, 2:] & 15, a[:, 2:] >> 4], 1).astype(int)
+        nb = np.concatenate([b[:, 2:] & 15, b[:, 2:] >> 4], 1).astype(int)
+        d = np.abs(na - nb)
+        assert d.max() <= 1 and (d > 0).mean() < 0.01, (d.max(), (d > 0).mean())
+    # and bit-exact against the reference's own C quantiser (ggml_quantize_chunk -> quantize_row_q4_0_ref,
+    # oracle/_ref/libggml-ref.so built from /root/reference), where that build is present
+    ref = os.path.join(os.path.dirname(GOLD), "..", "oracle", "_ref", "libggml-ref.so")
+    if os.path.exists(ref):
+        import ctypes
+        L = ctypes.CDLL(ref)
+        L.ggml_quantize_chunk.restype = ctypes.c_size_t
+        L.ggml_quantize_chunk.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_int64, ctypes.c_void_p]
+        rng = np.random.default_rng(3)
+        xr = (rng.standard_normal((8, 1024)) * np.array([1e-3, 1, 7, 300, 1, 1, 1, 1])[:, None]).astype(np.float32)
+        xr[4, :32] = 0.0
+        xr[5, :64:2] = -xr[5, 1:64:2]                     # equal-magnitude pairs: the first one wins
+        out = np.zeros((8, 1024 // 32 * 18), np.uint8)
+        L.ggml_quantize_chunk(2, xr.ctypes.data, out.ctypes.data, 0, 8, 1024, None)   # GGML_TYPE_Q4_0 = 2
+        for r in range(8):
+            assert np.array_equal(orc.quantize_q4_0(xr[r]), out[r]), r
+
+
 def test_fp16_conversion_matches_numpy(orc):
     rng = np.random.default_rng(0)
     vals = np.concatenate([rng.standard_normal(20000) * s for s in (1e-7, 1e-5, 1e-3, 1, 100, 1e4)]).astype(np.float32)
