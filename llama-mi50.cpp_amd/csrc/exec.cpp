@@ -671,6 +671,17 @@ static int try_split_group(OpCtx & c, ggml_cgraph * g, int i, std::unordered_map
     return ng;
 }
 
+// nodes that may read a pending q8_0 KV row (KvNewRow): every view of a quantised cache is
+// q8_0 / q4_0 typed, so any node with such an operand (conservatively: quantised weights too),
+// and any attention. Others (libllama's mask cast between the QKV block and the first
+// attention) leave the row pending.
+static bool kvnew_touches(const ggml_tensor * n) {
+    auto qt = [](const ggml_tensor * t) { return t && (t->type == GGML_TYPE_Q8_0 || t->type == GGML_TYPE_Q4_0); };
+    if (qt(n) || n->op == GGML_OP_FLASH_ATTN_EXT) return true;
+    for (int k = 0; k < GGML_MAX_SRC; ++k) if (qt(n->src[k])) return true;
+    return false;
+}
+
 static void run_nodes(Stream * s, ggml_cgraph * g) {
     OpCtx c{s, s->stream, &s->scratch};
     static thread_local UseMap uses;
@@ -691,9 +702,9 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
         if (is_view_op(n->op) || mx_is_empty(n)) continue;
         if (!done.empty() && done.count(n)) continue;
         s->scratch.reset();
-        // a q8_0 KV row the fused QKV launch left pending: stored now unless this node is the
-        // decode attention that takes it (KvNewRow, backend.h)
-        if (s->kvnew.on && !fa_takes_new_row(s, n)) kv_new_row_flush(c);
+        // a q8_0 KV row the fused QKV launch left pending: stored now by a node that may read
+        // the cache, unless it is the decode attention that takes the row (KvNewRow, backend.h)
+        if (s->kvnew.on && kvnew_touches(n) && !fa_takes_new_row(s, n)) kv_new_row_flush(c);
         // (pf_n read by the attention launch and gpf_node; the non-FA chain starts at
         // MUL_MAT(k, q) and is matched by fuse_attn_nofa below)
         if (n->op == GGML_OP_FLASH_ATTN_EXT) fa_prefetch_plan(s, g, i, n->src[0]->ne[1], false);

@@ -173,52 +173,33 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
     MX_TRACE(tr, 0);
     MX_TRACE_BLK(p.trace_blk, 0);
 
-    // q first (it is consumed first): the CPU vec-dot rounds q to the K type (f16)
+    // q and (round 6) this token's new K / V row are LOADED first, but converted only after
+    // the first chunk's K / V loads are issued (prep below): their conversion no longer holds
+    // the chunk loads back by a memory round trip. The CPU vec-dot rounds q to the K type:
+    // f16, or q8_0 blocks for a q8_0 K (amax over the block's 4 lanes by DPP, d = amax/127)
+    float4 qa[G], qb[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        const float * qp = (const float *) (p.q + (size_t) iq1 * p.q1 + (size_t) (hb + h) * p.q2 + (size_t) iq3 * p.q3) + 8 * c;
+        qa[h] = *(const float4 *) qp;
+        qb[h] = *(const float4 *) (qp + 4);
+    }
+    // the new row (q8_0 caches, FaDecArgs::nr_*): unconditional loads (a dummy source when
+    // absent: a load under a branch waits at the join)
+    const float * nks = KQ && p.nr_k ? p.nr_k + hk * D + 8 * c : (const float *) p.q;
+    const float * nvs = VQ && p.nr_v ? p.nr_v + hk * D + 8 * c : (const float *) p.q;
+    const float4 nk0 = *(const float4 *) nks, nk1 = *(const float4 *) (nks + 4);
+    const float4 nv0 = *(const float4 *) nvs, nv1 = *(const float4 *) (nvs + 4);
+    const int64_t nik = *(KQ && p.nr_k ? p.nr_ik : (const int64_t *) p.q), niv = *(VQ && p.nr_v ? p.nr_iv : (const int64_t *) p.q);
     h2v qh[G][4];
     int qq8[G][2];                                           // KQ: q as q8_0, 8 int8
     float qd[G];                                             // KQ: its block scale (f16-rounded)
-    if constexpr (KQ) {
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const float * qp = (const float *) (p.q + (size_t) iq1 * p.q1 + (size_t) (hb + h) * p.q2 + (size_t) iq3 * p.q3) + 8 * c;
-            const float4 a0 = *(const float4 *) qp, a1 = *(const float4 *) (qp + 4);
-            const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            float amax = 0.f;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(x[j]));
-            amax = dpp_max_group<4>(amax);
-            const float dq = amax / 127.0f, id = dq != 0.0f ? 1.0f / dq : 0.0f;
-            qd[h] = (float) (_Float16) dq;
-            int w0 = 0, w1 = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                w0 |= ((int) roundf(x[j] * id) & 0xFF) << (8 * j);
-                w1 |= ((int) roundf(x[4 + j] * id) & 0xFF) << (8 * j);
-            }
-            qq8[h][0] = w0; qq8[h][1] = w1;
-        }
-    } else {
-        float4 qa[G], qb[G];
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const float * qp = (const float *) (p.q + (size_t) iq1 * p.q1 + (size_t) (hb + h) * p.q2 + (size_t) iq3 * p.q3) + 8 * c;
-            qa[h] = *(const float4 *) qp;
-            qb[h] = *(const float4 *) (qp + 4);
-        }
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-            qh[h][0] = h2v{(_Float16) qa[h].x, (_Float16) qa[h].y}; qh[h][1] = h2v{(_Float16) qa[h].z, (_Float16) qa[h].w};
-            qh[h][2] = h2v{(_Float16) qb[h].x, (_Float16) qb[h].y}; qh[h][3] = h2v{(_Float16) qb[h].z, (_Float16) qb[h].w};
-        }
-    }
-    // this token's new K / V row (q8_0 caches, FaDecArgs::nr_*): quantize_row_q8_0 of the
-    // lane's 8 values (the 32-block over 4 lanes: d = amax/127 as f16, q = round(x/d)), the
-    // bytes k_kv_store_q8 would have written
     int64_t nrk = -1, nrv = -1;
     uint2 nkq = {0, 0}, nvq = {0, 0};
     uint16_t nkd = 0, nvd = 0;
-    auto nr_quant = [&](const float * src, uint2 & q8, uint16_t & dh) {
-        const float4 a0 = *(const float4 *) (src + hk * D + 8 * c), a1 = *(const float4 *) (src + hk * D + 8 * c + 4);
+    // quantize_row_q8_0 of a lane's 8 values (the 32-block over 4 lanes): the bytes
+    // k_kv_store_q8 would have written for the new row
+    auto nr_quant = [&](float4 a0, float4 a1, uint2 & q8, uint16_t & dh) {
         const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         float amax = 0.f;
 #pragma unroll
@@ -234,8 +215,35 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         }
         q8 = make_uint2(w0, w1);
     };
-    if constexpr (KQ) if (p.nr_k) { nrk = *p.nr_ik; nr_quant(p.nr_k, nkq, nkd); }
-    if constexpr (VQ) if (p.nr_v) { nrv = *p.nr_iv; nr_quant(p.nr_v, nvq, nvd); }
+    auto prep = [&]() {
+        if constexpr (KQ) {
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                const float x[8] = {qa[h].x, qa[h].y, qa[h].z, qa[h].w, qb[h].x, qb[h].y, qb[h].z, qb[h].w};
+                float amax = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(x[j]));
+                amax = dpp_max_group<4>(amax);
+                const float dq = amax / 127.0f, id = dq != 0.0f ? 1.0f / dq : 0.0f;
+                qd[h] = (float) (_Float16) dq;
+                int w0 = 0, w1 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    w0 |= ((int) roundf(x[j] * id) & 0xFF) << (8 * j);
+                    w1 |= ((int) roundf(x[4 + j] * id) & 0xFF) << (8 * j);
+                }
+                qq8[h][0] = w0; qq8[h][1] = w1;
+            }
+            if (p.nr_k) { nrk = nik; nr_quant(nk0, nk1, nkq, nkd); }
+        } else {
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                qh[h][0] = h2v{(_Float16) qa[h].x, (_Float16) qa[h].y}; qh[h][1] = h2v{(_Float16) qa[h].z, (_Float16) qa[h].w};
+                qh[h][2] = h2v{(_Float16) qb[h].x, (_Float16) qb[h].y}; qh[h][3] = h2v{(_Float16) qb[h].z, (_Float16) qb[h].w};
+            }
+        }
+        if constexpr (VQ) if (p.nr_v) { nrv = niv; nr_quant(nv0, nv1, nvq, nvd); }
+    };
     // running (max, sum, O) of this wave; O not yet reduced over the wave's key rows
     float M[G], L[G], o[G][8];
 #pragma unroll
@@ -352,6 +360,8 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         // exposed after its single round trip, and 4x the splits for the combine)
         Chunk bf[2];
         load(min(split * CPW, nch - 1), bf[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        prep();
 #pragma unroll
         for (int ci = 0; ci < CPW; ++ci) {
             // (compiler memory barrier: the next chunk's loads are issued here, not hoisted
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
             Chunk b;
             load(ch, b);
             __builtin_amdgcn_sched_barrier(0);
-            if (ci == 0) MX_TRACE(tr, 1);
+            if (ci == 0) { MX_TRACE(tr, 1); prep(); }
             process(ch, b, ci == 0);
         }
     }

@@ -31,8 +31,10 @@ for st in "$@"; do
   set -- $st
   kind=$1; shift
   case $kind in
-    tests)
-      timeout -k 10 ${TTMO:-1500} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $OUT/tests_$n.log 2>&1
+    tests)   # ('+' in an argument stands for a space: -k "a+or+b")
+      set -- "${@//+/ }"
+      [ $# -eq 0 ] && set -- tests
+      timeout -k 10 ${TTMO:-1500} python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $OUT/tests_$n.log 2>&1
       rc=$?; tail -n 25 $OUT/tests_$n.log; fin tests_$n $rc ;;
     lb)
       gguf; name=$1; shift
