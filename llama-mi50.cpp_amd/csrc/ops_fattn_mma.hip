@@ -29,7 +29,42 @@ struct FaMmaArgs {
     _Float16 * h;                         // k_fa_mma2: also f16 [n_q][H * D] (act cache) or null
     int n_q, n_kv, H, Hkv;
     float scale;
+    int qround;                           // q in K's vec-dot type before f16 (fa_q_round): 0 f16, 1 q8_0, 2 bf16
 };
+
+// Round 6: q as the CPU backend rounds it for the K cache's vec-dot type
+// (type_traits_cpu[k->type].vec_dot_type, ggml-cpu/ops.cpp:8045-8130): q8_0 blocks for q8_0 /
+// q4_0 caches (d = amax/127 as f16, q = round(x/d): the value d·q, then f16), bf16 for bf16.
+// x[s][0..7] = dims 16 s + 8 hl .. + 7 of the lane's query; a 32-dim block is steps 2b, 2b+1
+// of this lane and of its partner lane^32 (the other hl).
+template <int NKS>
+__device__ __forceinline__ void fa_q_round(float (&x)[NKS][8], int mode) {
+    if (mode == 1) {
+#pragma unroll
+        for (int b = 0; b < NKS / 2; ++b) {
+            float m = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m = fmaxf(m, fmaxf(fabsf(x[2 * b][j]), fabsf(x[2 * b + 1][j])));
+            m = fmaxf(m, __shfl_xor(m, 32, 64));
+            const float d = m / 127.0f, id = d != 0.0f ? 1.0f / d : 0.0f;
+            const float dh = (float) (_Float16) d;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                x[2 * b][j] = dh * roundf(x[2 * b][j] * id);
+                x[2 * b + 1][j] = dh * roundf(x[2 * b + 1][j] * id);
+            }
+        }
+    } else if (mode == 2) {
+#pragma unroll
+        for (int s = 0; s < NKS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                uint32_t u = __float_as_uint(x[s][j]);
+                u = (u + 0x7fff + ((u >> 16) & 1)) & 0xffff0000u;
+                x[s][j] = __uint_as_float(u);
+            }
+    }
+}
 
 static const bool g_fa_mma1 = getenv("GGML_MI355X_FA_MMA1") != nullptr;   // A/B: the first kernel
 
@@ -70,13 +105,18 @@ __global__ __launch_bounds__(128, 2) void k_fa_mma(FaMmaArgs p) {
     {
         const int qr = min(qw + r32, p.n_q - 1);
         const float * qp = (const float *) (p.q + (size_t) qr * p.q1 + (size_t) h * p.q2);
+        float x[NKS][8];
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
             const float4 f0 = *(const float4 *) (qp + 16 * s + 8 * hsel);
             const float4 f1 = *(const float4 *) (qp + 16 * s + 8 * hsel + 4);
-            qa[s][0] = (_Float16) f0.x; qa[s][1] = (_Float16) f0.y; qa[s][2] = (_Float16) f0.z; qa[s][3] = (_Float16) f0.w;
-            qa[s][4] = (_Float16) f1.x; qa[s][5] = (_Float16) f1.y; qa[s][6] = (_Float16) f1.z; qa[s][7] = (_Float16) f1.w;
+            x[s][0] = f0.x; x[s][1] = f0.y; x[s][2] = f0.z; x[s][3] = f0.w; x[s][4] = f1.x; x[s][5] = f1.y; x[s][6] = f1.z; x[s][7] = f1.w;
         }
+        if (p.qround) fa_q_round<NKS>(x, p.qround);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qa[s][j] = (_Float16) x[s][j];
     }
     ffloat16v acc_o[NDT];
 #pragma unroll
@@ -280,13 +320,18 @@ __global__ __launch_bounds__(256) void k_fa_mma2(FaMmaArgs p) {
     fhalf8 qa[NKS];
     {
         const float * qp = (const float *) (p.q + (size_t) qr * p.q1 + (size_t) h * p.q2);
+        float x[NKS][8];
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
             const float4 f0 = *(const float4 *) (qp + 16 * s + 8 * hl);
             const float4 f1 = *(const float4 *) (qp + 16 * s + 8 * hl + 4);
-            qa[s][0] = (_Float16) f0.x; qa[s][1] = (_Float16) f0.y; qa[s][2] = (_Float16) f0.z; qa[s][3] = (_Float16) f0.w;
-            qa[s][4] = (_Float16) f1.x; qa[s][5] = (_Float16) f1.y; qa[s][6] = (_Float16) f1.z; qa[s][7] = (_Float16) f1.w;
+            x[s][0] = f0.x; x[s][1] = f0.y; x[s][2] = f0.z; x[s][3] = f0.w; x[s][4] = f1.x; x[s][5] = f1.y; x[s][6] = f1.z; x[s][7] = f1.w;
         }
+        if (!VT && p.qround) fa_q_round<NKS>(x, p.qround);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qa[s][j] = (_Float16) x[s][j];
     }
     // the lane's 32 keys of a tile: 32 n + 8 m + 4 hl + (0..3), n < 2, m < 4 (S^T's C layout).
     // load_mask only issues (8-byte loads at clamped keys, unconditional: a load under a
@@ -593,6 +638,7 @@ void fa_mma_run(OpCtx & c, ggml_tensor * dst) {
     p.dst = (char *) dst->data; p.d1 = dst->nb[1]; p.d2 = dst->nb[2];
     p.n_q = (int) q->ne[1]; p.n_kv = (int) k->ne[1]; p.H = (int) q->ne[2]; p.Hkv = (int) k->ne[2];
     p.scale = mx_op_param<float>(dst, 0);
+    p.qround = k->type == GGML_TYPE_Q8_0 || k->type == GGML_TYPE_Q4_0 ? 1 : (k->type == GGML_TYPE_BF16 ? 2 : 0);
     if (k->ne[0] == 128 && k->ne[1] >= 4 && !g_fa_mma1 && (dst->nb[1] % 16) == 0 && ((uintptr_t) dst->data % 16) == 0) {
         const int Gt = p.H / p.Hkv, HG = Gt % 4 == 0 ? 4 : (Gt % 2 == 0 ? 2 : 1);
         // contiguous [D, H, n_q] output: the output projection reads it as [H*D, n_q] rows

@@ -54,6 +54,17 @@ for st in "$@"; do
       GGML_BACKEND_PATH=$LIB DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -s KILL 120 rocprofv3 --pmc $ctr -d $OUT/$name -o run \
         --output-format csv -- $REFB -m $G -t 8 -ngl 99 "$@" > $OUT/$name.log 2>&1
       rc=$?; fin $name $rc ;;
+    tbo)     # the reference's test-backend-ops against MI355X0 (perf / test mode)
+      name=$1; shift
+      set -- "${@//+/ }"
+      GGML_BACKEND_PATH=$LIB timeout -k 10 ${OTMO:-600} oracle/_ref/test-backend-ops "$@" > $OUT/$name.log 2>&1
+      rc=$?; grep -E "us/run|tests passed|FAIL" $OUT/$name.log | tail -n 60; fin $name $rc ;;
+    envlb)   # lb with env assignments first: envlb <name> VAR=val,VAR2=val -- flags
+      name=$1; ev=$2; shift 3; gguf
+      env ${ev//,/ } GGML_BACKEND_PATH=$LIB timeout -k 10 ${LTMO:-600} $LB -m $G -t 8 -ngl 99 -o jsonl -v "$@" > $OUT/$name.jsonl 2> $OUT/$name.err
+      rc=$?
+      echo "$name: $(grep -o '"avg_ts": [0-9.]*' $OUT/$name.jsonl | tr '\n' ' ') splits: $(grep -o 'graph splits = .*' $OUT/$name.err | sort -u | tr '\n' ' ')"
+      fin $name $rc ;;
     bench)
       timeout -k 10 ${BTMO:-1200} python -u bench.py "$@" > $OUT/bench_$n.json 2> $OUT/bench_$n.err
       rc=$?; tail -c 3000 $OUT/bench_$n.json; fin bench_$n $rc ;;

@@ -144,7 +144,12 @@ def test_dropin_mixed_kv_cache(ggufs, tmp_path, incremental, ctk, ctv):
     cpu, _ = run_ref(tmp_path, g, toks, 0, 1, incremental=incremental, ctk=ctk, ctv=ctv)
     gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, ctk=ctk, ctv=ctv, klog=klog)
     assert "MI355X" in log
-    assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+    # a q4_0 K cache: 16 levels per block, so a last-bit difference in a K value computed by
+    # the two backends (the projections' own rounding) moves a quantised K element by a whole
+    # step d = amax/8 (q8_0: amax/127) — the stored keys themselves differ, before any
+    # attention arithmetic (SET_ROWS q4_0 is bit-exact on equal input, test_ops_gpu.py)
+    tol = 5e-3 if ctk == 2 else TOL
+    assert nmse(gpu, cpu) < tol, nmse(gpu, cpu)
     kl = klog.read_text().splitlines()
     if incremental and {ctk, ctv} <= {1, 8}:
         kq, vq = int(ctk == 8), int(ctv == 8)
