@@ -192,6 +192,11 @@ struct QkvPpArgs {
     char * kc; size_t kc_nb1; const int64_t * kidx;      // K cache view rows (f16), row per token
     char * vc; size_t vc_nb1; const int64_t * vidx;
     int Mq, Mk, Mv;
+    // round 6: caches the epilogue cannot store itself (q8_0 / q4_0 rows, the transposed V of
+    // -fa 0) get their f32 rows here instead — roped K in the ROPE(k) output, V in the V
+    // projection — for the graph's own SET_ROWS node right after; skip_v: V is materialised
+    // already (the plain GEMM wrote it) and only that SET_ROWS runs
+    float * kf32; float * vf32; int skip_v;
 };
 // KS: 0 = the plain projections; > 0 = the q/k/v GEMM ran split-K (KS planes; -1: any
 // count) and left its partial planes, summed here in plane order as k_mmq4_reduce adds
@@ -223,10 +228,10 @@ __global__ __launch_bounds__(256) void k_qkv_pp_epi(QkvArgs p, QkvPpArgs e) {
     const int np = p.n_dims / 2;
     const float pf = (float) p.pos[t];
     for (int i = threadIdx.x; i < np; i += blockDim.x) tab[i] = qkv_rope_cs(p, pf, i);
-    const int pq = e.Mq / 2, pk = e.Mk / 2, pv = e.Mv / 2, total = pq + pk + pv;
+    const int pq = e.Mq / 2, pk = e.Mk / 2, pv = e.skip_v ? 0 : e.Mv / 2, total = pq + pk + pv;
     float2 * rq = (float2 *) (e.rq + (size_t) t * e.Mq);
-    uint32_t * kr = (uint32_t *) (e.kc + (size_t) e.kidx[t] * e.kc_nb1);
-    uint32_t * vr = (uint32_t *) (e.vc + (size_t) e.vidx[t] * e.vc_nb1);
+    uint32_t * kr = (uint32_t *) (e.kf32 ? nullptr : e.kc + (size_t) e.kidx[t] * e.kc_nb1);
+    uint32_t * vr = (uint32_t *) (e.vf32 || e.skip_v ? nullptr : e.vc + (size_t) e.vidx[t] * e.vc_nb1);
     constexpr int CH = 6;
     auto load_chunk = [&](int j0, float2 (&x)[CH]) {
 #pragma unroll
@@ -247,10 +252,13 @@ __global__ __launch_bounds__(256) void k_qkv_pp_epi(QkvArgs p, QkvPpArgs e) {
             } else if (j < pq + pk) {
                 const int jj = j - pq;
                 const float2 cs = tab[jj % np];
-                kr[jj] = (uint32_t) f2h(x[c].x * cs.x - x[c].y * cs.y) | ((uint32_t) f2h(x[c].x * cs.y + x[c].y * cs.x) << 16);
+                const float2 r = make_float2(x[c].x * cs.x - x[c].y * cs.y, x[c].x * cs.y + x[c].y * cs.x);
+                if (e.kf32) ((float2 *) (e.kf32 + (size_t) t * e.Mk))[jj] = r;
+                else kr[jj] = (uint32_t) f2h(r.x) | ((uint32_t) f2h(r.y) << 16);
             } else {
                 const int jj = j - pq - pk;
-                vr[jj] = (uint32_t) f2h(x[c].x) | ((uint32_t) f2h(x[c].y) << 16);
+                if (e.vf32) ((float2 *) (e.vf32 + (size_t) t * e.Mv))[jj] = x[c];
+                else vr[jj] = (uint32_t) f2h(x[c].x) | ((uint32_t) f2h(x[c].y) << 16);
             }
         }
     };
@@ -298,14 +306,33 @@ static int qkv_prefill(OpCtx & c, ggml_cgraph * g, int i, int last, const ggml_t
         if (m->type != GGML_TYPE_F32 || !mx_is_contiguous(m) || m->ne[1] != N || m->ne[2] != 1 || m->ne[3] != 1 || m->ne[0] % 2) return 0;
     if (mx_nelements(rq) != Mq * N || mx_nelements(rk) != Mk * N || Mq % n_dims || Mk % n_dims) return 0;
     if ((mq->flags | mk->flags | mv->flags | rk->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
-    if (uses(mq) != 1 || uses(mk) != 1 || uses(mv) != 1 || uses(rk) != 1) return 0;
-    // SET_ROWS: f16 cache views, one row of the projection per token, I64 indices
+    if (uses(mq) != 1 || uses(mk) != 1 || uses(rk) != 1) return 0;
+    // (mv: one use, or two for -fa 0's V — the reshape the transposed SET_ROWS reads and
+    // nothing else: uses counts the graph's direct consumers)
+    if (uses(mv) != 1) return 0;
+    // SET_ROWS: f16 cache views stored by the epilogue (one row of the projection per token,
+    // I64 indices); round 6: other caches keep their SET_ROWS node, fed f32 rows by the
+    // epilogue (k_mode / v_mode 1: q8_0 / q4_0 rows; v_mode 2: -fa 0's transposed V, one index
+    // per element) — the q/k/v GEMM stays grouped and the two ROPEs fused either way
     const ggml_tensor * kix = sk->src[1], * vix = sv->src[1];
-    if (sk->type != GGML_TYPE_F16 || sv->type != GGML_TYPE_F16 || sk->nb[0] != 2 || sv->nb[0] != 2) return 0;
+    auto qcache = [](const ggml_tensor * t) { return t->type == GGML_TYPE_Q8_0 || t->type == GGML_TYPE_Q4_0; };
+    int k_mode = 0, v_mode = 0;
+    if (sk->type == GGML_TYPE_F16 && sk->nb[0] == 2) k_mode = 0;
+    else if (qcache(sk) && sk->ne[0] == Mk) k_mode = 1;
+    else return 0;
     if (sk->ne[0] != Mk || sk->src[0]->ne[0] != Mk || sk->src[0]->ne[1] != N || kix->ne[0] != N || kix->type != GGML_TYPE_I64) return 0;
-    if (sv->ne[0] != Mv || sv->src[0]->ne[0] != Mv || sv->src[0]->ne[1] != N || vix->ne[0] != N || vix->type != GGML_TYPE_I64) return 0;
-    if (sk->nb[1] % 4 || sv->nb[1] % 4 || (uintptr_t) sk->data % 4 || (uintptr_t) sv->data % 4) return 0;
-    if (!mx_is_contiguous(kix) || !mx_is_contiguous(vix)) return 0;
+    if (sv->type == GGML_TYPE_F16 && sv->nb[0] == 2 && sv->ne[0] == Mv && sv->src[0]->ne[0] == Mv && sv->src[0]->ne[1] == N && vix->ne[0] == N) v_mode = 0;
+    else if (qcache(sv) && sv->ne[0] == Mv && sv->src[0]->ne[0] == Mv && sv->src[0]->ne[1] == N && vix->ne[0] == N) v_mode = 1;
+    else if (sv->type == GGML_TYPE_F16 && sv->ne[0] == 1 && sv->src[0]->ne[0] == 1 && sv->src[0]->ne[1] == Mv * N &&
+             vix->ne[0] == Mv * N) v_mode = 2;
+    else return 0;
+    if (vix->type != GGML_TYPE_I64 || !mx_is_contiguous(kix) || !mx_is_contiguous(vix)) return 0;
+    if (k_mode == 0 && (sk->nb[1] % 4 || (uintptr_t) sk->data % 4)) return 0;
+    if (v_mode == 0 && (sv->nb[1] % 4 || (uintptr_t) sv->data % 4)) return 0;
+    // f32 rows for the SET_ROWS nodes: where those nodes read (the ROPE(k) output, the V
+    // projection), contiguous [M, N]; kept in place only (no scratch copies below)
+    if (k_mode && (base_of(sk->src[0]) != rk || !mx_is_contiguous(rk) || (rk->flags & GGML_TENSOR_FLAG_OUTPUT))) return 0;
+    if (v_mode && (base_of(sv->src[0]) != mv || (mv->flags & GGML_TENSOR_FLAG_OUTPUT))) return 0;
     for (int j = i; j <= last; ++j) {
         deferred_guard_node_ext(c, g->nodes[j]);
         act_cache_invalidate(c.s, g->nodes[j]);
@@ -320,6 +347,10 @@ static int qkv_prefill(OpCtx & c, ggml_cgraph * g, int i, int last, const ggml_t
                           !t_overlaps_ext(rq, mk) && !t_overlaps_ext(rq, mv) && (rq->data == mq->data || !t_overlaps_ext(rq, mq));
     ggml_tensor tcp[3];
     ggml_tensor * mms[3] = {mq, mk, mv};
+    if (!disjoint && (k_mode || v_mode)) return 0;   // (the SET_ROWS nodes read the tensors in place)
+    // (ROPE may run in place: rk exactly on mk is fine, each thread reads its pair before writing it)
+    if (k_mode && (t_overlaps_ext(rk, mq) || (t_overlaps_ext(rk, mk) && rk->data != mk->data) || t_overlaps_ext(rk, mv) ||
+                   t_overlaps_ext(rk, rq) || t_overlaps_ext(rk, x))) return 0;
     if (!disjoint) {
         const size_t need = (size_t) (Mq + Mk + Mv) * N * sizeof(float) + 3 * 256;
         if (c.scratch->avail() < need) return 0;
@@ -352,14 +383,23 @@ static int qkv_prefill(OpCtx & c, ggml_cgraph * g, int i, int last, const ggml_t
     e.kc = (char *) sk->data; e.kc_nb1 = sk->nb[1]; e.kidx = (const int64_t *) kix->data;
     e.vc = (char *) sv->data; e.vc_nb1 = sv->nb[1]; e.vidx = (const int64_t *) vix->data;
     e.Mq = (int) Mq; e.Mk = (int) Mk; e.Mv = (int) Mv;
-    MX_KLOG("qkv_pp N=%lld Mq=%lld Mk=%lld Mv=%lld n_dims=%d ks=%d disjoint=%d", (long long) N, (long long) Mq, (long long) Mk,
-            (long long) Mv, n_dims, sp.ks, (int) disjoint);
+    if (k_mode) e.kf32 = (float *) rk->data;
+    if (v_mode) {
+        if (sp.ks > 1) e.vf32 = (float *) mv->data;    // the split-K planes summed into the V projection
+        else e.skip_v = 1;                             // the plain GEMM wrote it
+    }
+    MX_KLOG("qkv_pp N=%lld Mq=%lld Mk=%lld Mv=%lld n_dims=%d ks=%d disjoint=%d k_mode=%d v_mode=%d", (long long) N, (long long) Mq,
+            (long long) Mk, (long long) Mv, n_dims, sp.ks, (int) disjoint, k_mode, v_mode);
     if (sp.ks > 1) {
         e.part = sp.part; e.part_ld = sp.part_ld; e.ks = sp.ks; e.N = (int) N;
         for (int k = 0; k < 3; ++k) e.row0[k] = sp.row0[k];
         if (sp.ks == 2) k_qkv_pp_epi<2><<<(unsigned) N, 256, 0, c.st>>>(p, e);
         else k_qkv_pp_epi<-1><<<(unsigned) N, 256, 0, c.st>>>(p, e);
     } else k_qkv_pp_epi<0><<<(unsigned) N, 256, 0, c.st>>>(p, e);
+    // the SET_ROWS nodes of the caches the epilogue did not store (q8_0 / q4_0 rows, the
+    // transposed V) — their sources now hold the f32 rows
+    if (k_mode) op_set_rows(c, sk);
+    if (v_mode) op_set_rows(c, sv);
     return last - i + 1;
 }
 

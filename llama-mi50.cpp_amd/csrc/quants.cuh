@@ -116,7 +116,9 @@ __device__ __forceinline__ void quantize_block_q4_0(const float * x, char * out)
         const float v = x[j];
         if (amax < fabsf(v)) { amax = fabsf(v); mx = v; }
     }
-    const float d = mx / -8;
+    // d = mx / -8 exactly (a power of two); an all-zero block gives -0.0 (mx = +0), which
+    // the compiler's zero handling lost here when written as a division: the sign is explicit
+    const float d = __builtin_copysignf(fabsf(mx) * 0.125f, mx > 0.0f || mx == 0.0f ? -1.0f : 1.0f);
     const float id = d != 0.0f ? 1.0f / d : 0.0f;
     const uint16_t dh = f2h(d);
     memcpy(out, &dh, 2);
