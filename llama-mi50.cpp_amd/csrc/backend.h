@@ -180,8 +180,8 @@ struct OpCtx {
 // returns true when the backend can execute `op` (supports_op contract,
 // ggml-backend-impl.h:171)
 bool supports_op(const ggml_tensor * op);
-// scratch bytes a node needs (upper bound)
-size_t scratch_bytes(const ggml_tensor * node);
+// scratch bytes a node needs (upper bound; add_norm: the MUL_MAT feeds an ADD -> RMS_NORM pair)
+size_t scratch_bytes(const ggml_tensor * node, bool add_norm = false);
 
 // kernels: each computes `dst` from dst->src[] on the stream
 void op_get_rows(OpCtx & c, ggml_tensor * dst);
@@ -212,7 +212,7 @@ void split_stream_free(const Stream * main);   // be_free: drop the freed stream
 void op_mul_mat_id(OpCtx & c, ggml_tensor * dst);
 void op_flash_attn_ext(OpCtx & c, ggml_tensor * dst);
 
-size_t mul_mat_scratch(const ggml_tensor * dst);
+size_t mul_mat_scratch(const ggml_tensor * dst, bool add_norm = false);   // add_norm: an ADD -> RMS_NORM follows
 size_t mul_mat_id_scratch(const ggml_tensor * dst);
 size_t flash_attn_scratch(const ggml_tensor * dst);
 bool mul_mat_supported(const ggml_tensor * dst);
@@ -255,8 +255,6 @@ void kv_new_row_flush(OpCtx & c);
 bool fa_takes_new_row(const Stream * s, const ggml_tensor * fa);
 // -fa 0 decode attention chain (ops_fattn_dec.hip)
 int fuse_attn_nofa(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
-// FLASH_ATTN_EXT -> RESHAPE -> MUL_MAT(wo) -> ADD(residual) of one decode token (ops_attn_o.hip)
-int fuse_attn_oproj(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
 bool t_overlaps_ext(const ggml_tensor * a, const ggml_tensor * b);
 // no output of a fused launch overlaps its inputs or another output, except the named
 // element-wise in-place (output, input) pairs at the same start (exec.cpp)

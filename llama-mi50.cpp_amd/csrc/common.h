@@ -191,7 +191,7 @@ __device__ __forceinline__ float lane_bcast(float v, int lane) {
 // pointer (null unless tracing) for its first workgroup and records s_memtime per wave at
 // phase boundaries: ptr[wave * 8 + phase].
 // A/B-experiment code (timing variants whose results are wrong by construction, debug
-// masks, opt-in alternatives measured slower: ops_attn_o.hip, the balanced QKV layout) is
+// masks, opt-in alternatives measured slower: the balanced QKV layout) is
 // compiled only into variant builds (scripts/build_variants.sh: EXTRA=-DMX_AB_VARIANTS=1);
 // in the product library those knobs are dead code.
 #ifndef MX_AB_VARIANTS

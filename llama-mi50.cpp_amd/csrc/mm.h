@@ -22,7 +22,7 @@ _Float16 * mmq_act_f16(OpCtx & c, const ggml_tensor * x, int64_t kp);
 
 // prefill GEMM v4 (ops_mmq4.hip): false when not eligible (nothing launched)
 bool mmq4_on();
-size_t mmq4_scratch(const ggml_tensor * dst);   // split-K partial sums
+size_t mmq4_scratch(const ggml_tensor * dst, bool add_norm = false);   // split-K partial sums
 size_t mmq4_moe_scratch(const ggml_tensor * dst);
 bool mmq4_moe_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up, ggml_tensor * glu);   // + SwiGLU, prefill
 bool mmq4_moe(OpCtx & c, ggml_tensor * dst);     // MUL_MAT_ID prefill, expert-grouped

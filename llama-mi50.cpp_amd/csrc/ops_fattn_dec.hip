@@ -1025,7 +1025,13 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec3(FaDecArgs p, int kps) {
     // relaxed count: the partials went out as agent-scope (write-through) atomic stores and
     // have completed (waitcnt above); the merge reads them back with agent-scope loads. An
     // acq_rel count adds an L2 writeback (buffer_wbl2) to every workgroup and an L2
-    // invalidate to the merging one, ~2 us of this launch's tail
+    // invalidate to the merging one, ~2 us of this launch's tail.
+    // Hardware assumption (gfx950, coarse-grained device memory): an agent-scope atomic
+    // store is written through the XCD's L2 to the device coherence point and s_waitcnt
+    // vmcnt(0) returns only once it is there; an agent-scope atomic load reads that point.
+    // Every byte the merge reads is such a store, so no fence is needed for them — only for
+    // ordinary stores, which this protocol never relies on. Pinned by
+    // tests/test_ops_gpu.py::test_flash_attn_stream_merge_visibility (64K keys, 24 runs).
     if (tid == 0) s_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned) (ns - 1);
     __syncthreads();
     if (!s_last) return;

@@ -140,16 +140,24 @@ __global__ __launch_bounds__(64 * W) void k_gemv2(G2Args p) {
     }
 }
 
+// The geometries compiled with the attention-partials source (XS_FAP*: the output
+// projection after fa_dec2_partials): residual epilogue, 4 waves, no EXT items, UPL 4 or
+// LPR 64 x UPL 2. ONE predicate for what launch_mode instantiates and what gemv2_fap_ok
+// admits (round 5's abort came from two hand-kept lists disagreeing): a geometry outside it
+// is declined before the attention runs, never launched.
+__host__ __device__ constexpr bool fap_geom(int LPR, int UPL, int EPI, int W, bool EXT) {
+    return EPI == 2 && !EXT && W == 4 && (UPL == 4 || (LPR == 64 && UPL == 2));
+}
+
 template <int QT, int LPR, int UPL, int EPI, int W, bool EXT>
 static void launch_mode(hipStream_t st, const G2Args & p, int mode, dim3 grid, size_t lds) {
-    if (xs_fap(mode)) {   // the output projection after fa_dec2_partials: residual epilogue only
-        // (instantiated for the decode output projection's geometries only: gemv2_fap_ok)
-        if constexpr (EPI == 2 && !EXT && W == 4 && (UPL == 4 || (LPR == 64 && UPL == 2))) {
+    if (xs_fap(mode)) {
+        if constexpr (fap_geom(LPR, UPL, EPI, W, EXT)) {
             if (mode == XS_FAP8) k_gemv2<QT, LPR, UPL, EPI, W, XS_FAP8, EXT><<<grid, 64 * W, lds, st>>>(p);
             else k_gemv2<QT, LPR, UPL, EPI, W, XS_FAP4, EXT><<<grid, 64 * W, lds, st>>>(p);
             return;
         }
-        MX_ABORT("gemv2: attention-partials source needs the residual epilogue, 4 waves");
+        MX_ABORT("gemv2: gemv2_fap_ok admitted geometry lpr=%d upl=%d epi=%d w=%d ext=%d", LPR, UPL, EPI, W, (int) EXT);   // (unreachable)
     }
     switch (mode) {
         case XS_Q8: k_gemv2<QT, LPR, UPL, EPI, W, XS_Q8, EXT><<<grid, 64 * W, lds, st>>>(p); break;
@@ -178,6 +186,19 @@ static void launch_cfg(hipStream_t st, const G2Args & p0, bool regs = false) {
     else launch_mode<QT, LPR, UPL, EPI, W, false>(st, p, mode, grid, lds);
 }
 
+// the weight types with the full (LPR, UPL) tuning grid in launch_type; the others run
+// (LPR in {16, 32, 64}, UPL 2 for the SwiGLU else 4)
+__host__ __device__ constexpr bool gemv2_full_grid(int qt) { return qt == GGML_TYPE_Q4_K || qt == GGML_TYPE_Q6_K; }
+
+// the (LPR, UPL) launch_type actually instantiates for a request (epi != 1 or no q8
+// emission; waves 4 unless g_tune[16] widens a plain EPI 0 launch)
+static void resolve_geom(int type, int epi, int lpr, int upl, int & L, int & U) {
+    const bool listed = (lpr == 16 || lpr == 32 || lpr == 64) && (upl == 2 || upl == 4);
+    if (gemv2_full_grid(type) && listed) { L = lpr; U = upl; return; }
+    U = epi == 1 ? 2 : 4;
+    L = lpr == 16 ? 16 : (lpr == 32 ? 32 : 64);
+}
+
 template <int QT, int EPI>
 static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
     if constexpr (EPI == 1) {
@@ -191,7 +212,7 @@ static void launch_type(hipStream_t st, const G2Args & p, int lpr, int upl) {
             return launch_cfg<QT, 16, 2, 1, 8>(st, p);
         }
     }
-    constexpr bool FULL = QT == GGML_TYPE_Q4_K || QT == GGML_TYPE_Q6_K;   // full tuning grid
+    constexpr bool FULL = gemv2_full_grid(QT);   // full tuning grid
     if constexpr (FULL && EPI == 0) {
         // g_tune[16]: waves per workgroup of the plain 16 x 4 geometry (lm_head): 8 or 16
         // halve / quarter the workgroups that each stage (and normalise) the activation —
@@ -233,10 +254,10 @@ static void pick_cfg(int type, int units, int nrows, bool glu, int & lpr, int & 
 // a geometry instantiated for it (launch_mode), one 16-value half per thread
 bool gemv2_fap_ok(int type, int64_t K, int64_t M) {
     if (!gemv2_type_ok(type) || K > 16 * 256 || K % 32) return false;
-    int lpr, upl;
+    int lpr, upl, L, U;
     pick_cfg(type, units_of(type, K), (int) M, false, lpr, upl);
-    if (type != GGML_TYPE_Q4_K && type != GGML_TYPE_Q6_K) upl = 4;   // launch_type: the reduced tuning grid
-    return upl == 4 || (lpr == 64 && upl == 2);
+    resolve_geom(type, 2, lpr, upl, L, U);
+    return fap_geom(L, U, 2, 4, false);   // (gemv2_launch never arms the EXT prefetch with a fap source)
 }
 
 bool gemv2_type_ok(int t) {
@@ -276,7 +297,8 @@ void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, cons
         p.q8o = (int8_t *) q8out->q; p.q8od = (float *) q8out->d; p.q8os = (float *) q8out->s;
     }
     MX_ASSERT(!(glu && res));
-    if (c.s->gpf_armed && !glu) {               // the executor's second prefetch stage
+    if (c.s->gpf_armed && !glu && !xs.fap) {    // the executor's second prefetch stage (not with
+                                                // partials: fap_geom has no EXT instantiations)
         c.s->gpf_armed = false;
         p.pf_n = c.s->pf_n;
         for (int r = 0; r < p.pf_n; ++r) { p.pf[r] = c.s->pf_ptr[r]; p.pf_eighth[r] = c.s->pf_len[r] / 8; }

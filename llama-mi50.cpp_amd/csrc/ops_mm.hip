@@ -1215,11 +1215,11 @@ size_t mmq_act_bytes(const ggml_tensor * dst) {
     return (size_t) x->ne[1] * x->ne[2] * x->ne[3] * mmq_kp(dst) * 2;
 }
 
-size_t mul_mat_scratch(const ggml_tensor * dst) {
+size_t mul_mat_scratch(const ggml_tensor * dst, bool add_norm) {
     const ggml_tensor * x = dst->src[1];
     size_t s = 0;
     if (x->ne[1] <= 8 && quant_fast_path_ok(dst)) s = quantize_scratch(x);
-    else if (mmq_ok(dst)) s = mmq_scratch(dst) + mmq4_scratch(dst);
+    else if (mmq_ok(dst)) s = mmq_scratch(dst) + mmq4_scratch(dst, add_norm);
     return s;
 }
 

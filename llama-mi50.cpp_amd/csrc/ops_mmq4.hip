@@ -1076,14 +1076,15 @@ static int m4_ksplit(int64_t wgs, int nk, int64_t n, int64_t m) {
     return best;
 }
 
-size_t mmq4_scratch(const ggml_tensor * dst) {
+size_t mmq4_scratch(const ggml_tensor * dst, bool add_norm) {
     const ggml_tensor * w = dst->src[0], * x = dst->src[1];
     if (!m4_kq(w->type) || x->ne[1] <= 8) return 0;
     const int64_t rows = mx_ceil_div(w->ne[1] + w->ne[1] / 2, 256) * 256;   // room for a q/k/v group
     const int ks = m4_ksplit(mx_ceil_div(x->ne[1], 128) * mx_ceil_div(rows, 256), (int) (w->ne[0] / M4_KC), x->ne[1], rows);
-    // + the product itself: mm_add_rms_norm keeps an unsplit product in scratch when the ADD
-    // runs in place over its residual, and must not squeeze the split-K planes out
-    return (ks > 1 ? (size_t) ks * x->ne[1] * rows * 4 + 256 : 0) + (size_t) w->ne[1] * x->ne[1] * 4 + 256;
+    // + the product itself where an ADD -> RMS_NORM follows (add_norm, exec.cpp's sizing
+    // pass): mm_add_rms_norm keeps an unsplit product in scratch when the ADD runs in place
+    // over its residual, and must not squeeze the split-K planes out (only there)
+    return (ks > 1 ? (size_t) ks * x->ne[1] * rows * 4 + 256 : 0) + (add_norm ? (size_t) w->ne[1] * x->ne[1] * 4 + 256 : 0);
 }
 
 template <int EPI>

@@ -117,6 +117,9 @@ def test_dropin_q8_0_kv_cache(ggufs, tmp_path, incremental):
     gpu, log = run_ref(tmp_path, g, toks, 99, 1, incremental=incremental, ctk=8, klog=klog)
     assert "MI355X" in log
     assert nmse(gpu, cpu) < TOL, nmse(gpu, cpu)
+    if not incremental:   # (round 6) prefill: q/k/v + RoPE fused, the q8_0 rows by their SET_ROWS nodes
+        kl = klog.read_text().splitlines()
+        assert any(ln.startswith("qkv_pp ") and "k_mode=1 v_mode=1" in ln for ln in kl), kl[-40:]
     if incremental:
         kl = klog.read_text()
         assert "kq8=1" in kl and any(ln.startswith("qkv ") and "kq8=1" in ln for ln in kl.splitlines()), kl[-2000:]

@@ -246,6 +246,10 @@ def test_llama3_8b_width_pp512(l8b, tmp_path, fa):
     # allocator (the norm reuses the dead GEMM input's memory): layer 0's two sites (the last
     # layer's attention output meets libllama's inp_out_ids GET_ROWS first)
     assert k["add_rms_norm"] >= 2, k
+    # q/k/v GEMM + both ROPEs + the K/V stores fused (ops_qkv.hip qkv_prefill); -fa 0's
+    # transposed V (round 6): the epilogue fills the V projection, its SET_ROWS node stores it
+    qp = [ln for ln in klog if ln.startswith("qkv_pp ")]
+    assert len(qp) == 2 and all(f"v_mode={0 if fa else 2}" in ln for ln in qp), qp
     if fa:
         assert k["fa_mma2"] == 2, k
     else:   # the KQ -> softmax -> KQV chain as one transposed-V flash launch per layer
