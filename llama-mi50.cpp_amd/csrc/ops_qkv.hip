@@ -347,10 +347,16 @@ static int qkv_prefill(OpCtx & c, ggml_cgraph * g, int i, int last, const ggml_t
                           !t_overlaps_ext(rq, mk) && !t_overlaps_ext(rq, mv) && (rq->data == mq->data || !t_overlaps_ext(rq, mq));
     ggml_tensor tcp[3];
     ggml_tensor * mms[3] = {mq, mk, mv};
-    if (!disjoint && (k_mode || v_mode)) return 0;   // (the SET_ROWS nodes read the tensors in place)
-    // (ROPE may run in place: rk exactly on mk is fine, each thread reads its pair before writing it)
-    if (k_mode && (t_overlaps_ext(rk, mq) || (t_overlaps_ext(rk, mk) && rk->data != mk->data) || t_overlaps_ext(rk, mv) ||
-                   t_overlaps_ext(rk, rq) || t_overlaps_ext(rk, x))) return 0;
+    // The epilogue's f32 rows for the SET_ROWS nodes go where those nodes read them (rk, mv);
+    // with them, the outputs the epilogue writes (rq, rk, mv) must be distinct memory. libllama's
+    // allocator puts a later projection over one that died in between (mv over mq: not
+    // disjoint), so then the GEMM writes scratch copies below and only rq / rk / mv are written
+    // in place. (ROPE may run in place: rk exactly on mk is fine, each thread reads its pair
+    // before writing it.)
+    if (k_mode && (t_overlaps_ext(rk, rq) || (v_mode && t_overlaps_ext(rk, mv)) ||
+                   (disjoint && ((t_overlaps_ext(rk, mk) && rk->data != mk->data) || t_overlaps_ext(rk, mq) || t_overlaps_ext(rk, mv) ||
+                                 t_overlaps_ext(rk, x))))) return 0;
+    if (v_mode && t_overlaps_ext(mv, rq)) return 0;
     if (!disjoint) {
         const size_t need = (size_t) (Mq + Mk + Mv) * N * sizeof(float) + 3 * 256;
         if (c.scratch->avail() < need) return 0;
@@ -385,8 +391,10 @@ static int qkv_prefill(OpCtx & c, ggml_cgraph * g, int i, int last, const ggml_t
     e.Mq = (int) Mq; e.Mk = (int) Mk; e.Mv = (int) Mv;
     if (k_mode) e.kf32 = (float *) rk->data;
     if (v_mode) {
-        if (sp.ks > 1) e.vf32 = (float *) mv->data;    // the split-K planes summed into the V projection
-        else e.skip_v = 1;                             // the plain GEMM wrote it
+        // the split-K planes summed (or the scratch copy moved) into the V projection; else
+        // the plain GEMM wrote it in place
+        if (sp.ks > 1 || mms[2] != mv) e.vf32 = (float *) mv->data;
+        else e.skip_v = 1;
     }
     MX_KLOG("qkv_pp N=%lld Mq=%lld Mk=%lld Mv=%lld n_dims=%d ks=%d disjoint=%d k_mode=%d v_mode=%d", (long long) N, (long long) Mq,
             (long long) Mk, (long long) Mv, n_dims, sp.ks, (int) disjoint, k_mode, v_mode);
