@@ -259,6 +259,24 @@ __global__ __launch_bounds__(256) void k_mmvq_lds(MmvArgs p, ActQ a) {
     const int64_t kp = a.kp, nb = kp / 32;
     const int ncols = (int) min<int64_t>(p.ncols, NC);
     const int64_t col0 = ch * p.ncols;
+    // the lane's first batch of weight loads goes out before the staging loads below (the
+    // staging's waits then cover the weights too: one latency for both)
+    const int64_t rr = min<int64_t>(row, p.nrows - 1);        // (clamped: every lane reaches the barrier)
+    const size_t off = (size_t) rr * p.w_row + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
+    const char * r = p.w + off;
+    const char * r2 = GLU ? p.w2 + off : nullptr;
+    URegs<QT> rg[UNR];
+    URegs<QT> rg2[GLU ? UNR : 1];
+    auto load_batch = [&](int u0) {
+#pragma unroll
+        for (int j = 0; j < UNR; ++j) {
+            const int u = min(u0 + j * LPR, (int) p.units - 1);
+            unit_load<QT>(r, u, rg[j]);
+            if constexpr (GLU) unit_load<QT>(r2, u, rg2[j]);
+        }
+    };
+    int u0 = sub;
+    load_batch(u0);
     // the channel's columns -> LDS: int8 [NC][kp], then d [NC][nb], s [NC][nb]
     int8_t * lq = (int8_t *) sm;
     float * ld = (float *) (sm + NC * kp);
@@ -276,19 +294,7 @@ __global__ __launch_bounds__(256) void k_mmvq_lds(MmvArgs p, ActQ a) {
     float acc[NC], acc2[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) { acc[c] = 0.f; acc2[c] = 0.f; }
-    const int64_t rr = min<int64_t>(row, p.nrows - 1);        // (clamped: every lane reaches the loop)
-    const size_t off = (size_t) rr * p.w_row + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
-    const char * r = p.w + off;
-    const char * r2 = GLU ? p.w2 + off : nullptr;
-    for (int u0 = sub; u0 < p.units; u0 += LPR * UNR) {
-        URegs<QT> rg[UNR];
-        URegs<QT> rg2[GLU ? UNR : 1];
-#pragma unroll
-        for (int j = 0; j < UNR; ++j) {
-            const int u = min(u0 + j * LPR, (int) p.units - 1);
-            unit_load<QT>(r, u, rg[j]);
-            if constexpr (GLU) unit_load<QT>(r2, u, rg2[j]);
-        }
+    while (true) {
 #pragma unroll
         for (int j = 0; j < UNR; ++j) {
             const int u = u0 + j * LPR;
@@ -297,6 +303,9 @@ __global__ __launch_bounds__(256) void k_mmvq_lds(MmvArgs p, ActQ a) {
                 if constexpr (GLU) unit_compute<QT, NC>(rg2[j], u, al, acc2);
             }
         }
+        u0 += LPR * UNR;
+        if (u0 >= p.units) break;
+        load_batch(u0);
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -335,11 +344,11 @@ static void launch_lds_u(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t n
 }
 
 // geometry (g_tune[41] = LPR, g_tune[43] = UNR for sweeps): LPR 16 (16 rows per workgroup:
-// activation staging amortised over more rows) unless the row is short; all of a lane's
-// units in flight, fewer for the wide column groups (registers: NC accumulators)
+// the activation staging amortised over more rows), up to 8 units of a lane in flight,
+// 4 for the wide column groups (registers: NC accumulators)
 template <int QT, int NC, int EPI>
 static void launch_lds(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
-    int lpr = p.units >= 256 ? 32 : 16;
+    int lpr = 16;
     if (g_tune[41] == 16 || g_tune[41] == 32 || g_tune[41] == 64) lpr = g_tune[41];
     const int64_t per_lane = mx_ceil_div(p.units, lpr);
     int unr = per_lane >= 8 ? 8 : (per_lane >= 4 ? 4 : 2);
