@@ -236,130 +236,6 @@ __global__ __launch_bounds__(256) void k_mmvq(MmvArgs p, ActQ a) {
     }
 }
 
-// Round 6: 2-8 activation columns (llama-server parallel slots, speculative decoding; the
-// reference templates mul_mat_vec_q per ncols, mmvq.cu:397-502, and times
-// 4096 x bs x 14336 in test-backend-ops perf mode, tests/test-backend-ops.cpp:8429-8435).
-// k_mmvq read each column's int8 activations from L2 inside the dot loop, after its weights
-// had landed: two dependent round trips per batch of 2 units, and NC x 40 B of L2 traffic
-// per unit and row (a 4096 x 14336 Q4_K at 2 columns: 14.1 us = 0.29 of HBM,
-// profiles/r06/test_backend_ops_perf_mul_mat_before.txt). Here the workgroup first copies
-// the quantised columns into LDS (NC x kp x 1.25 B, up to 160 KB), then every lane issues
-// ALL its units' weight loads at once (UNR up to 8, as the one-column kernel) and dots them
-// against LDS: one HBM round trip, the rows of a wave sharing each activation read.
-template <int QT, int NC, int LPR, int UNR, int EPI>
-__global__ __launch_bounds__(256) void k_mmvq_lds(MmvArgs p, ActQ a) {
-    constexpr bool GLU = EPI == 1;
-    extern __shared__ __align__(16) char sm[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int RPW = 64 / LPR;
-    const int64_t row = ((int64_t) blockIdx.x * 4 + wave) * RPW + lane / LPR;
-    const int sub = lane % LPR;
-    const int64_t ch = blockIdx.y;
-    const int64_t i12 = ch % p.ne12, i13 = ch / p.ne12;
-    const int64_t kp = a.kp, nb = kp / 32;
-    const int ncols = (int) min<int64_t>(p.ncols, NC);
-    const int64_t col0 = ch * p.ncols;
-    // the lane's first batch of weight loads goes out before the staging loads below (the
-    // staging's waits then cover the weights too: one latency for both)
-    const int64_t rr = min<int64_t>(row, p.nrows - 1);        // (clamped: every lane reaches the barrier)
-    const size_t off = (size_t) rr * p.w_row + (i12 / p.r2) * p.w_c2 + (i13 / p.r3) * p.w_c3;
-    const char * r = p.w + off;
-    const char * r2 = GLU ? p.w2 + off : nullptr;
-    URegs<QT> rg[UNR];
-    URegs<QT> rg2[GLU ? UNR : 1];
-    auto load_batch = [&](int u0) {
-#pragma unroll
-        for (int j = 0; j < UNR; ++j) {
-            const int u = min(u0 + j * LPR, (int) p.units - 1);
-            unit_load<QT>(r, u, rg[j]);
-            if constexpr (GLU) unit_load<QT>(r2, u, rg2[j]);
-        }
-    };
-    int u0 = sub;
-    load_batch(u0);
-    // the channel's columns -> LDS: int8 [NC][kp], then d [NC][nb], s [NC][nb]
-    int8_t * lq = (int8_t *) sm;
-    float * ld = (float *) (sm + NC * kp);
-    float * ls = ld + NC * nb;
-    {
-        const int4 * gq = (const int4 *) (a.q + col0 * kp);
-        const int n16 = (int) (ncols * kp / 16);
-        for (int i = threadIdx.x; i < n16; i += 256) ((int4 *) lq)[i] = gq[i];
-        const int nf = (int) (ncols * nb);
-        for (int i = threadIdx.x; i < nf; i += 256) { ld[i] = a.d[col0 * nb + i]; ls[i] = a.s[col0 * nb + i]; }
-        for (int i = threadIdx.x + nf; i < NC * nb; i += 256) { ld[i] = 0.f; ls[i] = 0.f; }   // padded columns: zero scales
-    }
-    __syncthreads();
-    const ActQ al{lq, ld, ls, kp};
-    float acc[NC], acc2[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) { acc[c] = 0.f; acc2[c] = 0.f; }
-    while (true) {
-#pragma unroll
-        for (int j = 0; j < UNR; ++j) {
-            const int u = u0 + j * LPR;
-            if (u < p.units) {
-                unit_compute<QT, NC>(rg[j], u, al, acc);
-                if constexpr (GLU) unit_compute<QT, NC>(rg2[j], u, al, acc2);
-            }
-        }
-        u0 += LPR * UNR;
-        if (u0 >= p.units) break;
-        load_batch(u0);
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-#pragma unroll
-        for (int o = LPR / 2; o > 0; o >>= 1) {
-            acc[c] += __shfl_xor(acc[c], o, 64);
-            if constexpr (GLU) acc2[c] += __shfl_xor(acc2[c], o, 64);
-        }
-    }
-    if (sub == 0 && row < p.nrows) {
-        float * out = p.dst + i12 * p.d_c2 + i13 * p.d_c3 + row;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            if (c < ncols) {
-                float v = acc[c];
-                if constexpr (GLU) v = (v / (1.0f + expf(-v))) * acc2[c];
-                if constexpr (EPI == 2) v += p.res[row + c * p.r_col];
-                out[c * p.d_col] = v;
-            }
-        }
-    }
-}
-
-static size_t mmvq_lds_bytes(int nc, int64_t kp) { return (size_t) nc * kp + 2 * (size_t) nc * (kp / 32) * sizeof(float); }
-constexpr size_t MMVQ_LDS_MAX = 160 * 1024;   // gfx950: LDS per CU (opt-in above 64 KB)
-
-template <int QT, int NC, int EPI, int LPR, int UNR>
-static void launch_lds_u(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
-    constexpr int RPB = 4 * (64 / LPR);
-    const size_t lds = mmvq_lds_bytes(NC, a.kp);
-    MX_LDS_OPTIN((k_mmvq_lds<QT, NC, LPR, UNR, EPI>), (int) MMVQ_LDS_MAX);
-    dim3 grid((unsigned) mx_ceil_div(p.nrows, RPB), (unsigned) nch);
-    MX_KLOG("mmvq_lds qt=%d nc=%d ncols=%d lpr=%d unr=%d epi=%d M=%d K=%d lds=%zu", QT, NC, (int) p.ncols, LPR, UNR, EPI, (int) p.nrows,
-            (int) (p.units * 32), lds);
-    k_mmvq_lds<QT, NC, LPR, UNR, EPI><<<grid, 256, lds, c.st>>>(p, a);
-}
-
-// geometry (g_tune[41] = LPR, g_tune[43] = UNR for sweeps): LPR 16 (16 rows per workgroup:
-// the activation staging amortised over more rows), up to 8 units of a lane in flight,
-// 4 for the wide column groups (registers: NC accumulators)
-template <int QT, int NC, int EPI>
-static void launch_lds(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
-    int lpr = 16;
-    if (g_tune[41] == 16 || g_tune[41] == 32 || g_tune[41] == 64) lpr = g_tune[41];
-    const int64_t per_lane = mx_ceil_div(p.units, lpr);
-    int unr = per_lane >= 8 ? 8 : (per_lane >= 4 ? 4 : 2);
-    if (NC >= 8 && unr > 4) unr = 4;
-    if (g_tune[43] == 2 || g_tune[43] == 4 || g_tune[43] == 8) unr = g_tune[43];
-#define LU(L, U) if (lpr == L && unr == U) return launch_lds_u<QT, NC, EPI, L, U>(c, p, a, nch);
-    LU(16, 2) LU(16, 4) LU(16, 8) LU(32, 2) LU(32, 4) LU(32, 8) LU(64, 2) LU(64, 4) LU(64, 8)
-#undef LU
-    MX_ABORT("mmvq_lds lpr=%d unr=%d", lpr, unr);
-}
-
 // launch geometry: enough blocks to cover 256 CUs, every lane's units in flight at once
 template <int QT, int NC, int EPI, int LPR>
 static void launch_lpr(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
@@ -367,9 +243,14 @@ static void launch_lpr(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch
     dim3 grid((unsigned) mx_ceil_div(p.nrows, RPB), (unsigned) nch);
     const int64_t per_lane = mx_ceil_div(p.units, LPR);
     MX_KLOG("mmvq1 qt=%d nc=%d lpr=%d epi=%d M=%d", QT, NC, LPR, EPI, (int) p.nrows);
+    // round 6: two columns keep up to 4 units of a lane in flight (g_tune[43] = 2: the round-1
+    // depth of 2; the wider groups stay at 2 — their activation registers grow with NC)
     if constexpr (NC == 1) {
         if (per_lane >= 5) k_mmvq<QT, NC, LPR, 8, EPI><<<grid, 256, 0, c.st>>>(p, a);
         else if (per_lane >= 3) k_mmvq<QT, NC, LPR, 4, EPI><<<grid, 256, 0, c.st>>>(p, a);
+        else k_mmvq<QT, NC, LPR, 2, EPI><<<grid, 256, 0, c.st>>>(p, a);
+    } else if constexpr (NC == 2) {
+        if (per_lane >= 3 && g_tune[43] != 2) k_mmvq<QT, NC, LPR, 4, EPI><<<grid, 256, 0, c.st>>>(p, a);
         else k_mmvq<QT, NC, LPR, 2, EPI><<<grid, 256, 0, c.st>>>(p, a);
     } else {
         k_mmvq<QT, NC, LPR, 2, EPI><<<grid, 256, 0, c.st>>>(p, a);
@@ -386,18 +267,8 @@ static void launch_mmvq_nc(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t
     else launch_lpr<QT, NC, EPI, 32>(c, p, a, nch);
 }
 
-static const bool g_mmvq_lds_off = getenv("GGML_MI355X_MMVQ_LDS_OFF") != nullptr;   // A/B (or g_tune[44] = 1): the round-1 k_mmvq for 2-8 columns
-
 template <int QT, int EPI>
 static void launch_mmvq(OpCtx & c, const MmvArgs & p, const ActQ & a, int64_t nch) {
-    if (p.ncols >= 2 && p.ncols <= 8 && !g_mmvq_lds_off && g_tune[44] != 1) {
-        const int nc = p.ncols == 2 ? 2 : (p.ncols <= 4 ? 4 : 8);
-        if (mmvq_lds_bytes(nc, a.kp) <= MMVQ_LDS_MAX) {
-            if (nc == 2) return launch_lds<QT, 2, EPI>(c, p, a, nch);
-            if (nc == 4) return launch_lds<QT, 4, EPI>(c, p, a, nch);
-            return launch_lds<QT, 8, EPI>(c, p, a, nch);
-        }
-    }
     switch (p.ncols) {
         case 1: launch_mmvq_nc<QT, 1, EPI>(c, p, a, nch); break;
         case 2: launch_mmvq_nc<QT, 2, EPI>(c, p, a, nch); break;

@@ -325,7 +325,6 @@ struct RouterArgs {
     const char * wr; size_t wr1; int wf16;                       // router weights, row (expert) stride in bytes
     float * logits;                                               // MUL_MAT output [n_exp]
     unsigned int * cnt;                                           // arrival counter, zero between launches
-    int acqrel;                                                   // g_tune[45] = 1: acq_rel count + acquire fence (A/B)
     TopkArgs tk;
 };
 
@@ -404,20 +403,10 @@ __global__ __launch_bounds__(256) void k_moe_router(RouterArgs p) {
     // ---- the last workgroup to arrive runs the top-k chain
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    // round 6: a RELAXED count, as k_fattn_dec3's merge: every value the last workgroup reads
-    // (the logits) went out as an agent-scope atomic store, written through to the device
-    // coherence point and complete at the s_waitcnt above, and is read back by agent-scope
-    // loads — the acq_rel count's L2 writeback on every workgroup and the acquire fence's
-    // L2 invalidate on the last one (~1-2 us of this launch's tail) order nothing more.
-    // g_tune[45] = 1: the round-5 acq_rel form (A/B)
-    if (tid == 0) {
-        const unsigned prev = p.acqrel ? __hip_atomic_fetch_add(p.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
-                                       : __hip_atomic_fetch_add(p.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == gridDim.x - 1;
-    }
+    if (tid == 0) s_last = __hip_atomic_fetch_add(p.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (!s_last) return;
-    if (p.acqrel) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (tid < 64) {
         const float lg = lane < p.tk.n_exp ? __hip_atomic_load(&p.logits[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
         topk_chain(p.tk, 0, lane, lg);
@@ -486,7 +475,6 @@ int fuse_moe_router(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map)
     r.logits = (float *) mm->data;
     r.tk = tk;
     r.cnt = c.s->fa_cnt + MX_FA_CNT - 2;        // (a slot of its own above the decode attention's counters)
-    r.acqrel = g_tune[45] == 1;
     MX_KLOG("moe_router K=%d n_exp=%d k=%d norm=%d wf16=%d", (int) K, n_exp, tk.k, tk.wn != nullptr, r.wf16);
     k_moe_router<<<(unsigned) n_exp, 256, 0, c.st>>>(r);
     return last - i + 1;
