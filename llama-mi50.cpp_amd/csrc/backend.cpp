@@ -167,6 +167,15 @@ static void staged_writes_pending_wait(int dev, hipStream_t stream) {
 // ---------------------------------------------------------------------------
 // device buffers
 // ---------------------------------------------------------------------------
+// Round 6: a generation count of the model weights — bumped by any buffer free and by every
+// write into a weights buffer (ggml_backend_buffer_set_usage(WEIGHTS), which libllama sets
+// on its model buffers): copies of weights kept elsewhere (split.cpp's slice-local norm
+// weights) are valid while it is unchanged
+static std::atomic<unsigned> g_weights_gen{1};
+unsigned mx_weights_gen() { return g_weights_gen.load(std::memory_order_relaxed); }
+static void weights_touched(ggml_backend_buffer_t b) {
+    if (b && b->usage == GGML_BACKEND_BUFFER_USAGE_WEIGHTS) g_weights_gen.fetch_add(1, std::memory_order_relaxed);
+}
 // Staged writes into this buffer that are still queued (be_sync no longer flushes, round 5)
 // or flushed but in flight must land before the memory goes back: otherwise the later
 // k_stage_flush writes into a freed range — or into the next allocation at that address.
@@ -188,6 +197,7 @@ static void stage_release_range(int dev, const char * lo, const char * hi) {
     }
 }
 static void buf_free(ggml_backend_buffer_t b) {
+    g_weights_gen.fetch_add(1, std::memory_order_relaxed);
     BufferCtx * c = (BufferCtx *) b->context;
     if (c->base) {
         hipSetDevice(c->device);
@@ -200,6 +210,7 @@ static void * buf_base(ggml_backend_buffer_t b) { return ((BufferCtx *) b->conte
 static ggml_status buf_init_tensor(ggml_backend_buffer_t, ggml_tensor *) { return GGML_STATUS_SUCCESS; }
 
 static void buf_memset(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size_t off, size_t size) {
+    weights_touched(b);
     BufferCtx * c = (BufferCtx *) b->context;
     HIP_CHECK(hipSetDevice(c->device));
     staged_writes_wait(c->device, hipStreamPerThread);
@@ -207,6 +218,7 @@ static void buf_memset(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size
     HIP_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
 static void buf_set(ggml_backend_buffer_t b, ggml_tensor * t, const void * data, size_t off, size_t size) {
+    weights_touched(b);
     BufferCtx * c = (BufferCtx *) b->context;
     HIP_CHECK(hipSetDevice(c->device));
     if (stage_write(c->device, (char *) t->data + off, data, size)) return;
@@ -239,6 +251,7 @@ static bool buf_cpy(ggml_backend_buffer_t b, const ggml_tensor * src, ggml_tenso
     return true;
 }
 static void buf_clear(ggml_backend_buffer_t b, uint8_t v) {
+    weights_touched(b);
     BufferCtx * c = (BufferCtx *) b->context;
     HIP_CHECK(hipSetDevice(c->device));
     staged_writes_wait(c->device, hipStreamPerThread);
@@ -367,6 +380,7 @@ static void be_free(ggml_backend_t b) {
     delete s;  // the ggml_backend struct lives inside Stream
 }
 static void be_set_async(ggml_backend_t b, ggml_tensor * t, const void * data, size_t off, size_t size) {
+    weights_touched(t->buffer);
     Stream * s = stream_of(b);
     const double t0 = now_us();
     HIP_CHECK(hipSetDevice(s->device));

@@ -207,6 +207,9 @@ int split_local_slices(const Stream * s, const ggml_tensor * w, void ** data, in
 int split_slices(const Stream * s, const ggml_tensor * w, void ** data, int64_t * lo, int64_t * hi, int * dev);
 bool split_on_main(const Stream * s, const ggml_tensor * w, int dev);   // slice of w runs on the main stream itself
 OpCtx split_fork(OpCtx & c, int dev);             // the slice device's stream, after the main stream's work so far
+struct XStage;
+// (round 6) the activation of a fused per-slice launch copied to the slice device once (split.cpp)
+XStage split_local_xs(OpCtx & dc, const Stream * main, int dev, const XStage & xs, int64_t K, size_t * bytes);
 void split_join(OpCtx & c, int dev);              // the main stream, after the slice stream's work so far
 void split_stream_free(const Stream * main);   // be_free: drop the freed stream's row-split staging
 void op_mul_mat_id(OpCtx & c, ggml_tensor * dst);

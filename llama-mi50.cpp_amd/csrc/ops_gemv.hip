@@ -335,7 +335,14 @@ bool gemv2_fap_o_ok(const Stream * s, const ggml_tensor * wo, const ggml_tensor 
     int64_t lo[MX_MAX_DEVICES], hi[MX_MAX_DEVICES];
     int dv[MX_MAX_DEVICES];
     const int ns = split_slices(s, wo, sd, lo, hi, dv);
-    for (int k = 0; k < ns; ++k) if (!gemv2_fap_ok(wo->type, wo->ne[0], hi[k] - lo[k])) return false;
+    // round 6: slices on other GPUs take the merged attention output instead (16 KB per
+    // slice device at Llama-3-8B, against 66 KB of split partials); GGML_MI355X_SPLIT_FAP=1
+    // keeps the partials for them too (A/B)
+    static const bool fap_remote = getenv("GGML_MI355X_SPLIT_FAP") != nullptr;
+    for (int k = 0; k < ns; ++k) {
+        if (!gemv2_fap_ok(wo->type, wo->ne[0], hi[k] - lo[k])) return false;
+        if (!fap_remote && !split_on_main(s, wo, dv[k])) return false;
+    }
     return ns > 0;
 }
 
@@ -358,7 +365,9 @@ void gemv2_fap_o_launch(OpCtx & c, const ggml_tensor * wo, const XStage & xs, fl
     for (int k = 0; k < ns; ++k) {
         if (split_on_main(c.s, wo, dv[k])) { gemv2_launch(c, &ws[k], nullptr, xs, add + lo[k], res + lo[k]); continue; }
         OpCtx dc = split_fork(c, dv[k]);
-        gemv2_launch(dc, &ws[k], nullptr, xs, add + lo[k], res + lo[k]);
+        size_t moved = 0;   // (round 6) the attention partials copied to the slice device once
+        const XStage lx = split_local_xs(dc, c.s, dv[k], xs, wo->ne[0], &moved);
+        gemv2_launch(dc, &ws[k], nullptr, lx, add + lo[k], res + lo[k]);
     }
     for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, wo, dv[k])) split_join(c, dv[k]);
     HIP_CHECK(hipSetDevice(c.s->device));

@@ -369,7 +369,9 @@ bool mmvq_fused_glu(OpCtx & c, const ggml_tensor * gate, const ggml_tensor * up,
             if (q8) { qs = *q8; qs.q += lg[k]; qs.d += lg[k] / 32; qs.s += lg[k] / 32; }
             if (split_on_main(c.s, wg, vg[k])) { gemv2_launch(c, &ws[0][k], &ws[1][k], xs, (float *) glu->data + lg[k], nullptr, q8 ? &qs : nullptr); continue; }
             OpCtx dc = split_fork(c, vg[k]);
-            gemv2_launch(dc, &ws[0][k], &ws[1][k], xs, (float *) glu->data + lg[k], nullptr, q8 ? &qs : nullptr);
+            size_t moved = 0;   // (round 6) x and the norm weight copied to the slice device once
+            const XStage lx = split_local_xs(dc, c.s, vg[k], xs, wg->ne[0], &moved);
+            gemv2_launch(dc, &ws[0][k], &ws[1][k], lx, (float *) glu->data + lg[k], nullptr, q8 ? &qs : nullptr);
         }
         for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, wg, vg[k])) split_join(c, vg[k]);
         HIP_CHECK(hipSetDevice(c.s->device));
@@ -421,7 +423,9 @@ bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, 
         for (int k = 0; k < ns; ++k) {
             if (split_on_main(c.s, w, dv[k])) { gemv2_launch(c, &ws[k], nullptr, xs, (float *) add->data + lo[k], (const float *) res->data + lo[k]); continue; }
             OpCtx dc = split_fork(c, dv[k]);
-            gemv2_launch(dc, &ws[k], nullptr, xs, (float *) add->data + lo[k], (const float *) res->data + lo[k]);
+            size_t moved = 0;   // (round 6) x (or its q8 image) copied to the slice device once
+            const XStage lx = split_local_xs(dc, c.s, dv[k], xs, w->ne[0], &moved);
+            gemv2_launch(dc, &ws[k], nullptr, lx, (float *) add->data + lo[k], (const float *) res->data + lo[k]);
         }
         for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, w, dv[k])) split_join(c, dv[k]);
         HIP_CHECK(hipSetDevice(c.s->device));

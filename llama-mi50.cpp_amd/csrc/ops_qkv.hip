@@ -627,6 +627,8 @@ int fuse_qkv_rope_store(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_
                 continue;
             }
             OpCtx dc = split_fork(c, sdev[0][k]);
+            size_t moved = 0;   // (round 6) x and the norm weight copied to the slice device once
+            ps.xs = split_local_xs(dc, c.s, sdev[0][k], p.xs, p.K, &moved);
             hipLaunchKernelGGL(kern, gs, dim3(nthr), gemv_lds_bytes(p.K, mode), dc.st, ps);
         }
         for (int k = 0; k < ns; ++k) if (!split_on_main(c.s, wq, sdev[0][k])) split_join(c, sdev[0][k]);

@@ -20,6 +20,7 @@
 // GGML_MI355X_VIRTUAL_DEVICES=N exposes the GPUs N times over (tests: a row split over
 // two logical devices of one MI355X exercises every path but the xGMI link itself).
 #include "backend.h"
+#include "gemv.h"
 
 #include <array>
 #include <map>
@@ -171,6 +172,9 @@ ggml_backend_buffer_type_t split_buffer_type(int main_device, const float * tens
 // second context's peer copy could overwrite the no-peer gather buffer before the first
 // one's scatter had read it).
 struct SliceState {
+    void * a = nullptr; size_t acap = 0;        // round 6: the fused launches' activation, slice-local
+    std::map<const void *, void *> nw;          // norm weights copied to the slice device (weights gen below)
+    unsigned nw_gen = 0;
     void * x = nullptr; size_t xcap = 0;        // no-peer path: src1 copy on the slice device
     void * y = nullptr; size_t ycap = 0;        // no-peer path: the slice's partial dst there
     void * g = nullptr; size_t gcap = 0;        // no-peer gather: the partial dst staged on main
@@ -201,6 +205,8 @@ void split_stream_free(const Stream * main) {
         HIP_CHECK(hipSetDevice(mx_dev_hip(d)));
         if (st.ev_done) { HIP_CHECK(hipEventSynchronize(st.ev_done)); HIP_CHECK(hipEventDestroy(st.ev_done)); }
         if (st.x) HIP_CHECK(hipFree(st.x));
+        if (st.a) HIP_CHECK(hipFree(st.a));
+        for (auto & kv : st.nw) HIP_CHECK(hipFree(kv.second));
         if (st.y) HIP_CHECK(hipFree(st.y));
         HIP_CHECK(hipSetDevice(main->device));
         if (st.ev_main) { HIP_CHECK(hipEventSynchronize(st.ev_main)); HIP_CHECK(hipEventDestroy(st.ev_main)); }
@@ -294,6 +300,73 @@ int split_slices(const Stream * s, const ggml_tensor * w, void ** data, int64_t 
 // GPUs; the main device's own slice stays on the main stream, as it would on real hardware
 bool split_on_main(const Stream * s, const ggml_tensor * w, int dev) {
     return mx_dev_hip(dev) == s->device && (!mx_force_peer() || dev == split_main_device(w->buffer->buft));
+}
+
+// Round 6: the activation of a fused per-slice decode launch, copied to a slice device that
+// is not the main GPU — once per op and device — instead of read from the main GPU by
+// every workgroup over xGMI (the QKV slice alone was ~224 workgroups x 32 KB of
+// remote reads per layer; the reference quantises src1 once and peer-copies it, ggml-cuda.cu:
+// 1603-1611, 1680-1692). On dc's stream (after split_fork): x (f32) or its q8 image, the
+// attention's split partials (fap), and the deferred norm's weight — static model data,
+// copied once per device and kept while no weights buffer changes (mx_weights_gen). Returns
+// the XStage over the local copies; *bytes = the bytes this call moved to the device.
+unsigned mx_weights_gen();
+XStage split_local_xs(OpCtx & dc, const Stream * main, int dev, const XStage & xs, int64_t K, size_t * bytes) {
+    *bytes = 0;
+    const int hip = mx_dev_hip(dev);
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    int main_l = 0;
+    for (int d = 0; d < mx_dev_count(); ++d) if (mx_dev_hip(d) == main->device) { main_l = d; break; }
+    SliceState & st = slice_state(main, main_l, dev);
+    XStage r = xs;
+    auto copy = [&](void * dst, const void * src, size_t n) {
+        HIP_CHECK(hipSetDevice(hip));
+        // (one GPU under FORCE_PEER: a plain device copy — a peer copy between a device and
+        // itself is not captured into a graph, it would run once at capture time)
+        if (hip == main->device) HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, dc.st));
+        else HIP_CHECK(hipMemcpyPeerAsync(dst, hip, src, main->device, n, dc.st));
+        *bytes += n;
+    };
+    size_t need = 0;
+    const size_t xb = (size_t) K * 4, qb = (size_t) K + 2 * (size_t) (K / 32) * 4;
+    const size_t fb = xs.fap ? (size_t) (K / xs.fap_d) * xs.fap_ns * (xs.fap_d + 2) * 4 : 0;
+    if (xs.fap) need = fb;
+    else if (xs.q8) need = qb;
+    else need = xb;
+    char * buf = (char *) grow(st.a, st.acap, hip, need + 512);
+    if (xs.fap) {
+        copy(buf, xs.fap, fb);
+        r.fap = (const float *) buf;
+    } else if (xs.q8) {
+        copy(buf, xs.q8, (size_t) K);
+        copy(buf + ((K + 255) & ~(int64_t) 255), xs.q8d, (size_t) (K / 32) * 4);
+        copy(buf + ((K + 255) & ~(int64_t) 255) + 256 + (size_t) (K / 32) * 4, xs.q8s, (size_t) (K / 32) * 4);
+        r.q8 = (const int8_t *) buf;
+        r.q8d = (const float *) (buf + ((K + 255) & ~(int64_t) 255));
+        r.q8s = (const float *) (buf + ((K + 255) & ~(int64_t) 255) + 256 + (size_t) (K / 32) * 4);
+    } else {
+        copy(buf, xs.x, xb);
+        r.x = (const float *) buf;
+    }
+    if (xs.norm) {
+        if (st.nw_gen != mx_weights_gen()) {
+            HIP_CHECK(hipSetDevice(hip));
+            for (auto & kv : st.nw) HIP_CHECK(hipFree(kv.second));
+            st.nw.clear();
+            st.nw_gen = mx_weights_gen();
+        }
+        auto it = st.nw.find(xs.nw);
+        if (it == st.nw.end()) {
+            void * p = nullptr;
+            HIP_CHECK(hipSetDevice(hip));
+            HIP_CHECK(hipMalloc(&p, xb));
+            copy(p, xs.nw, xb);
+            it = st.nw.emplace(xs.nw, p).first;
+        }
+        r.nw = (const float *) it->second;
+    }
+    MX_KLOG("split_stage dev=%d K=%lld bytes=%zu src=%s", dev, (long long) K, *bytes, xs.fap ? "fap" : (xs.q8 ? "q8" : (xs.norm ? "norm" : "f32")));
+    return r;
 }
 
 OpCtx split_fork(OpCtx & c, int dev) {

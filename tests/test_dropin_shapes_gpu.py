@@ -197,8 +197,9 @@ def test_llama3_8b_width_row_split_decode(l8b, tmp_path, ts, fa):
     branch separate GPUs with peer access take): q/k/v + RoPE + K/V stores run as ONE fused
     launch per slice (round 5, ops_qkv.hip: slices split at head boundaries), the other
     slices on their devices' own streams; -fa 0 stores V transposed (per-element cache
-    indices); the attention's split partials are merged by every O-projection slice. Logits against the reference CPU backend; graph capture on (the production
-    path on one GPU)."""
+    indices); each remote slice's activation staged on its device once per op (round 6).
+    Logits against the reference CPU backend; graph capture on (the production path on one
+    GPU)."""
     n_dev = len(ts.split(","))
     toks = np.random.default_rng(25).integers(0, 128000, 10)
     cpu, _, _ = run_ref(tmp_path, l8b, toks, 0, fa, incremental=True)
@@ -216,10 +217,18 @@ def test_llama3_8b_width_row_split_decode(l8b, tmp_path, ts, fa):
     sr = [tuple(map(int, re.search(r"slices=(\d+) remote=(\d+)", ln).groups())) for ln in qs]
     assert all(a == n_dev and b == n_dev - 1 for a, b in sr), sr[:4]
     assert not any(ln.startswith("qkv ") for ln in klog), klog[-40:]
-    # the attention's split partials merged by every O-projection slice (-fa 1 and -fa 0)
-    fs = [ln for ln in klog if ln.startswith("fap_split ")]
-    assert len(fs) >= 2 and all(f"slices={n_dev} remote={n_dev - 1}" in ln for ln in fs), klog[-40:]
-    assert any(ln.startswith("fattn_dec2_part " if fa else "attn_nofa_part ") for ln in klog), klog[-40:]
+    # round 6: every slice on another device gets its activation copied there ONCE per op
+    # (split.cpp split_local_xs: x or its q8 image, and the norm weight the first time) instead
+    # of each workgroup reading it over the link; the attention is merged on the main device
+    # (16 KB per slice device instead of 66 KB of split partials), so the O projection runs as
+    # the residual GEMV per slice
+    st = [ln for ln in klog if ln.startswith("split_stage ")]
+    assert st and not any("src=fap" in ln for ln in st), klog[-40:]
+    moved = [int(re.search(r"bytes=(\d+)", ln).group(1)) for ln in st]
+    assert max(moved) <= 2 * 4 * 4096 + 2 * 14336, moved[:12]    # (x + the norm weight once; the down q8 image)
+    assert not any(ln.startswith("fap_split ") for ln in klog), klog[-40:]
+    adds = [ln for ln in klog if ln.startswith("mm_split_add ")]
+    assert adds and all(f"slices={n_dev} remote={n_dev - 1}" in ln for ln in adds), klog[-40:]
 
 
 def test_llama3_8b_width_decode_graph_replay(l8b, tmp_path):
