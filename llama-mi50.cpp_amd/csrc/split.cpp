@@ -22,6 +22,7 @@
 #include "backend.h"
 #include "gemv.h"
 
+#include <algorithm>
 #include <array>
 #include <map>
 #include <mutex>
@@ -333,7 +334,9 @@ XStage split_local_xs(OpCtx & dc, const Stream * main, int dev, const XStage & x
     if (xs.fap) need = fb;
     else if (xs.q8) need = qb;
     else need = xb;
-    char * buf = (char *) grow(st.a, st.acap, hip, need + 512);
+    // one buffer for every op of the graph, sized once: a later op must not reallocate it
+    // while an earlier op's slice kernel still reads it (nor inside a graph capture)
+    char * buf = (char *) grow(st.a, st.acap, hip, std::max<size_t>(need + 512, (size_t) 512 << 10));
     if (xs.fap) {
         copy(buf, xs.fap, fb);
         r.fap = (const float *) buf;
