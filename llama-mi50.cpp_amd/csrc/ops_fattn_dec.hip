@@ -643,11 +643,6 @@ static void fd_take_new_row(OpCtx & c, const ggml_tensor * dst, FaDecArgs & a) {
     a.nr_k = r.k; a.nr_ik = r.kidx;
     a.nr_v = r.v; a.nr_iv = r.vidx;
     r.on = false;
-    // TEMPORARY timing knob (round 6 attribution; wrong results by construction): 1 = drop the
-    // row, 2 = read the new row from q instead of the stage
-    static const int dbg = getenv("GGML_MI355X_KVNEW_DBG") ? atoi(getenv("GGML_MI355X_KVNEW_DBG")) : 0;
-    if (dbg == 1) { a.nr_k = a.nr_v = nullptr; }
-    if (dbg == 2) { a.nr_k = a.nr_k ? (const float *) a.q : nullptr; a.nr_v = a.nr_v ? (const float *) a.q : nullptr; }
 }
 
 size_t fa_dec2_scratch(const ggml_tensor * dst) {
