@@ -53,29 +53,7 @@ static Device * dev_ctx(ggml_backend_dev_t d) { return (Device *) d->context; }
 // synchronize. Per decoded token libllama writes ~6 inputs: 6 x (hipMemcpyAsync +
 // hipEventRecord) of host time on the critical path between tokens, and 6 blit launches on
 // the GPU (drop-in profile, profiles/r04/), became one launch.
-struct StageEntry { const char * src; char * dst; uint32_t n, chunk0; };
-constexpr int kFlushMax = 16;                  // ranges per flush launch
-// bytes per workgroup: one 16-B load per thread, i.e. ONE round trip over PCIe per workgroup
-// (16 KB per workgroup took four: the decoded token's 16 KB embedding row made the flush
-// 10.4 us, profiles/r05/)
-constexpr uint32_t kFlushChunk = 4096;
-struct StageFlushArgs { StageEntry e[kFlushMax]; int n; };
-
-__global__ __launch_bounds__(256) void k_stage_flush(StageFlushArgs a) {
-    int k = 0;
-    while (k + 1 < a.n && blockIdx.x >= a.e[k + 1].chunk0) ++k;   // workgroup-uniform
-    const StageEntry e = a.e[k];
-    const uint32_t off = (blockIdx.x - e.chunk0) * kFlushChunk;
-    const uint32_t n = min(kFlushChunk, e.n - off);
-    const char * src = e.src + off;
-    char * dst = e.dst + off;
-    if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0) {
-        for (uint32_t i = 16 * threadIdx.x; i + 16 <= n; i += 16 * 256) *(uint4 *) (dst + i) = *(const uint4 *) (src + i);
-        for (uint32_t i = (n & ~15u) + threadIdx.x; i < n; i += 256) dst[i] = src[i];
-    } else {
-        for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
-    }
-}
+// (StageEntry / StageFlushArgs and the flush kernel k_stage_flush: backend.h, ops_misc.hip)
 
 struct Staging {
     std::mutex mu;
@@ -106,7 +84,7 @@ static void stage_flush_locked(Staging & st) {
             a.e[k].chunk0 = chunks;
             chunks += (a.e[k].n + kFlushChunk - 1) / kFlushChunk;
         }
-        k_stage_flush<<<chunks, 256, 0, st.s->stream>>>(a);
+        stage_flush_launch(a, chunks, st.s->stream);
         st.n_flush++;
     }
     HIP_CHECK(hipEventRecord(st.ev, st.s->stream));

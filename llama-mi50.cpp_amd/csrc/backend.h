@@ -56,6 +56,17 @@ struct Scratch {
 };
 
 // quantised activation columns: int8 values + per-32 f32 scale d and d·Σq
+// staged small writes (backend.cpp): queued ranges of the pinned ring copied by one
+// k_stage_flush launch (ops_misc.hip)
+struct StageEntry { const char * src; char * dst; uint32_t n, chunk0; };
+constexpr int kFlushMax = 16;                  // ranges per flush launch
+// bytes per workgroup: one 16-B load per thread, i.e. ONE round trip over PCIe per workgroup
+// (16 KB per workgroup took four: the decoded token's 16 KB embedding row made the flush
+// 10.4 us, profiles/r05/)
+constexpr uint32_t kFlushChunk = 4096;
+struct StageFlushArgs { StageEntry e[kFlushMax]; int n; };
+void stage_flush_launch(const StageFlushArgs & a, unsigned chunks, hipStream_t st);
+
 struct ActQ {
     const int8_t * q;    // [ncols][kp]
     const float * d;     // [ncols][kp/32]
@@ -230,8 +241,10 @@ bool mmq_fused_glu(OpCtx & c, const ggml_tensor * gate_mm, const ggml_tensor * u
 bool mmq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * res, ggml_tensor * add);
 // 2-3 prefill GEMMs sharing src1 (q/k/v) in one launch (k_mmq3m); false if not eligible (nothing run)
 bool mmq_group_run(OpCtx & c, ggml_tensor * const * mms, int n);
+#if defined(__HIPCC__)
 // f16 act-cache slot for a producer's f32 output rows (ops_mm.hip); null if it does not fit
 _Float16 * mmq_act_claim(OpCtx & c, const void * data, int64_t K, int64_t ncols, size_t row_bytes);
+#endif
 // out = W·x + residual (MUL_MAT followed by ADD)
 bool mmvq_fused_add(OpCtx & c, const ggml_tensor * mm, const ggml_tensor * residual, ggml_tensor * add);
 // RMS_NORM → MUL(w) that also emits the quantised activation of its output

@@ -139,6 +139,14 @@ extern int g_klog;
 void klog_add(const char * fmt, ...) __attribute__((format(printf, 1, 2)));
 }
 #define MX_KLOG(...) do { if (mx::g_klog) mx::klog_add(__VA_ARGS__); } while (0)
+// A/B-experiment code (timing variants whose results are wrong by construction, debug
+// masks, opt-in alternatives measured slower: the balanced QKV layout) is
+// compiled only into variant builds (scripts/build_variants.sh: EXTRA=-DMX_AB_VARIANTS=1);
+// in the product library those knobs are dead code.
+#ifndef MX_AB_VARIANTS
+#define MX_AB_VARIANTS 0
+#endif
+#define MX_DBG(x) (MX_AB_VARIANTS && (x))
 #if defined(__HIPCC__)
 
 // Cross-lane reductions on DPP (gfx9 data-parallel primitives: quad_perm, half/row
@@ -190,14 +198,6 @@ __device__ __forceinline__ float lane_bcast(float v, int lane) {
 // Debug phase tracing (tools/opbench.py --trace): an instrumented kernel gets a device
 // pointer (null unless tracing) for its first workgroup and records s_memtime per wave at
 // phase boundaries: ptr[wave * 8 + phase].
-// A/B-experiment code (timing variants whose results are wrong by construction, debug
-// masks, opt-in alternatives measured slower: the balanced QKV layout) is
-// compiled only into variant builds (scripts/build_variants.sh: EXTRA=-DMX_AB_VARIANTS=1);
-// in the product library those knobs are dead code.
-#ifndef MX_AB_VARIANTS
-#define MX_AB_VARIANTS 0
-#endif
-#define MX_DBG(x) (MX_AB_VARIANTS && (x))
 
 #define MX_TRACE(ptr, ph) do { if ((ptr) && (threadIdx.x & 63) == 0) \
     (ptr)[(threadIdx.x >> 6) * 8 + (ph)] = __builtin_amdgcn_s_memtime(); } while (0)

@@ -11,6 +11,8 @@ bool mmvq_type_ok(int t);
 ActQ quantize_activations(OpCtx & c, const ggml_tensor * src1);
 size_t quantize_scratch(const ggml_tensor * src1);
 void mmvq_run(OpCtx & c, ggml_tensor * dst);
+bool gemv_nc_ok(const ggml_tensor * dst);          // ops_gemv_nc.hip: 2..8 columns, LDS-staged
+void gemv_nc_run(OpCtx & c, ggml_tensor * dst);
 void mmv_generic_run(OpCtx & c, ggml_tensor * dst);
 
 // prefill GEMM on MFMA (ops_mm.hip)

@@ -248,6 +248,14 @@ static void pick_cfg(int type, int units, int nrows, bool glu, int & lpr, int & 
     const int base = glu ? 2 : 0;
     if (g_tune[base]) lpr = g_tune[base];
     if (g_tune[base + 1]) upl = g_tune[base + 1];
+    // round 6: the FFN down projections alone (sweeps). tg128, one box (profiles/r06/
+    // down_geometry_sweep.txt): default (Q6_K 32x2, Q4_K 32x4) 635.6, 32x4 637.0, 64x4 634.1,
+    // 64x2 633.1, 16x4 603.6; every unit of a lane in one batch (32x8, built for the sweep)
+    // 632.9 tok/s — the down projection's geometry is not what its time is made of
+    if (!glu && units >= 128) {
+        if (g_tune[44]) lpr = g_tune[44];
+        if (g_tune[45]) upl = g_tune[45];
+    }
 }
 
 // the residual GEMV can take its x as attention split partials (XS_FAP*: fa_dec2_partials):

@@ -1,0 +1,154 @@
+// ops_gemv_nc.hip — multi-column decode GEMV (round 6): dst[:, c] = W · x_c for 2..8
+// activation columns (llama-server's parallel slots, speculative drafts). Reference:
+// mul_mat_vec_q templated on ncols_dst 1..8 (ggml-cuda/mmvq.cu:397-502, dispatch
+// ggml-cuda.cu:2183-2266 for src1->ne[1] <= MMVQ_MAX_BATCH_SIZE); its perf case is
+// tests/test-backend-ops.cpp:8429-8435 (4096 x bs x 14336, bs 1..8).
+//
+// MI355X design. The round-1 k_mmvq (ops_mmvq.hip) read every column's q8 activation from
+// the vector-memory path for every weight unit — NC x (32 + 8) bytes per 18-36 weight bytes
+// — so its load path, not HBM, set the time (bs 2 at 0.30 of HBM, bs 8 at 0.11). Here the
+// columns' q8 images (k_quantize_act, shared through the act cache) are staged into LDS by
+// LDS-DMA once per workgroup, behind the first batch of weight loads (the k_gemv2 order:
+// activation DMA, weights, wait for the DMA only); each lane unpacks a weight unit once and
+// dots it against all NC columns out of LDS (w2_dot per column: the unpacking is common
+// subexpression, the activation reads are the only per-column loads).
+#include "backend.h"
+#include "gemv.cuh"
+#include "mm.h"
+
+namespace mx {
+
+struct GncArgs {
+    const char * w; size_t w_row;
+    float * dst; size_t d_col;           // dst column stride (floats)
+    const int8_t * q; const float * d; const float * s; int64_t kp;   // ActQ columns
+    int nrows, units, K, ncols;
+};
+
+// LDS: NC q8 images (K bytes each), then NC x K/32 scales d, then NC x K/32 sums s
+__host__ __device__ constexpr size_t gnc_lds_bytes(int nc, int64_t K) { return (size_t) nc * ((size_t) K + (size_t) K / 4); }
+
+template <int QT, int LPR, int UPL, int NC>
+__global__ __launch_bounds__(256) void k_gemv_nc(GncArgs p) {
+    extern __shared__ __align__(16) char smem[];
+    constexpr int NT = 256, RPW = 64 / LPR, STEP = LPR * UPL;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane % LPR;
+    const int blk = xcd_block((int) blockIdx.x, (int) gridDim.x, true);
+    const int row = (blk * 4 + wave) * RPW + lane / LPR;
+    const bool valid = row < p.nrows;
+    const char * rows[1] = {p.w + (int64_t) (valid ? row : p.nrows - 1) * p.w_row};
+    const int K = p.K, nb = K / 32;
+    int8_t * lq = (int8_t *) smem;
+    float * ld = (float *) (smem + (size_t) NC * K);
+    float * ls = ld + NC * nb;
+    // the activation DMA first: it retires before the weight loads issued after it
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int cc = min(c, p.ncols - 1);      // padding columns re-read the last one
+        dma_to_lds<NT, 16>(p.q + (int64_t) cc * p.kp, lq + (size_t) c * K, K);
+        dma_to_lds<NT, 4>(p.d + (int64_t) cc * (p.kp / 32), ld + c * nb, nb * 4);
+        dma_to_lds<NT, 4>(p.s + (int64_t) cc * (p.kp / 32), ls + c * nb, nb * 4);
+    }
+    W2<QT> r[1][UPL], r2[1][UPL];
+    __builtin_amdgcn_sched_barrier(0);
+    w2_load_batch<QT, UPL, 1>(rows, sub, LPR, p.units, r);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_vmcnt<UPL * w2_loads<QT>()>();          // the DMA has landed (loads retire in order)
+    lds_barrier();
+    LdsAct act[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) act[c] = LdsAct{lq + (size_t) c * K, ld + c * nb, ls + c * nb};
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+    // two register stages: batch it + 1's weights are in flight while batch it is dotted
+    // against the NC columns (the grids here run 1-2 waves per SIMD: with one stage every
+    // batch paid the whole memory latency and then its VALU work in series)
+    auto dots = [&](const W2<QT> (&w)[1][UPL], int it) {
+#pragma unroll
+        for (int j = 0; j < UPL; ++j) {
+            const int u = it * STEP + sub + j * LPR;
+            if (u < p.units) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) acc[c] += w2_dot<QT>(w[0][j], u, act[c]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    const int n_iter = (p.units + STEP - 1) / STEP;
+    for (int it = 0; it < n_iter; it += 2) {
+        if (it + 1 < n_iter) w2_load_batch<QT, UPL, 1>(rows, (it + 1) * STEP + sub, LPR, p.units, r2);
+        __builtin_amdgcn_sched_barrier(0);
+        dots(r, it);
+        if (it + 2 < n_iter) w2_load_batch<QT, UPL, 1>(rows, (it + 2) * STEP + sub, LPR, p.units, r);
+        __builtin_amdgcn_sched_barrier(0);
+        if (it + 1 < n_iter) dots(r2, it + 1);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = dpp_sum_group<LPR>(acc[c]);
+    if (sub == LPR - 1 && valid) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) if (c < p.ncols) p.dst[(size_t) c * p.d_col + row] = acc[c];
+    }
+}
+
+template <int QT, int NC>
+static void gnc_launch(OpCtx & c, const GncArgs & p) {
+    // 16 lanes x 4 units per row (Q6_K: 2 units, its unit holds 5 loads), 16 rows per workgroup
+    constexpr int LPR = 16, UPL = QT == GGML_TYPE_Q6_K ? 2 : 4;
+    constexpr int RPB = 4 * (64 / LPR);
+    const size_t lds = gnc_lds_bytes(NC, p.K);
+    if (lds > 65536) MX_LDS_OPTIN((k_gemv_nc<QT, LPR, UPL, NC>), 160 * 1024);
+    MX_KLOG("gemv_nc qt=%d nc=%d ncols=%d K=%d M=%d lds=%zu", QT, NC, p.ncols, p.K, p.nrows, lds);
+    k_gemv_nc<QT, LPR, UPL, NC><<<(unsigned) ((p.nrows + RPB - 1) / RPB), 256, lds, c.st>>>(p);
+}
+
+template <int QT>
+static void gnc_type(OpCtx & c, const GncArgs & p) {
+    switch (p.ncols) {
+        case 2: gnc_launch<QT, 2>(c, p); break;
+        case 3: gnc_launch<QT, 3>(c, p); break;
+        case 4: gnc_launch<QT, 4>(c, p); break;
+        case 5: case 6: gnc_launch<QT, 6>(c, p); break;
+        default: gnc_launch<QT, 8>(c, p); break;
+    }
+}
+
+static int gnc_nc(int64_t ncols) { return ncols <= 4 ? (int) ncols : (ncols <= 6 ? 6 : 8); }
+
+// 2..8 columns of one channel (x->ne[2] == x->ne[3] == 1), contiguous dst columns, the
+// LDS images within one CU's 160 KB
+bool gemv_nc_ok(const ggml_tensor * dst) {
+    static const bool off = getenv("GGML_MI355X_GEMV_NC_OFF") != nullptr;   // A/B: the round-1 k_mmvq
+    const ggml_tensor * w = dst->src[0], * x = dst->src[1];
+    if (off || !g_gemv2 || !gemv2_type_ok(w->type) || x->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
+    const int64_t K = w->ne[0];
+    const int64_t qk = (w->type == GGML_TYPE_Q4_0 || w->type == GGML_TYPE_Q8_0) ? 32 : 256;
+    if (K % qk || x->ne[0] != K || x->ne[1] < 2 || x->ne[1] > 8 || x->ne[2] != 1 || x->ne[3] != 1) return false;
+    if (w->ne[2] != 1 || w->ne[3] != 1 || w->nb[0] != (size_t) mx_type(w->type).size || w->ne[1] > INT32_MAX) return false;
+    if (x->nb[0] != 4 || dst->nb[0] != 4 || dst->ne[0] != w->ne[1] || dst->ne[1] != x->ne[1] || dst->nb[1] % 4) return false;
+    return gnc_lds_bytes(gnc_nc(x->ne[1]), K) <= 160 * 1024;
+}
+
+void gemv_nc_run(OpCtx & c, ggml_tensor * dst) {
+    const ggml_tensor * w = dst->src[0], * x = dst->src[1];
+    const ActQ a = quantize_activations(c, x);
+    GncArgs p{};
+    p.w = (const char *) w->data; p.w_row = w->nb[1];
+    p.dst = (float *) dst->data; p.d_col = dst->nb[1] / 4;
+    p.q = a.q; p.d = a.d; p.s = a.s; p.kp = a.kp;
+    p.nrows = (int) w->ne[1]; p.K = (int) w->ne[0]; p.ncols = (int) x->ne[1];
+    p.units = (int) (w->ne[0] / ((w->type == GGML_TYPE_Q4_0 || w->type == GGML_TYPE_Q8_0) ? 32 : 64));
+    MX_ASSERT(a.kp == p.K);
+    switch (w->type) {
+        case GGML_TYPE_Q4_K: gnc_type<GGML_TYPE_Q4_K>(c, p); break;
+        case GGML_TYPE_Q5_K: gnc_type<GGML_TYPE_Q5_K>(c, p); break;
+        case GGML_TYPE_Q6_K: gnc_type<GGML_TYPE_Q6_K>(c, p); break;
+        case GGML_TYPE_Q4_0: gnc_type<GGML_TYPE_Q4_0>(c, p); break;
+        case GGML_TYPE_Q8_0: gnc_type<GGML_TYPE_Q8_0>(c, p); break;
+        default: MX_ABORT("gemv_nc type %d", (int) w->type);
+    }
+}
+
+}  // namespace mx

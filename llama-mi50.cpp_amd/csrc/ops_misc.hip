@@ -13,6 +13,28 @@
 
 namespace mx {
 
+// the staged-write flush (backend.cpp stage_flush_locked): workgroup = one kFlushChunk of
+// one queued range, copied from the pinned ring (zero-copy reads over PCIe)
+__global__ __launch_bounds__(256) void k_stage_flush(StageFlushArgs a) {
+    int k = 0;
+    while (k + 1 < a.n && blockIdx.x >= a.e[k + 1].chunk0) ++k;   // workgroup-uniform
+    const StageEntry e = a.e[k];
+    const uint32_t off = (blockIdx.x - e.chunk0) * kFlushChunk;
+    const uint32_t n = min(kFlushChunk, e.n - off);
+    const char * src = e.src + off;
+    char * dst = e.dst + off;
+    if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0) {
+        for (uint32_t i = 16 * threadIdx.x; i + 16 <= n; i += 16 * 256) *(uint4 *) (dst + i) = *(const uint4 *) (src + i);
+        for (uint32_t i = (n & ~15u) + threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    }
+}
+
+void stage_flush_launch(const StageFlushArgs & a, unsigned chunks, hipStream_t st) {
+    k_stage_flush<<<chunks, 256, 0, st>>>(a);
+}
+
 struct T4 {  // geometry of one operand, passed by value
     int64_t ne[4];
     size_t nb[4];

@@ -1229,6 +1229,7 @@ void op_mul_mat(OpCtx & c, ggml_tensor * dst) {
         gemv2_launch(c, dst->src[0], nullptr, xstage_of(c.s, x), (float *) dst->data, nullptr);
         return;
     }
+    if (x->ne[1] <= 8 && gemv_nc_ok(dst)) { gemv_nc_run(c, dst); return; }
     if (x->ne[1] <= 8 && quant_fast_path_ok(dst)) { mmvq_run(c, dst); return; }
     if (x->ne[1] > 8 && mm_skinny_run(c, dst)) return;   // few f32/f16 rows (the MoE router in prefill)
     if (x->ne[1] > 8 && mmq_ok(dst)) { mmq_run(c, dst); return; }

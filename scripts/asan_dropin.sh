@@ -7,7 +7,7 @@
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/asan}
 mkdir -p $OUT
-RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
+RT=$(gcc -print-file-name=libasan.so)   # GCC's runtime (Makefile: clang's intercepts HSA allocations)
 LIB=$PWD/llama-mi50.cpp_amd/lib/asan/libggml-mi355x.so
 G=$OUT/small.gguf
 [ -f $G ] || python tools/gguf_synth.py --shape small --recipe q4_k_m --out $G > /dev/null || exit 1

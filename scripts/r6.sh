@@ -18,7 +18,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 LB=oracle/_ref/llama-bench
 REFB=oracle/_ref/ref-llama-bench
-LIB=$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so
+LIB=${MXLIB:-$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so}
 G=""
 gguf() { [ -n "$G" ] || G=$(python -c "import bench; print(bench.bench_gguf('${MODEL:-llama3_8b}', '${RECIPE:-q4_k_m}'))") || exit 1; }
 fin() {  # name rc

@@ -51,6 +51,35 @@ def test_mul_mat_quant(pkg, backend, orc, tname, N):
     assert nmse(y, ref_exact) < 5e-4
 
 
+@pytest.mark.parametrize("tname", ["q4_K", "q6_K", "q5_K", "q4_0", "q8_0"])
+@pytest.mark.parametrize("N,K", [(2, 1024), (4, 1024), (5, 1024), (7, 2048), (8, 14336), (3, 14336)])
+def test_mul_mat_multicolumn(pkg, backend, orc, tname, N, K):
+    """2..8 activation columns on the LDS-staged multi-column GEMV (ops_gemv_nc.hip): every
+    column count class (5 and 7 run with a padding column), K 14336 = the down projection's
+    width with the 143 KB LDS image of 8 columns, a ragged last row tile (M % 16 != 0)"""
+    tid = NAMES[tname]
+    rng = np.random.default_rng(hash((tname, N, K, 5)) % 2**32)
+    M = 333 if K <= 2048 else 1000
+    w, rb = rand_quant(tid, M, K, rng)
+    x = rng.standard_normal((N, K)).astype(np.float32)
+
+    def build(ctx):
+        tw = ctx.new_tensor(tid, K, M)
+        tx = ctx.new_tensor("f32", K, N)
+        return [ctx.mul_mat(tw, tx)], [(tw, w), (tx, x)]
+
+    backend.klog(True)
+    try:
+        y = run(pkg, backend, build)[0].reshape(N, M)
+        log = backend.klog_read()
+    finally:
+        backend.klog(False)
+    nc = N if N <= 4 else (6 if N <= 6 else 8)
+    assert any(ln.startswith(f"gemv_nc qt={tid} nc={nc} ncols={N} K={K} M={M} ") for ln in log), log
+    assert np.all(np.isfinite(y))
+    assert nmse(y, orc.mul_mat(tid, w, rb, x)) < 5e-4
+
+
 @pytest.mark.parametrize("tname", ["q4_K", "q6_K", "q5_K"])
 @pytest.mark.parametrize("kernel", [1, 2])
 def test_mul_mat_quant_prefill_kernels(pkg, backend, orc, tname, kernel):
