@@ -277,6 +277,7 @@ bool t_overlaps_ext(const ggml_tensor * a, const ggml_tensor * b);
 bool fused_io_ok(std::initializer_list<const ggml_tensor *> outs, std::initializer_list<const ggml_tensor *> ins,
                  std::initializer_list<std::pair<const ggml_tensor *, const ggml_tensor *>> inplace = {});
 int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);
+int fuse_moe_down_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & uses);   // MUL_MAT_ID + combine
 // the executor's guard for a node about to run (deferred norms it reads or overwrites)
 void deferred_guard_node_ext(OpCtx & c, const ggml_tensor * n);
 

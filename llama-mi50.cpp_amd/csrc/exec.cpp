@@ -768,6 +768,10 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
                 const int k = fuse_attn_split_o(c, g, i, uses);
                 if (k > 0) { i += k - 1; s->n_fused += 2; s->n_nodes_run += 3; deferred_retire(s, g, i0, i); continue; }
             }
+            if (n->op == GGML_OP_MUL_MAT_ID && !g_no_moe_fusion && !g_no_combine) {   // down projection + combine
+                const int k = fuse_moe_down_combine(c, g, i, uses);
+                if (k > 0) { i += k - 1; s->n_fused += k - 1; s->n_nodes_run += k; deferred_retire(s, g, i0, i); continue; }
+            }
             if (n->op == GGML_OP_MUL_MAT_ID && try_fuse_moe_glu(c, g, i, uses)) { i += 2; s->n_fused += 2; s->n_nodes_run += 3; continue; }
             if (n->op == GGML_OP_SOFT_MAX && !g_no_moe_fusion && !g_no_topk) {
                 const int k = fuse_topk_moe(c, g, i);

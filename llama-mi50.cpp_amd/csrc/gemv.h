@@ -58,6 +58,20 @@ void gemv2_launch(OpCtx & c, const ggml_tensor * w, const ggml_tensor * w2, cons
 bool gemv2_fap_o_ok(const Stream * s, const ggml_tensor * wo, const ggml_tensor * x, const ggml_tensor * mm);
 void gemv2_fap_o_launch(OpCtx & c, const ggml_tensor * wo, const XStage & xs, float * add, const float * res);
 
+// MoE decode (ops_gemv_nc.hip): the down projection's MUL_MAT_ID and the expert combine
+// (MUL by the router weights, the per-slot ADDs, optionally + residual) in one launch
+struct MoeDownComb {
+    const ggml_tensor * as;                              // experts [K, M, n_expert]
+    const char * ids; size_t id0, id1;                   // [n_used, n_tok] i32, byte strides
+    const int8_t * q; const float * qd; const float * qs; int64_t kp;   // q8 of b: column t * n_used + slot
+    const float * wt; size_t wt1, wt2;                   // router weights, float strides (slot, token)
+    const float * res; size_t r1;                        // residual (nullable), floats per token
+    float * out; size_t o1;                              // combined output, floats per token
+    int n_used, n_tok;
+};
+bool moe_down_combine_ok(int type, int64_t K, int64_t M, int n_used, int n_tok);
+void moe_down_combine_launch(OpCtx & c, const MoeDownComb & a);
+
 // The activation a GEMV should stage for src1: the deferred RMS_NORM→MUL pair that
 // produces src1 when there is one (exec.cpp), else src1 itself.
 XStage xstage_of(Stream * s, const ggml_tensor * src1);

@@ -16,6 +16,8 @@
 #include "gemv.cuh"
 #include "mm.h"
 
+#include <type_traits>
+
 namespace mx {
 
 struct GncArgs {
@@ -148,6 +150,154 @@ void gemv_nc_run(OpCtx & c, ggml_tensor * dst) {
         case GGML_TYPE_Q4_0: gnc_type<GGML_TYPE_Q4_0>(c, p); break;
         case GGML_TYPE_Q8_0: gnc_type<GGML_TYPE_Q8_0>(c, p); break;
         default: MX_ABORT("gemv_nc type %d", (int) w->type);
+    }
+}
+
+}  // namespace mx
+
+namespace mx {
+
+// ---------------------------------------------------------------------------
+// MoE decode: the down projection's MUL_MAT_ID and the expert combine in one launch
+// (round 6). build_moe_ffn (src/llama-graph.cpp:1201-1296) ends every MoE layer with
+// experts = MUL_MAT_ID(down_exps, glu, ids) -> MUL(experts, weights) -> the ADDs of the
+// per-slot views [-> ADD(residual)]; k_moe_combine ran that tail as its own ~5 us launch
+// (profiles/r06/, Mixtral tg: 4.8 us per layer). Here a workgroup owns RPB rows of one
+// token for EVERY slot: it stages the n_used q8 activations (the gate/up SwiGLU's q8 copy)
+// into LDS, streams each slot's expert rows (expert id read on the device), and writes
+// out[row] = sum_s w_s * (W_{e_s} x_s)[row] (+ residual) — the combine's arithmetic in its
+// order (slot 0 first, then + each next slot, then + the residual).
+// ---------------------------------------------------------------------------
+struct GmcArgs {
+    const char * w; size_t w_row, w_exp; int n_expert;
+    const char * ids; size_t id0, id1;
+    const int8_t * q; const float * d; const float * s; int64_t kp;   // q8 column t * n_used + slot
+    const float * wt; size_t wt1, wt2;                                 // weights [1, n_used, n_tok] (floats)
+    const float * res; size_t r1;
+    float * out; size_t o1;
+    int nrows, units, K;
+};
+
+template <int QT, int LPR, int UPL, int NU>
+__global__ __launch_bounds__(256) void k_moe_down_comb(GmcArgs p) {
+    extern __shared__ __align__(16) char smem[];
+    constexpr int NT = 256, RPW = 64 / LPR, STEP = LPR * UPL;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = lane % LPR;
+    const int blk = xcd_block((int) blockIdx.x, (int) gridDim.x, true);
+    const int row = (blk * 4 + wave) * RPW + lane / LPR;
+    const bool valid = row < p.nrows;
+    const int64_t rr = valid ? row : p.nrows - 1;
+    const int t = blockIdx.y;
+    const int K = p.K, nb = K / 32;
+    int8_t * lq = (int8_t *) smem;
+    float * ld = (float *) (smem + (size_t) NU * K);
+    float * ls = ld + NU * nb;
+    // expert ids, router weights and the residual first: the weight addresses wait for the ids
+    int ex[NU];
+    float wt[NU];
+#pragma unroll
+    for (int s = 0; s < NU; ++s) {
+        ex[s] = *(const int32_t *) (p.ids + (size_t) s * p.id0 + (size_t) t * p.id1);
+        wt[s] = p.wt[(size_t) t * p.wt2 + (size_t) s * p.wt1];
+    }
+    const float res = p.res ? p.res[(size_t) t * p.r1 + rr] : 0.f;
+#pragma unroll
+    for (int s = 0; s < NU; ++s) {
+        const int64_t col = (int64_t) t * NU + s;
+        dma_to_lds<NT, 16>(p.q + col * p.kp, lq + (size_t) s * K, K);
+        dma_to_lds<NT, 4>(p.d + col * (p.kp / 32), ld + s * nb, nb * 4);
+        dma_to_lds<NT, 4>(p.s + col * (p.kp / 32), ls + s * nb, nb * 4);
+    }
+    const char * rows[NU];
+#pragma unroll
+    for (int s = 0; s < NU; ++s) rows[s] = p.w + (size_t) min(max(ex[s], 0), p.n_expert - 1) * p.w_exp + (size_t) rr * p.w_row;
+    W2<QT> r[NU][UPL];
+    __builtin_amdgcn_sched_barrier(0);
+    w2_load_batch<QT, UPL, NU>(rows, sub, LPR, p.units, r);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_vmcnt<UPL * NU * w2_loads<QT>()>();      // the DMA has landed (loads retire in order)
+    lds_barrier();
+    LdsAct act[NU];
+#pragma unroll
+    for (int s = 0; s < NU; ++s) act[s] = LdsAct{lq + (size_t) s * K, ld + s * nb, ls + s * nb};
+    float acc[NU];
+#pragma unroll
+    for (int s = 0; s < NU; ++s) acc[s] = 0.f;
+    const int n_iter = (p.units + STEP - 1) / STEP;
+    for (int it = 0; it < n_iter; ++it) {
+        if (it) w2_load_batch<QT, UPL, NU>(rows, it * STEP + sub, LPR, p.units, r);
+#pragma unroll
+        for (int j = 0; j < UPL; ++j) {
+            const int u = it * STEP + sub + j * LPR;
+            if (u < p.units) {
+#pragma unroll
+                for (int s = 0; s < NU; ++s) acc[s] += w2_dot<QT>(r[s][j], u, act[s]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NU; ++s) acc[s] = dpp_sum_group<LPR>(acc[s]);
+    if (sub == LPR - 1 && valid) {
+        float v = 0.f;
+#pragma unroll
+        for (int s = 0; s < NU; ++s) {
+            const float e = ex[s] >= 0 && ex[s] < p.n_expert ? acc[s] * wt[s] : 0.f;
+            v = s == 0 ? e : v + e;
+        }
+        if (p.res) v += res;
+        p.out[(size_t) t * p.o1 + row] = v;
+    }
+}
+
+bool moe_down_combine_ok(int type, int64_t K, int64_t M, int n_used, int n_tok) {
+    if (!g_gemv2 || !gemv2_type_ok(type) || M > INT32_MAX || n_tok < 1 || n_tok > 8) return false;
+    if (n_used != 2 && n_used != 4 && n_used != 8) return false;
+    const int64_t qk = (type == GGML_TYPE_Q4_0 || type == GGML_TYPE_Q8_0) ? 32 : 256;
+    return K % qk == 0 && K <= GEMV2_MAX_K && gnc_lds_bytes(n_used, K) <= 160 * 1024;
+}
+
+template <int QT, int NU>
+static void gmc_launch(OpCtx & c, const GmcArgs & p, int n_tok) {
+    constexpr int UPL = NU <= 2 ? 2 : 1;
+    const size_t lds = gnc_lds_bytes(NU, p.K);
+    auto go = [&](auto lpr) {
+        constexpr int LPR = decltype(lpr)::value, RPB = 4 * (64 / LPR);
+        if (lds > 65536) MX_LDS_OPTIN((k_moe_down_comb<QT, LPR, UPL, NU>), 160 * 1024);
+        MX_KLOG("moe_down_comb qt=%d n_used=%d n_tok=%d lpr=%d K=%d M=%d res=%d", QT, NU, n_tok, LPR, p.K, p.nrows, p.res != nullptr);
+        k_moe_down_comb<QT, LPR, UPL, NU><<<dim3((unsigned) ((p.nrows + RPB - 1) / RPB), (unsigned) n_tok), 256, lds, c.st>>>(p);
+    };
+    if (p.units >= 128) go(std::integral_constant<int, 32>());
+    else go(std::integral_constant<int, 16>());
+}
+
+template <int QT>
+static void gmc_type(OpCtx & c, const GmcArgs & p, int n_used, int n_tok) {
+    if (n_used == 2) gmc_launch<QT, 2>(c, p, n_tok);
+    else if (n_used == 4) gmc_launch<QT, 4>(c, p, n_tok);
+    else gmc_launch<QT, 8>(c, p, n_tok);
+}
+
+void moe_down_combine_launch(OpCtx & c, const MoeDownComb & a) {
+    const ggml_tensor * as = a.as;
+    GmcArgs p{};
+    p.w = (const char *) as->data; p.w_row = as->nb[1]; p.w_exp = as->nb[2]; p.n_expert = (int) as->ne[2];
+    p.ids = a.ids; p.id0 = a.id0; p.id1 = a.id1;
+    p.q = a.q; p.d = a.qd; p.s = a.qs; p.kp = a.kp;
+    p.wt = a.wt; p.wt1 = a.wt1; p.wt2 = a.wt2;
+    p.res = a.res; p.r1 = a.r1;
+    p.out = a.out; p.o1 = a.o1;
+    p.nrows = (int) as->ne[1]; p.K = (int) as->ne[0];
+    p.units = (int) (as->ne[0] / ((as->type == GGML_TYPE_Q4_0 || as->type == GGML_TYPE_Q8_0) ? 32 : 64));
+    MX_ASSERT(a.kp == p.K && moe_down_combine_ok(as->type, p.K, p.nrows, a.n_used, a.n_tok));
+    switch (as->type) {
+        case GGML_TYPE_Q4_K: gmc_type<GGML_TYPE_Q4_K>(c, p, a.n_used, a.n_tok); break;
+        case GGML_TYPE_Q5_K: gmc_type<GGML_TYPE_Q5_K>(c, p, a.n_used, a.n_tok); break;
+        case GGML_TYPE_Q6_K: gmc_type<GGML_TYPE_Q6_K>(c, p, a.n_used, a.n_tok); break;
+        case GGML_TYPE_Q4_0: gmc_type<GGML_TYPE_Q4_0>(c, p, a.n_used, a.n_tok); break;
+        case GGML_TYPE_Q8_0: gmc_type<GGML_TYPE_Q8_0>(c, p, a.n_used, a.n_tok); break;
+        default: MX_ABORT("moe_down_comb type %d", (int) as->type);
     }
 }
 

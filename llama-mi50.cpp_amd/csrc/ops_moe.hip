@@ -414,6 +414,93 @@ __global__ __launch_bounds__(256) void k_moe_router(RouterArgs p) {
     if (tid == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Round 6: the same block as ONE 1024-thread workgroup for routers of <= 8 experts (Mixtral):
+// thread t holds 4-float groups t (+ 1024) of x, the norm weight and of EVERY expert's router
+// row — all (2 + n_exp) x G 16-byte loads issued together, one memory round trip — then one
+// barrier for the sum of squares, one for the n_exp partial logits, and wave 0 runs the
+// top-k chain. The 8-workgroup form above paid, after its own loads and reductions, a
+// write-through logit store, a device-scope arrival, an acquire and the logits' reload in
+// the last workgroup: 8.3-8.7 us per layer (profiles/r06/). The norm's sum of squares and
+// the logits are summed in another order than there (per-thread groups of 4 instead of 32).
+template <int G, bool F16>
+__global__ __launch_bounds__(1024) void k_moe_router1(RouterArgs p) {
+    constexpr int NE = 8, NW = 16;
+    __shared__ float red[NW][NE + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = p.K, ng = K / 4;
+    float4 xv[G], wv[G], rv[G][NE];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int gi = min(tid + 1024 * g, ng - 1);
+        xv[g] = *(const float4 *) (p.x + 4 * gi);
+        wv[g] = *(const float4 *) (p.nw + 4 * gi);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int ee = min(e, p.tk.n_exp - 1);
+            const char * row = p.wr + (size_t) ee * p.wr1;
+            if constexpr (F16) {
+                const uint2 h = *(const uint2 *) (row + 8 * (size_t) gi);
+                rv[g][e] = make_float4(h2f((uint16_t) (h.x & 0xFFFF)), h2f((uint16_t) (h.x >> 16)),
+                                       h2f((uint16_t) (h.y & 0xFFFF)), h2f((uint16_t) (h.y >> 16)));
+            } else {
+                rv[g][e] = *(const float4 *) (row + 16 * (size_t) gi);
+            }
+        }
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if (tid + 1024 * g < ng) ss += xv[g].x * xv[g].x + xv[g].y * xv[g].y + xv[g].z * xv[g].z + xv[g].w * xv[g].w;
+    ss = wave_sum(ss);
+    if (lane == 0) red[wave][NE] = ss;
+    __syncthreads();
+    ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) ss += red[w][NE];
+    const float scale = 1.0f / sqrtf(ss / (float) K + p.eps);
+    float acc[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int gi = tid + 1024 * g;
+        const bool on = gi < ng;
+        const float v[4] = {(xv[g].x * scale) * wv[g].x, (xv[g].y * scale) * wv[g].y,
+                            (xv[g].z * scale) * wv[g].z, (xv[g].w * scale) * wv[g].w};
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+            if (on) acc[e] += rv[g][e].x * v[0] + rv[g][e].y * v[1] + rv[g][e].z * v[2] + rv[g][e].w * v[3];
+        // cur and its q8 copy: 8 threads (32 values) per block, the block's amax and sum by DPP
+        float amax = on ? fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) : 0.f;
+        amax = dpp_max_group<8>(amax);                 // (groups of <= 16 lanes: in every lane)
+        const Q8Scale qsc = q8_scale(amax);
+        int qi[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { qi[j] = q8_round(v[j], qsc.id); sum += qi[j]; }
+        sum = dpp_sum_group_i<8>(sum);
+        if (on) {
+            *(float4 *) (p.cur + 4 * gi) = make_float4(v[0], v[1], v[2], v[3]);
+            *(int *) (p.q + 4 * gi) = (qi[0] & 0xFF) | ((qi[1] & 0xFF) << 8) | ((qi[2] & 0xFF) << 16) | ((qi[3] & 0xFF) << 24);
+            if ((lane & 7) == 0) { p.qd[gi >> 3] = qsc.d; p.qs[gi >> 3] = qsc.d * (float) sum; }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const float a = wave_sum(acc[e]);
+        if (lane == 0) red[wave][e] = a;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        float lg = 0.f;
+        if (lane < p.tk.n_exp) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) lg += red[w][lane];
+            p.logits[lane] = lg;
+        }
+        topk_chain(p.tk, 0, lane, lg);
+    }
+}
+
 // RMS_NORM at node i -> MUL(w) -> MUL_MAT(gate_inp, cur) -> the top-k chain, one token.
 // Returns the nodes consumed (0: no match).
 int fuse_moe_router(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map) {
@@ -475,6 +562,15 @@ int fuse_moe_router(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map)
     r.logits = (float *) mm->data;
     r.tk = tk;
     r.cnt = c.s->fa_cnt + MX_FA_CNT - 2;        // (a slot of its own above the decode attention's counters)
+    // round 6: <= 8 experts and K <= 8192 in one 1024-thread workgroup (k_moe_router1);
+    // GGML_MI355X_MOE_ROUTER_WG=1 or g_tune[46] = 1 keeps one workgroup per expert (A/B)
+    static const bool per_expert = getenv("GGML_MI355X_MOE_ROUTER_WG") != nullptr;
+    if (!per_expert && g_tune[46] != 1 && n_exp <= 8 && K % 128 == 0 && K <= 8192) {
+        MX_KLOG("moe_router1 K=%d n_exp=%d k=%d norm=%d wf16=%d", (int) K, n_exp, tk.k, tk.wn != nullptr, r.wf16);
+        if (K <= 4096) { if (r.wf16) k_moe_router1<1, true><<<1, 1024, 0, c.st>>>(r); else k_moe_router1<1, false><<<1, 1024, 0, c.st>>>(r); }
+        else { if (r.wf16) k_moe_router1<2, true><<<1, 1024, 0, c.st>>>(r); else k_moe_router1<2, false><<<1, 1024, 0, c.st>>>(r); }
+        return last - i + 1;
+    }
     MX_KLOG("moe_router K=%d n_exp=%d k=%d norm=%d wf16=%d", (int) K, n_exp, tk.k, tk.wn != nullptr, r.wf16);
     k_moe_router<<<(unsigned) n_exp, 256, 0, c.st>>>(r);
     return last - i + 1;
@@ -499,7 +595,17 @@ __global__ void k_moe_combine(const float * ex, size_t e1, size_t e2, const floa
     out[(size_t) t * o1 + row] = acc;
 }
 
-int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map) {
+// The combine chain starting at the MUL node i: MUL(experts, weights), the ADDs of its
+// per-slot views [, ADD(residual)], with every alias check the fused launches need.
+// Returns the index of its last node (0: no match).
+struct CombineMatch {
+    ggml_tensor * mul = nullptr, * out = nullptr;
+    const ggml_tensor * ex = nullptr, * w = nullptr;
+    const float * res = nullptr; size_t r1 = 0;
+    bool mul_needed = false;
+    int M = 0, n_used = 0, n_tok = 0;
+};
+static int match_moe_combine(ggml_cgraph * g, int i, const UseCount & use_map, CombineMatch & m) {
     auto uses = [&](const ggml_tensor * t) { auto it = use_map.find(t); return it == use_map.end() ? 0 : it->second; };
     ggml_tensor * mul = g->nodes[i];
     if (mul->op != GGML_OP_MUL || mul->type != GGML_TYPE_F32) return 0;
@@ -558,15 +664,72 @@ int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map
         if (!chain_alias_ok(regs, 4, n_tok == 1)) return 0;
         if (!chain_alias_ok(wr, 3, false) || (wr[1].p && wr[1].p == wr[0].p) || wr[2].p == wr[0].p) return 0;
     }
+    m.mul = mul; m.out = out; m.ex = ex; m.w = w; m.res = res; m.r1 = r1; m.mul_needed = mul_needed;
+    m.M = M; m.n_used = n_used; m.n_tok = n_tok;
+    return last;
+}
+
+int fuse_moe_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map) {
+    CombineMatch m;
+    const int last = match_moe_combine(g, i, use_map, m);
+    if (!last) return 0;
     for (int j = i; j <= last; ++j) {
         deferred_guard_node_ext(c, g->nodes[j]);
         act_cache_invalidate(c.s, g->nodes[j]);
     }
-    MX_KLOG("moe_combine M=%d n_used=%d n_tok=%d res=%d", M, n_used, n_tok, res != nullptr);
-    const dim3 grid((unsigned) mx_ceil_div(M, 256), (unsigned) n_tok);
+    const ggml_tensor * ex = m.ex, * w = m.w;
+    MX_KLOG("moe_combine M=%d n_used=%d n_tok=%d res=%d", m.M, m.n_used, m.n_tok, m.res != nullptr);
+    const dim3 grid((unsigned) mx_ceil_div(m.M, 256), (unsigned) m.n_tok);
     k_moe_combine<<<grid, 256, 0, c.st>>>((const float *) ex->data, ex->nb[1] / 4, ex->nb[2] / 4, (const float *) w->data,
-                                          w->nb[1] / 4, w->nb[2] / 4, n_used, res, r1, mul_needed ? (float *) mul->data : nullptr,
-                                          (float *) out->data, out->nb[1] / 4, M);
+                                          w->nb[1] / 4, w->nb[2] / 4, m.n_used, m.res, m.r1,
+                                          m.mul_needed ? (float *) m.mul->data : nullptr, (float *) m.out->data, m.out->nb[1] / 4, m.M);
+    return last - i + 1;
+}
+
+// Round 6: the down projection's MUL_MAT_ID at node i together with the combine chain that
+// follows it (moe_down_combine_launch, ops_gemv_nc.hip): the experts' outputs are never
+// written, so nothing else may read them (the MUL is their only consumer and needs no
+// output of its own). GGML_MI355X_NO_MOE_DOWN_COMBINE=1: the two launches (A/B).
+int fuse_moe_down_combine(OpCtx & c, ggml_cgraph * g, int i, const UseCount & use_map) {
+    static const bool off = getenv("GGML_MI355X_NO_MOE_DOWN_COMBINE") != nullptr;
+    auto uses = [&](const ggml_tensor * t) { auto it = use_map.find(t); return it == use_map.end() ? 0 : it->second; };
+    ggml_tensor * dst = g->nodes[i];
+    if (off || dst->op != GGML_OP_MUL_MAT_ID || uses(dst) != 1 || (dst->flags & GGML_TENSOR_FLAG_OUTPUT)) return 0;
+    int j = i + 1;
+    while (j < g->n_nodes && (g->nodes[j]->op == GGML_OP_VIEW || g->nodes[j]->op == GGML_OP_RESHAPE)) ++j;
+    if (j >= g->n_nodes || g->nodes[j]->op != GGML_OP_MUL || g->nodes[j]->src[0] != dst) return 0;
+    CombineMatch m;
+    const int last = match_moe_combine(g, j, use_map, m);
+    if (!last || m.mul_needed || m.ex != dst) return 0;
+    const ggml_tensor * as = dst->src[0], * b = dst->src[1], * ids = dst->src[2];
+    const int64_t K = as->ne[0];
+    if (as->ne[3] != 1 || as->nb[0] != (size_t) mx_type(as->type).size || b->type != GGML_TYPE_F32 || ids->type != GGML_TYPE_I32) return 0;
+    if (!moe_down_combine_ok(as->type, K, as->ne[1], m.n_used, m.n_tok)) return 0;
+    if (b->ne[0] != K || b->ne[1] != m.n_used || b->ne[2] != m.n_tok || !mx_is_contiguous(b)) return 0;
+    if (ids->ne[0] != m.n_used || ids->ne[1] != m.n_tok || dst->ne[0] != as->ne[1]) return 0;
+    // the combined output is written while ids, the weights, b and its q8 copy are read
+    for (const ggml_tensor * in : {b, ids, m.w})
+        if (t_overlaps_ext(m.out, in)) return 0;
+    ActQ a{};
+    if (const ActQ * q = act_cache_find(c.s, b)) a = *q;
+    if (!a.q || a.kp != K) {
+        if (!mmvq_type_ok(as->type)) return 0;
+        a = quantize_activations(c, b);   // (the SwiGLU's q8 copy is normally in the act cache)
+    }
+    if (a.kp != K) return 0;
+    for (int k = i; k <= last; ++k) {
+        deferred_guard_node_ext(c, g->nodes[k]);
+        if (k != i) act_cache_invalidate(c.s, g->nodes[k]);
+    }
+    MoeDownComb d{};
+    d.as = as;
+    d.ids = (const char *) ids->data; d.id0 = ids->nb[0]; d.id1 = ids->nb[1];
+    d.q = a.q; d.qd = a.d; d.qs = a.s; d.kp = a.kp;
+    d.wt = (const float *) m.w->data; d.wt1 = m.w->nb[1] / 4; d.wt2 = m.w->nb[2] / 4;
+    d.res = m.res; d.r1 = m.r1;
+    d.out = (float *) m.out->data; d.o1 = m.out->nb[1] / 4;
+    d.n_used = m.n_used; d.n_tok = m.n_tok;
+    moe_down_combine_launch(c, d);
     return last - i + 1;
 }
 

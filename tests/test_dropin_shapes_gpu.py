@@ -524,7 +524,19 @@ def test_mixtral_width_moe(mixtral, tmp_path):
     qkv = [ln for ln in klog_i if ln.startswith("qkv ")]
     assert len(qkv) == 2 * len(t2) and all("qta=13 qtk=8 qtv=8" in ln for ln in qkv), (qkv[:4], klog_i[:20])
     # round 5: norm + router + top-k of every decoded token's MoE block in one launch
-    assert sum(ln.startswith("moe_router ") for ln in klog_i) == 2 * len(t2), [l for l in klog_i if "moe" in l][:8]
+    # (round 6: Mixtral's 8 experts take the one-workgroup form, k_moe_router1)
+    assert sum(ln.startswith("moe_router1 ") for ln in klog_i) == 2 * len(t2), [l for l in klog_i if "moe" in l][:8]
+    # round 6: the down projection's MUL_MAT_ID + the expert combine (+ residual) in one launch
+    # per layer; its per-row dots run the unfused GEMV's lane order, so the logits equal the
+    # two-launch form's (GGML_MI355X_NO_MOE_DOWN_COMBINE=1)
+    assert sum(ln.startswith("moe_down_comb ") and "res=1" in ln for ln in klog_i) == 2 * len(t2), \
+        [l for l in klog_i if "moe" in l][:8]
+    assert not any(ln.startswith("moe_combine ") for ln in klog_i), [l for l in klog_i if "moe" in l][:8]
+    gpu_u, _, klog_u = run_ref(tmp_path, mixtral, t2, 99, 1, incremental=True, tag="iu",
+                               env_extra={"GGML_MI355X_DISABLE_GRAPHS": "1", "GGML_MI355X_NO_MOE_DOWN_COMBINE": "1"})
+    assert sum(ln.startswith("moe_combine ") for ln in klog_u) == 2 * len(t2), [l for l in klog_u if "moe" in l][:8]
+    du = [nmse(gpu_u[i], gpu_i[i]) for i in range(len(t2))]
+    assert max(du) < 1e-9, du
 
 
 def test_runner_launch_mix_equals_dropin(pkg, backend, l8b, tmp_path):

@@ -884,13 +884,16 @@ def test_attn_split_oproj_decode(pkg, backend, orc, kind, n_kv, H, Hkv, M, wt, m
     assert nmse(y, y3) < 1e-5, nmse(y, y3)
 
 
+@pytest.mark.parametrize("per_expert", [False, True])
 @pytest.mark.parametrize("n_exp,E,wtype,knorm", [(8, 4096, "f32", True), (8, 4096, "f16", True), (4, 256, "f32", False),
-                                                 (16, 1024, "f32", True), (8, 6144, "f32", True)])
-def test_moe_router_head_fusion(pkg, backend, orc, n_exp, E, wtype, knorm):
+                                                 (16, 1024, "f32", True), (8, 6144, "f32", True), (8, 6144, "f16", False)])
+def test_moe_router_head_fusion(pkg, backend, orc, n_exp, E, wtype, knorm, per_expert):
     """Round 5: the MoE block's head of one decoded token — RMS_NORM -> MUL(ffn_norm) ->
     MUL_MAT(router) -> SOFT_MAX -> ARGSORT -> top-k GET_ROWS [-> SUM_ROWS -> CLAMP -> DIV] —
-    as ONE k_moe_router launch (ops_moe.hip fuse_moe_router), every node's output checked
-    against numpy, and against the node-by-node launches (g_tune[34] = 1)"""
+    as ONE launch (ops_moe.hip fuse_moe_router), every node's output checked against numpy,
+    and against the node-by-node launches (g_tune[34] = 1). Round 6: <= 8 experts run the
+    single 1024-thread workgroup k_moe_router1; per_expert (g_tune[46] = 1) the round-5 one
+    workgroup per expert with the last-arriver top-k"""
     rng = np.random.default_rng(7 + n_exp + E)
     k = 2
     x = rng.standard_normal((1, E)).astype(np.float32)
@@ -918,16 +921,21 @@ def test_moe_router_head_fusion(pkg, backend, orc, n_exp, E, wtype, knorm):
         return outs, [(tx, x), (tn, nw), (tw, wr_feed)]
 
     lib = pkg._lib.load()
-    backend.klog(True)
-    res = run(pkg, backend, build)
-    log = backend.klog_read()
-    backend.klog(False)
+    lib.ggml_backend_mi355x_set_tune(46, int(per_expert))
+    try:
+        backend.klog(True)
+        res = run(pkg, backend, build)
+        log = backend.klog_read()
+        backend.klog(False)
+    finally:
+        lib.ggml_backend_mi355x_set_tune(46, 0)
     lib.ggml_backend_mi355x_set_tune(34, 1)
     try:
         res_u = run(pkg, backend, build)
     finally:
         lib.ggml_backend_mi355x_set_tune(34, 0)
-    assert any(ln.startswith("moe_router ") for ln in log), log
+    one = not per_expert and n_exp <= 8 and E % 128 == 0 and E <= 8192
+    assert any(ln.startswith("moe_router1 " if one else "moe_router ") for ln in log), log
     cur_ref = orc.rms_norm(x, 1e-5) * nw
     assert nmse(res[0].reshape(1, E), cur_ref) < 1e-7
     lg_ref = (cur_ref.astype(np.float64) @ wr_ref.T.astype(np.float64))[0]
