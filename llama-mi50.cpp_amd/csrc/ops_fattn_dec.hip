@@ -717,6 +717,14 @@ void fa_dec2_run(OpCtx & c, ggml_tensor * dst) {
             FS(2, 1) FS(2, 2) FS(4, 1) FS(4, 2) FS(4, 4) FS(16, 1) FS(16, 2) FS(16, 4)
 #undef FS
         }
+        if (ni == 16 && kv != 0 && D == 128 && f.G == 2) {   // sweep: 16 key rows per lane, quantised caches
+            fd_kv_dispatch(kv, [&](auto KVC) { k_fattn_dec2<128, 2, 4, decltype(KVC)::value, 16, true><<<grid, 256, 0, c.st>>>(a); });
+            k_fattn_dec2_combine<128, 2><<<gc, 256, lds, c.st>>>(a);
+            return;
+        }
+        // fd_cfg sized the splits for `ni` keys rows per lane: a kernel of another NI would
+        // cover only part of the cache (a sweep knob outside the instantiated set)
+        MX_ASSERT(ni == FD_LONG_NI);
 #define CPW4(DD, GG) FLC(DD, GG, 2) else FLC(DD, GG, 4) else FLC(DD, GG, 8) else FLC(DD, GG, 1)
         FLW(128, 1, CPW4(128, 1)) FLW(128, 2, CPW4(128, 2)) FLW(128, 4, FLC(128, 4, 1))
         FLW(64, 1, CPW4(64, 1)) FLW(64, 2, CPW4(64, 2)) FLW(64, 4, FLC(64, 4, 1))

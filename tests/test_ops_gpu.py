@@ -565,6 +565,44 @@ def test_flash_attn_mixed_kv_types(pkg, backend, orc, kt, vt, n_q, n_kv, H, Hkv,
         assert any(ln.startswith("fa_mma") for ln in log), log
 
 
+@pytest.mark.parametrize("ni", [0, 16])
+@pytest.mark.parametrize("kt,vt", [("q8_0", "q8_0"), ("q8_0", "f16")])
+def test_flash_attn_long_quantised_geometry(pkg, backend, orc, kt, vt, ni):
+    """Decode attention over a long quantised cache (the LONG split geometry + combine) at the
+    default keys rows per lane and at 16 (g_tune[28], the geometry swept for q8_0 caches in
+    round 6): the splits must cover every key whichever NI the launch uses"""
+    from qgen import KV_TYPES, kv_rows
+    n_q, n_kv, H, Hkv, D = 1, 6000, 32, 8, 128
+    rng = np.random.default_rng(n_kv + 31 * ni + len(vt))
+    q = rng.standard_normal((H, n_q, D)).astype(np.float32)
+    k = kv_rows(kt, Hkv, n_kv, D, rng, orc)
+    v = kv_rows(vt, Hkv, n_kv, D, rng, orc)
+    mask = np.zeros((n_q, n_kv), np.float32)
+    mask[:, -17:] = -np.inf                       # the tail past the "current" token masked
+    m16 = mask.astype(np.float16).view(np.uint16)
+    scale = 1.0 / np.sqrt(D)
+
+    def build(ctx):
+        tq = ctx.new_tensor("f32", D, n_q, H)
+        tk = ctx.new_tensor(KV_TYPES[kt], D, n_kv, Hkv)
+        tv = ctx.new_tensor(KV_TYPES[vt], D, n_kv, Hkv)
+        tm = ctx.new_tensor("f16", n_kv, n_q)
+        return [ctx.flash_attn_ext(tq, tk, tv, tm, scale, 0.0, 0.0)], [(tq, q), (tk, k), (tv, v), (tm, m16)]
+
+    lib = pkg._lib.load()
+    lib.ggml_backend_mi355x_set_tune(28, ni)
+    try:
+        backend.klog(True)
+        y = run(pkg, backend, build)[0].reshape(n_q, H, D)
+        log = backend.klog_read()
+        backend.klog(False)
+    finally:
+        lib.ggml_backend_mi355x_set_tune(28, 0)
+    ref = orc.flash_attn_t(q, k, v, m16, scale, KV_TYPES[kt], v_type=KV_TYPES[vt])
+    assert nmse(y, ref) < 5e-4, nmse(y, ref)
+    assert any(ln.startswith("fattn_dec2") and "long=1" in ln for ln in log), log
+
+
 def test_mul_mat_id(pkg, backend, orc):
     tid = NAMES["q4_K"]
     rng = np.random.default_rng(8)
