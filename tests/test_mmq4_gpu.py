@@ -232,13 +232,15 @@ def test_mmq5_glu(pkg, backend, orc, M, N, outlier):
 
 
 @pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K", "q8_0"])
-def test_mmq4_moe(pkg, backend, orc, tname):
-    """MUL_MAT_ID prefill: items sorted by expert on the device, ONE k_mmq4 launch of
-    expert-grouped tiles (EPI 2, activation rows gathered, outputs scattered); a skewed
-    routing (expert 3 unused, expert 1 takes most items) and outliers in expert 2"""
+@pytest.mark.parametrize("T", [70, 300])
+def test_mmq4_moe(pkg, backend, orc, tname, T):
+    """MUL_MAT_ID prefill: items sorted by expert on the device, expert-grouped k_mmq4 tiles
+    (EPI 2, activation rows gathered, outputs scattered); a skewed routing (expert 3 unused,
+    expert 1 takes most items) and outliers in expert 2. T 300: full 128-token tiles plus
+    partial last tiles in both the 128- and the 64-token launch (round 6)"""
     tid = NAMES[tname]
-    rng = np.random.default_rng(5 + tid)
-    K, M, E, used, T = 2048, 200, 4, 2, 70
+    rng = np.random.default_rng(5 + tid + T)
+    K, M, E, used = 2048, 200, 4, 2
     parts = [rand_quant(tid, M, K, rng) for _ in range(E)]
     rb = parts[0][1]
     w2, rows_out = with_outliers(parts[2][0], tid, M, K, rng)
@@ -267,15 +269,16 @@ def test_mmq4_moe(pkg, backend, orc, tname):
 
 
 @pytest.mark.parametrize("tname", ["q4_K", "q5_K", "q6_K", "q8_0"])
-def test_mmq4_moe_glu(pkg, backend, orc, tname):
+@pytest.mark.parametrize("T", [70, 300])
+def test_mmq4_moe_glu(pkg, backend, orc, tname, T):
     """MoE prefill gate/up/SwiGLU (llama build_moe_ffn) in ONE k_mmq4 launch (EPI 3): the
     expert-grouped tiles with gate waves and up waves over the same gathered activations,
     silu(g) * u scattered to the GLU output and its f16 copy claimed for the down
     projection's expert GEMM (checked through the down product too); skewed routing,
     outliers in one expert's up rows"""
     tid = NAMES[tname]
-    rng = np.random.default_rng(77 + tid)
-    K, M, Md, E, used, T = 2048, 512, 200, 4, 2, 70
+    rng = np.random.default_rng(77 + tid + T)
+    K, M, Md, E, used = 2048, 512, 200, 4, 2
     wg = [rand_quant(tid, M, K, rng) for _ in range(E)]
     wu = [rand_quant(tid, M, K, rng) for _ in range(E)]
     rb = wg[0][1]
