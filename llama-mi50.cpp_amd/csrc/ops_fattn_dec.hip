@@ -215,6 +215,13 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
         }
         q8 = make_uint2(w0, w1);
     };
+    // the new row concerns only the workgroup whose keys hold it and the one that stores it
+    // (below): the others skip its quantisation (workgroup-uniform)
+    auto nr_mine = [&](int64_t r) {
+        const int cw = LONG ? CPW : cpb;                       // chunks of this workgroup
+        const int64_t lo = (int64_t) split * cw * CS, hi = lo + (int64_t) cw * CS;
+        return (gb == 0 && split == 0 && iq1 == 0 && iq3 == 0) || (r >= lo && r < hi);
+    };
     auto prep = [&]() {
         if constexpr (KQ) {
 #pragma unroll
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
                 }
                 qq8[h][0] = w0; qq8[h][1] = w1;
             }
-            if (p.nr_k) { nrk = nik; nr_quant(nk0, nk1, nkq, nkd); }
+            if (p.nr_k && nr_mine(nik)) { nrk = nik; nr_quant(nk0, nk1, nkq, nkd); }
         } else {
 #pragma unroll
             for (int h = 0; h < G; ++h) {
@@ -242,7 +249,7 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
                 qh[h][2] = h2v{(_Float16) qb[h].x, (_Float16) qb[h].y}; qh[h][3] = h2v{(_Float16) qb[h].z, (_Float16) qb[h].w};
             }
         }
-        if constexpr (VQ) if (p.nr_v) { nrv = niv; nr_quant(nv0, nv1, nvq, nvd); }
+        if constexpr (VQ) if (p.nr_v && nr_mine(niv)) { nrv = niv; nr_quant(nv0, nv1, nvq, nvd); }
     };
     // running (max, sum, O) of this wave; O not yet reduced over the wave's key rows
     float M[G], L[G], o[G][8];
@@ -340,9 +347,10 @@ __global__ __launch_bounds__(64 * NW) void k_fattn_dec2(FaDecArgs p) {
                     const bool isnv = key0 + t * KPI == nrv;
                     const float dv = h2f(isnv ? nvd : b.vd[t]);
                     const uint32_t vw[2] = {isnv ? nvq.x : b.vr[t].x, isnv ? nvq.y : b.vr[t].y};
+                    const float pdv = pr[t] * dv;     // (the block scale folded into the weight)
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
-                        o[h][i] += pr[t] * (dv * (float) (int8_t) ((vw[i >> 2] >> (8 * (i & 3))) & 0xFF));
+                        o[h][i] += pdv * (float) (int8_t) ((vw[i >> 2] >> (8 * (i & 3))) & 0xFF);
                 } else {
                     const uint32_t vw[4] = {b.vr[t].x, b.vr[t].y, b.vr[t].z, b.vr[t].w};
 #pragma unroll
