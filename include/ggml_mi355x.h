@@ -40,6 +40,10 @@ ggml_backend_buffer_type_t ggml_backend_mi355x_buffer_type(int device);
 /* Executor counters: [graph_compute calls, HIP-graph replays, nodes run, nodes fused]. */
 void ggml_backend_mi355x_stats(ggml_backend_t backend, uint64_t out[4]);
 
+/* Staged small writes of one device: [writes staged, flush launches, queued writes dropped
+   because their buffer was freed before a flush]. */
+void ggml_backend_mi355x_stage_stats(int device, uint64_t out[3]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,7 @@ struct Staging {
     std::vector<StageEntry> queued;   // in the ring, not yet copied
     uint64_t n = 0;                // staged writes (GGML_MI355X_STATS)
     uint64_t n_flush = 0;          // flush launches
+    uint64_t n_dropped = 0;        // queued writes dropped because their buffer was freed
 };
 static Staging g_stage[MX_MAX_DEVICES];
 static bool env_flag(const char * name) { const char * v = getenv(name); return v && *v && strcmp(v, "0") != 0; }
@@ -163,9 +164,11 @@ static void stage_release_range(int dev, const char * lo, const char * hi) {
     if (dev < 0 || dev >= MX_MAX_DEVICES) return;
     Staging & st = g_stage[dev];
     std::lock_guard<std::mutex> lk(st.mu);
+    const size_t n0 = st.queued.size();
     st.queued.erase(std::remove_if(st.queued.begin(), st.queued.end(),
                                    [&](const StageEntry & e) { return e.dst >= lo && e.dst + e.n <= hi; }),
                     st.queued.end());
+    st.n_dropped += n0 - st.queued.size();
     bool overlap = false;   // (a range straddling the buffer's edge: flush it, it writes a neighbour too)
     for (const StageEntry & e : st.queued) overlap |= e.dst < hi && lo < e.dst + e.n;
     if (overlap) stage_flush_locked(st);
@@ -353,6 +356,7 @@ static void be_free(ggml_backend_t b) {
     if (s->rope_tab) hipFree(s->rope_tab);
     if (s->fa_cnt) hipFree(s->fa_cnt);
     if (s->kvq8_stage) hipFree(s->kvq8_stage);
+    if (s->mask16) hipFree(s->mask16);
     if (s->cpy_ev) hipEventDestroy(s->cpy_ev);
     hipStreamDestroy(s->stream);
     delete s;  // the ggml_backend struct lives inside Stream
@@ -758,6 +762,14 @@ ggml_backend_buffer_type_t ggml_backend_mi355x_buffer_type(int device) {
 void ggml_backend_mi355x_stats(ggml_backend_t b, uint64_t out[4]) {
     mx::Stream * s = mx::stream_of(b);
     out[0] = s->n_graph_compute; out[1] = s->n_graph_replay; out[2] = s->n_nodes_run; out[3] = s->n_fused;
+}
+
+void ggml_backend_mi355x_stage_stats(int device, uint64_t out[3]) {
+    out[0] = out[1] = out[2] = 0;
+    if (device < 0 || device >= mx::MX_MAX_DEVICES) return;
+    mx::Staging & st = mx::g_stage[device];
+    std::lock_guard<std::mutex> lk(st.mu);
+    out[0] = st.n; out[1] = st.n_flush; out[2] = st.n_dropped;
 }
 
 }  // extern "C"

@@ -66,6 +66,7 @@ constexpr int kFlushMax = 16;                  // ranges per flush launch
 constexpr uint32_t kFlushChunk = 4096;
 struct StageFlushArgs { StageEntry e[kFlushMax]; int n; };
 void stage_flush_launch(const StageFlushArgs & a, unsigned chunks, hipStream_t st);
+void exec_bump_buf_gen();   // exec.cpp: captured graphs re-capture before their next replay
 
 struct ActQ {
     const int8_t * q;    // [ncols][kp]
@@ -160,6 +161,11 @@ struct Stream {
     bool gpf_armed = false;                   // set while that node runs
     size_t gpf_off = 0, gpf_take = 0;
     bool rope_valid = false;
+    // -fa 0 prefill (round 6): the f16 copy of the graph's f32 KQ mask, converted by the first
+    // layer's attention and reused by the others of the same graph pass (every layer reads the
+    // same input mask); valid while mask16_src matches (reset at each pass)
+    uint16_t * mask16 = nullptr; size_t mask16_cap = 0;
+    const void * mask16_src = nullptr; int64_t mask16_key[3] = {0, 0, 0};
     const void * rope_pos = nullptr, * rope_ff = nullptr;
     int32_t rope_params[11] = {};
     bool use_graphs = true;

@@ -638,6 +638,7 @@ static void fa_prefetch_plan(Stream * s, ggml_cgraph * g, int i, int64_t n_q, bo
 // row-split slices ran on other streams (their buffers are not the capturing stream's)
 // must not replay over freed memory
 static std::atomic<unsigned> g_buf_gen{0};
+void exec_bump_buf_gen() { ++g_buf_gen; }   // a stream buffer a capture may reference moved (ops_fattn_mma.hip mask16)
 
 // row split: MUL_MATs right after node i (views between) that share its src1 and whose
 // split weights have the same non-empty slices, all reachable directly: run as one group
@@ -694,6 +695,7 @@ static void run_nodes(Stream * s, ggml_cgraph * g) {
     act_cache_reset(s);
     s->deferred.clear();
     s->rope_valid = false;
+    s->mask16_src = nullptr;
     s->kvnew.on = false;
     static thread_local std::unordered_map<const ggml_tensor *, int> done;   // run ahead by a group
     done.clear();

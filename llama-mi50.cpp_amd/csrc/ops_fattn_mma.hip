@@ -694,9 +694,31 @@ void fa_mma_nofa_launch(OpCtx & c, const ggml_tensor * q, const ggml_tensor * k,
     p.scale = scale;
     if (m) {
         if (m->type == GGML_TYPE_F32) {
-            uint16_t * m16 = (uint16_t *) c.scratch->take((size_t) p.n_kv * p.n_q * 2);
-            k_mask_to_f16<<<dim3((unsigned) mx_ceil_div(p.n_kv / 4, 256), (unsigned) p.n_q), 256, 0, c.st>>>(
-                (const char *) m->data, m->nb[1], p.n_kv, p.n_q, m16);
+            // round 6: converted once per graph pass — every layer's chain reads the same input
+            // mask (the per-layer conversion was 32 x 4.8 us per pp2048 ubatch, profiles/r06/)
+            Stream * s = c.s;
+            const size_t bytes = (size_t) p.n_kv * p.n_q * 2;
+            const int64_t key[3] = {(int64_t) p.n_kv, (int64_t) p.n_q, (int64_t) m->nb[1]};
+            uint16_t * m16 = nullptr;
+            static const bool no_cache = getenv("GGML_MI355X_NO_MASK_CACHE") != nullptr;   // A/B: per layer
+            if (!no_cache && s->mask16_src == m->data && !memcmp(s->mask16_key, key, sizeof(key))) {
+                m16 = s->mask16;
+            } else {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                HIP_CHECK(hipStreamIsCapturing(c.st, &cs));
+                if (!no_cache && bytes > s->mask16_cap && cs == hipStreamCaptureStatusNone) {   // (grown in an eager pass only)
+                    HIP_CHECK(hipStreamSynchronize(c.st));
+                    if (s->mask16) { HIP_CHECK(hipFree(s->mask16)); exec_bump_buf_gen(); }   // (captures hold the old one)
+                    HIP_CHECK(hipMalloc((void **) &s->mask16, bytes));
+                    s->mask16_cap = bytes;
+                }
+                const bool keep = !no_cache && bytes <= s->mask16_cap;
+                m16 = keep ? s->mask16 : (uint16_t *) c.scratch->take(bytes);
+                k_mask_to_f16<<<dim3((unsigned) mx_ceil_div(p.n_kv / 4, 256), (unsigned) p.n_q), 256, 0, c.st>>>(
+                    (const char *) m->data, m->nb[1], p.n_kv, p.n_q, m16);
+                s->mask16_src = keep ? m->data : nullptr;
+                memcpy(s->mask16_key, key, sizeof(key));
+            }
             p.mask = (const char *) m16; p.m1 = (size_t) p.n_kv * 2;
         } else {
             p.mask = (const char *) m->data; p.m1 = m->nb[1];

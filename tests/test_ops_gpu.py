@@ -603,6 +603,37 @@ def test_flash_attn_long_quantised_geometry(pkg, backend, orc, kt, vt, ni):
     assert any(ln.startswith("fattn_dec2") and "long=1" in ln for ln in log), log
 
 
+def test_staged_write_dropped_when_buffer_freed(pkg, backend):
+    """a small write is only queued (staged into the pinned ring, copied by the next
+    flush). If its buffer is freed before that flush, the queued copy must be dropped — else
+    it lands in freed memory or in the next allocation at that address. Write, free, reallocate
+    the same size many times (hipMalloc hands the address back), write the new owner through a
+    path that bypasses the queue (larger than a staged write), and read it back."""
+    import ctypes
+    lib = pkg._lib.load()
+    st = (ctypes.c_uint64 * 3)()
+    lib.ggml_backend_mi355x_stage_stats(0, st)
+    dropped0 = st[2]
+    n = (5 << 20) // 4                                  # 5 MB: above the 4 MB staging limit
+    big = np.arange(n, dtype=np.float32)
+    for trial in range(6):
+        c1 = pkg.Context()
+        a = c1.new_tensor("f32", n)
+        c1.alloc(backend)
+        # a staged write into a's buffer: the first 64 KB
+        lib.mxg_tensor_set(a.ptr, np.full(16384, -1.0, np.float32).ctypes.data, 0, 65536)
+        c1.free()                                       # freed with that write still queued
+        c2 = pkg.Context()
+        b = c2.new_tensor("f32", n)
+        c2.alloc(backend)
+        b.set(big)                                      # direct copy (not staged)
+        got = b.numpy().reshape(-1)
+        c2.free()
+        assert np.array_equal(got, big), (trial, got[:4])
+    lib.ggml_backend_mi355x_stage_stats(0, st)
+    assert st[2] >= dropped0 + 6, (dropped0, list(st))
+
+
 def test_mul_mat_id(pkg, backend, orc):
     tid = NAMES["q4_K"]
     rng = np.random.default_rng(8)
