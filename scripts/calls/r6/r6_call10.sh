@@ -1,5 +1,5 @@
 #!/bin/bash
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 P="type_a=(q4_0|q8_0|q4_K|q6_K),type_b=f32,m=4096,n=(1|2|3|4|5|8),k=14336"
 bash scripts/r6.sh "tests tests/test_ops_gpu.py tests/test_dropin_shapes_gpu.py -k mul_mat+or+mixtral" && \
 bash scripts/r6.sh "tbo perf_mm_v3 perf -b MI355X0 -o MUL_MAT -p $P" && \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # LDS activation-chunk permutation (act_swz) A/B + down-projection geometry sweep
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/r6
 NS=$PWD/llama-mi50.cpp_amd/lib/noswz/libggml-mi355x.so
 P="type_a=(q4_0|q8_0|q4_K|q5_K|q6_K),type_b=f32,m=4096,n=(1|2|3|4|5|6|7|8),k=14336"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # MoE router in one 1024-thread workgroup: parity, Mixtral tg128 A/B, profile
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/r6
 bash scripts/r6.sh "tests tests/test_ops_gpu.py -k moe" "tests tests/test_dropin_gpu.py -k tiny_moe" "tests tests/test_dropin_shapes_gpu.py -k mixtral" && \
 MODEL=mixtral_2l RECIPE=q5_k_m bash scripts/r6.sh "prof prof_mx2l_tg_r1 -fa 1 -p 0 -n 64 -c 256 -r 1" && \

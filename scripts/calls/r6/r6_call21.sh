@@ -1,6 +1,6 @@
 #!/bin/bash
 # LONG-geometry keys per lane (g_tune[28] = 16 vs the default) across depths and cache types
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/r6
 steps=()
 for d in 4096 8192 16384; do

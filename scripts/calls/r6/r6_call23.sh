@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters of the decode attention at depth 8192 (LONG geometry): f16 vs q8_0 caches
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/r6
 G=$(python -c "import bench; print(bench.bench_gguf())") || exit 1
 export GGML_BACKEND_PATH=$PWD/llama-mi50.cpp_amd/lib/libggml-mi355x.so

@@ -1,6 +1,6 @@
 #!/bin/bash
 # q8_0 decode attention: new-row quantisation only where needed, V scale folded — parity + same-box A/B
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/r6
 B=$PWD/llama-mi50.cpp_amd/lib/base/libggml-mi355x.so
 bash scripts/r6.sh "tests tests/test_ops_gpu.py -k flash_attn" "tests tests/test_dropin_gpu.py -k q8+or+mixed+or+incremental+or+kv_state" \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # -fa 0 prefill: the f16 mask converted once per graph pass — parity + same-box A/B
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/r6
 bash scripts/r6.sh "tests tests/test_ops_gpu.py -k nofa+or+staged" "tests tests/test_dropin_gpu.py -k prefill+or+incremental+or+layer_split" \
   "tests tests/test_dropin_shapes_gpu.py -k pp512+or+pp2048+or+prefill" || exit 1

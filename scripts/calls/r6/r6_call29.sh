@@ -1,6 +1,6 @@
 #!/bin/bash
 # prefill Q6_K dequantisation as one packed FMA per pair — parity + same-box A/B + profile
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/r6
 B=$PWD/llama-mi50.cpp_amd/lib/base/libggml-mi355x.so
 bash scripts/r6.sh "tests tests/test_mmq4_gpu.py" "tests tests/test_ops_gpu.py -k mul_mat_quant_prefill+or+grouped+or+mul_mat_quant" \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 6: attribution of the decode attention's new-row cost (GGML_MI355X_KVNEW_DBG, timing only)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 for dbg in 0 1 2; do
   GGML_MI355X_KVNEW_DBG=$dbg OUT=gpurun_out/r6 bash scripts/r6.sh "prof prof_kvnew_dbg$dbg -fa 1 -p 0 -n 128 -c 256 -r 1 -ctk 8" > gpurun_out/r6/kvnew_dbg$dbg.txt 2>&1 || exit $?
   echo "dbg=$dbg $(grep -h 'k_fattn_dec2' gpurun_out/r6/prof_kvnew_dbg${dbg}_kernel_stats.csv)"
