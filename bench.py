@@ -133,7 +133,7 @@ def roofline_glu(pkg, be, model, iters=256):
     traffic, traffic_src = None, None
     # scripts/pmc_roofline.sh (separate FETCH_SIZE / WRITE_SIZE passes of --roofline-only):
     # the newest round's counter file for this exact launch
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         pmc = os.path.join(ROOT, "profiles", rnd, "pmc_glu.json")
         if not os.path.exists(pmc):
             continue
