@@ -95,15 +95,28 @@ __global__ __launch_bounds__(256) void k_gemv_nc(GncArgs p) {
     }
 }
 
-template <int QT, int NC>
-static void gnc_launch(OpCtx & c, const GncArgs & p) {
-    // 16 lanes x 4 units per row (Q6_K: 2 units, its unit holds 5 loads), 16 rows per workgroup
-    constexpr int LPR = 16, UPL = QT == GGML_TYPE_Q6_K ? 2 : 4;
+template <int QT, int NC, int LPR>
+static void gnc_launch_l(OpCtx & c, const GncArgs & p) {
+    constexpr int UPL = QT == GGML_TYPE_Q6_K ? 2 : 4;
     constexpr int RPB = 4 * (64 / LPR);
     const size_t lds = gnc_lds_bytes(NC, p.K);
     if (lds > 65536) MX_LDS_OPTIN((k_gemv_nc<QT, LPR, UPL, NC>), 160 * 1024);
-    MX_KLOG("gemv_nc qt=%d nc=%d ncols=%d K=%d M=%d lds=%zu", QT, NC, p.ncols, p.K, p.nrows, lds);
+    MX_KLOG("gemv_nc qt=%d nc=%d ncols=%d K=%d M=%d lds=%zu lpr=%d", QT, NC, p.ncols, p.K, p.nrows, lds, LPR);
     k_gemv_nc<QT, LPR, UPL, NC><<<(unsigned) ((p.nrows + RPB - 1) / RPB), 256, lds, c.st>>>(p);
+}
+
+template <int QT, int NC>
+static void gnc_launch(OpCtx & c, const GncArgs & p) {
+    // 4 units per lane in flight (Q6_K: 2, its unit holds 5 loads). Up to 4 columns: 32 lanes
+    // per row, 8 rows per workgroup — twice the workgroups of 16-row tiles, and their LDS images
+    // still fit two or more per CU (the waves waited 0.55 of their time at one per SIMD,
+    // pmc_gnc_sq.json); 6 / 8 columns: 16 lanes x 16 rows (at 72-143 KB of LDS per workgroup
+    // smaller tiles only add staging). Test-backend-ops perf, 4096 x bs x 14336, same box
+    // (profiles/r06/multicolumn_gemv_table.txt): Q4_K bs 2 9.1 -> 7.7 us, bs 4 14.2 -> 12.2, bs 8
+    // 24.8 -> 30.7 with 8-row tiles. g_tune[47] = 16 / 32 forces one geometry (sweeps).
+    if (g_tune[47] == 16) return gnc_launch_l<QT, NC, 16>(c, p);
+    if (g_tune[47] == 32 || NC <= 4) return gnc_launch_l<QT, NC, 32>(c, p);
+    gnc_launch_l<QT, NC, 16>(c, p);
 }
 
 template <int QT>
