@@ -971,6 +971,8 @@ void graph_compute_impl(Stream * s, ggml_cgraph * g, ggml_status * status) {
         hipGraph_t graph = nullptr;
         HIP_CHECK(hipStreamEndCapture(s->stream, &graph));
         HIP_CHECK(hipGraphInstantiate(&gc.exec, graph, nullptr, nullptr, 0));
+        static const bool upload = getenv("GGML_MI355X_GRAPH_UPLOAD") != nullptr;
+        if (upload) HIP_CHECK(hipGraphUpload(gc.exec, s->stream));
         gc.graph = graph;
         gc.buf_gen = g_buf_gen.load();
         return;
